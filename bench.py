@@ -1,0 +1,250 @@
+"""bench.py — leapfrog-steps/s (all chains) + ESS/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], SURVEY §8d "Large"): hierarchical Normal,
+D = 1000 parameters (theta[997], mu, tau, sigma), N = 100,000 observations,
+HMC with L = 20 leapfrog steps, 256 chains per GPU (configs[3] at N = 8: 2048
+chains, 256/GPU, RCCL gather of the samples).  One *step* = one HMC iteration
+of every chain on the GPU = one launch of the persistent kernel k_hmc
+(L leapfrog steps, fused gradient tape, accept, sample store).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Warmup W = untimed warmup iterations of the sampler (step-size adaptation);
+K timed sampling iterations, each its own launch, bracketed by barrier +
+synchronize; value = sum over ranks of chain-leapfrog-steps / max-over-ranks
+wall time.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "leapfrog-steps/sec (all chains) + ESS/sec, 1000-dim Gaussian @1/2/4/8 GPUs"
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = f32-MFMA peak
+HBM_PEAK_GBS = 8000.0
+
+
+def _ensure_pkg():
+    import __graft_entry__ as ge
+
+    return ge._ensure_pkg()
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--shape", default="large", choices=["small", "medium", "large"])
+    ap.add_argument("--chains", type=int, default=256, help="chains per GPU")
+    ap.add_argument("--leapfrog", type=int, default=20)
+    ap.add_argument("--step-size", type=float, default=0.01)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="budget of the CPU-oracle baseline sample (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ess", action="store_true")
+    return ap.parse_args()
+
+
+def ess_device(samples, max_lag=100):
+    """Reference compute_ess (examples/06_nuts_comparison.py:22-41) for every
+    (chain, param) series at once, on the device.  samples: [C, S, D]."""
+    import torch
+
+    x = samples.double()
+    n = x.shape[1]
+    mean = x.mean(dim=1, keepdim=True)
+    var = x.var(dim=1, unbiased=False)
+    xc = x - mean
+    acf_sum = torch.zeros_like(var)
+    active = var != 0
+    safe = torch.where(active, var, torch.ones_like(var))
+    for lag in range(1, min(n // 2, max_lag)):
+        if not bool(active.any()):
+            break
+        c = (xc[:, :-lag] * xc[:, lag:]).mean(dim=1) / safe
+        acf_sum = torch.where(active, acf_sum + c, acf_sum)
+        active = active & ~(c < 0.05)
+    ess = n / (1.0 + 2.0 * acf_sum)
+    return torch.where(var == 0, torch.full_like(ess, float(n)), ess)   # [C, D]
+
+
+def cpu_baseline(G, N, L, step_size, budget_s):
+    """Time the CPU oracle (reference cost structure) on the same model, 1 chain, 1 thread."""
+    import torch
+
+    import workloads as W
+    from oracle import philox as R
+    from oracle import samplers as S
+
+    torch.set_num_threads(1)
+    lp, init = W.hierarchical(W.ns_oracle(), G, N)
+    M = S.EagerModel(lp, init)
+    q = M.flatten(init)
+    steps = 0
+    iters = 0
+    t0 = time.perf_counter()
+    # one HMC iteration = momentum, L two-gradient leapfrog steps, accept
+    while time.perf_counter() - t0 < budget_s:
+        p = R.momentum(0, 0, iters, M.D)
+        H0 = M.hamiltonian(q, p)
+        qp, pp = q, p
+        for _ in range(L):
+            qp, pp = M.leapfrog(qp, pp, step_size)
+            steps += 1
+        H1 = M.hamiltonian(qp, pp)
+        if R.logf_ref(R.uniform(0, 0, iters, R.TAG_ACCEPT)) < -(H1 - H0):
+            q = qp
+        iters += 1
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "leapfrog-steps/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle/samplers.py HMC restatement (2 gradients per leapfrog step, "
+                       f"torch-CPU autograd), 1 chain, 1 thread, {iters} iterations x L={L} "
+                       f"on the same D={G + 3}, N={N} model, {dt:.1f} s")}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    m = _ensure_pkg()
+    import workloads as W
+    from mlx_mcmc_amd import _engine, _trace
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    G, N = W.SHAPES[args.shape]
+    D = G + 3
+    C = args.chains
+    L = args.leapfrog
+    K = args.steps
+    Wm = args.warmup
+    lp_fn, init = W.hierarchical(W.ns_product(), G, N)
+    prog = _trace.compile_model(lp_fn, init)
+    chains = _engine.ChainSet(prog, C, prog.layout.flatten(init), args.step_size, device=dev)
+    samples = torch.empty((C, max(K, 1), D), dtype=torch.float32, device=dev)
+    cfg = dict(chain_offset=rank * C, num_warmup=Wm, num_samples=K, sample_begin=0,
+               sample_capacity=K, seed=args.seed, step_size=args.step_size,
+               target_accept=0.8, num_leapfrog_steps=L, adapt_step_size=True)
+
+    # ---- untimed warmup (step-size adaptation) -------------------------------
+    if Wm > 0:
+        chains.run_hmc(samples=samples, iter_begin=0, iter_count=Wm, **cfg)
+    torch.cuda.synchronize()
+
+    # ---- timed region: K steps, one launch each --------------------------------
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev[k][0].record(stream)
+        chains.run_hmc(samples=samples, iter_begin=Wm + k, iter_count=1, **cfg)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if K else float("nan")
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    elapsed = float(t_max.item())
+
+    sc = chains.scalars()
+    accept = float(np.mean(sc["n_accept"] / np.maximum(sc["n_total"], 1)))
+    eps = float(np.mean(sc["step_size"]))
+
+    # ---- final sample gather over RCCL (not timed) -----------------------------
+    gather_ms = None
+    all_samples = samples
+    if world > 1:
+        tg = time.perf_counter()
+        bufs = [torch.empty_like(samples) for _ in range(world)] if rank == 0 else None
+        dist.gather(samples, gather_list=bufs, dst=0)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+        if rank == 0:
+            all_samples = torch.cat(bufs, dim=0)
+
+    if rank == 0:
+        total_chains = C * world
+        steps_total = total_chains * L * K
+        value = steps_total / elapsed
+        flops_per_launch = C * L * W.hierarchical_flops_per_step(G, N)
+        achieved = flops_per_launch / (kern_ms * 1e-3) / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get(args.shape, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "leapfrog-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": Wm,
+            "ms_per_step": elapsed * 1e3 / max(K, 1),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (fixed-seed hierarchical Normal data, SURVEY §8d)",
+            "config": {
+                "workload": (f"hierarchical Normal '{args.shape}' HMC (BASELINE configs[2]/[3]): "
+                             f"D={D}, N={N}, L={L}, {C} chains per GPU"),
+                "num_params": D, "num_obs": N, "leapfrog_steps": L, "chains_per_gpu": C,
+                "total_chains": total_chains, "parallelism": f"chains sharded {C}/GPU",
+                "waves_per_chain": prog.waves_per_chain,
+            },
+            "roofline": {
+                "bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
+                "kernel": "k_hmc<16,LDS>", "kernel_ms": kern_ms,
+                "flops_per_launch": flops_per_launch,
+                "note": ("fp32 compute bound (vector FP32 peak = f32-MFMA peak 157.3 TF); "
+                         "F = 5N + 13D flops per chain-leapfrog-step, C*L per launch"),
+            },
+            "accept_rate": accept, "step_size": eps,
+        }
+        if gather_ms is not None:
+            out["gather_ms"] = gather_ms
+        if not args.no_ess and K >= 10:
+            ess = ess_device(all_samples[:, :K, :])           # [C_total, D]
+            ess_sum = ess.sum(dim=0)                          # per param
+            out["ess_per_sec"] = {"min": float(ess_sum.min()) / elapsed,
+                                  "median": float(ess_sum.median()) / elapsed,
+                                  "unit": "effective samples/s (sum over chains)"}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(G, N, L, max(eps, 1e-4), args.cpu_seconds)
+            out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

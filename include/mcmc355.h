@@ -1,0 +1,231 @@
+/*
+ * mcmc355.h — C-ABI of libmcmc355.so, the MI355X (gfx950) HMC / NUTS engine.
+ *
+ * This is the drop-in boundary for the reference's sampling hot path
+ * (korentomas/mlx-mcmc):
+ *
+ *   reference symbol                                   replaced by
+ *   -------------------------------------------------  ------------------------------
+ *   mlx_mcmc/kernels/hmc.py:7-206   hmc()              mc_hmc_run (+ mc_state_init)
+ *   mlx_mcmc/kernels/hmc.py:53-67   grad_log_prob      mc_logp_grad (tape evaluator)
+ *   mlx_mcmc/kernels/hmc.py:69-100  leapfrog_step      (fused inside mc_hmc_run)
+ *   mlx_mcmc/kernels/hmc.py:102-111 hamiltonian        (fused inside mc_hmc_run)
+ *   mlx_mcmc/kernels/hmc.py:113-153 hmc_step           (fused inside mc_hmc_run)
+ *   mlx_mcmc/kernels/nuts.py:16-358 nuts()             mc_nuts_run (+ mc_state_init)
+ *   mlx_mcmc/kernels/nuts.py:137-218 build_tree        (iterative, inside mc_nuts_run)
+ *   mlx_mcmc/kernels/nuts.py:119-135 no_u_turn         (inside mc_nuts_run)
+ *   mlx_mcmc/distributions/normal.py:33-56 log_prob    MC_DIST_NORMAL term / mc_dist_log_prob
+ *   mlx_mcmc/distributions/halfnormal.py:34-63         MC_DIST_HALFNORMAL term / mc_dist_log_prob
+ *   mlx.core.random (key/split/normal/uniform)         Philox4x32-10 counter RNG, mc_rng_fill
+ *
+ * The reference is pure Python on MLX and has no FFI of its own; the
+ * Python host layer of this repository (mlx_mcmc_amd/_lib.py) binds these
+ * symbols with ctypes — see INTEGRATION.md for the binding a maintainer of
+ * the reference would add.
+ *
+ * Conventions
+ *   - All array arguments named *_dev are device pointers (HIP, current
+ *     device); the caller owns them.  The library owns only mc_program.
+ *   - Every entry point returns 0 on success or a negative MC_ERR_* code;
+ *     nothing throws or aborts across the ABI.  mc_last_error() returns a
+ *     thread-local message for the last failure on the calling thread.
+ *   - Launch functions are asynchronous on the given stream and never
+ *     allocate, free or synchronise (they are graph-capturable).
+ *   - Parameters are one flat float32 vector of length n_params (the
+ *     concatenation of the user's parameter dict in insertion order).
+ */
+#ifndef MCMC355_H
+#define MCMC355_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MC_ABI_VERSION 1
+
+/* ---- error codes -------------------------------------------------------- */
+#define MC_OK              0
+#define MC_ERR_INVALID    -1   /* bad argument / malformed program           */
+#define MC_ERR_UNSUPPORTED -2  /* well-formed but outside what the kernels do */
+#define MC_ERR_HIP        -3   /* HIP runtime error                          */
+#define MC_ERR_NOMEM      -4   /* device allocation failed                   */
+
+/* ---- the tape: a log density as a sum of fused distribution terms ------- */
+/* A term is  weight * sum_i dist(loc_i, scale_i).log_prob(value_i)  over n
+ * broadcast elements.  This is exactly the shape every reference model takes
+ * (e.g. tests/test_hmc.py:187-198, examples/02_hmc_comparison.py:40-52).   */
+typedef enum {
+    MC_DIST_NORMAL     = 0,   /* normal.py:33-56      (value, loc, scale)   */
+    MC_DIST_HALFNORMAL = 1    /* halfnormal.py:34-63  (value, scale)        */
+} mc_dist_kind;
+
+typedef enum {
+    MC_OP_NONE    = 0,  /* operand unused (HalfNormal loc)                   */
+    MC_OP_CONST   = 1,  /* broadcast float constant `value`                  */
+    MC_OP_PSCALAR = 2,  /* broadcast parameter q[param_offset]               */
+    MC_OP_DATA    = 3,  /* data[pool_offset + i]        (float32 data pool)  */
+    MC_OP_PVEC    = 4,  /* q[param_offset + i]                               */
+    MC_OP_GATHER  = 5   /* q[param_offset + index[pool_offset + i]] (int32)  */
+} mc_operand_kind;
+
+typedef struct mc_operand {
+    int32_t kind;          /* mc_operand_kind                               */
+    int32_t param_offset;  /* PSCALAR / PVEC / GATHER                       */
+    int64_t pool_offset;   /* DATA: float pool; GATHER: index pool          */
+    float   value;         /* CONST                                         */
+    int32_t reserved;
+} mc_operand;
+
+typedef struct mc_term {
+    int32_t    dist;       /* mc_dist_kind                                  */
+    int32_t    reserved0;
+    int64_t    n;          /* broadcast length (>= 1)                       */
+    float      weight;     /* multiplies the term (1.0 for `lp += term`)    */
+    float      reserved1;
+    mc_operand value, loc, scale;
+} mc_term;
+
+typedef struct mc_program mc_program;
+
+/* Build a program.  data / index are HOST arrays; the library copies them to
+ * the device (and, for terms that gather through an unsorted index, stores a
+ * permuted copy so that every term is processed in index order — this is what
+ * makes the gather gradient a deterministic segmented sum).  Validates every
+ * operand range.  lp_const is added to the total log density.              */
+int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t n_params,
+                      float lp_const,
+                      const float* data, int64_t n_data,
+                      const int32_t* index, int64_t n_index,
+                      mc_program** out);
+int mc_program_destroy(mc_program* prog);
+int32_t mc_program_num_params(const mc_program* prog);
+/* The launch geometry the engine picked: waves per chain (1, 4 or 16).     */
+int32_t mc_program_waves_per_chain(const mc_program* prog);
+
+/* Batched tape evaluation: for every point p, logp[p] = log density at
+ * q[p, :] and grad[p, :] = its gradient (replaces hmc.py:53-67 mx.grad).   */
+int mc_logp_grad(const mc_program* prog, int64_t n_points,
+                 const float* q_dev, float* logp_dev, float* grad_dev,
+                 void* hip_stream);
+
+/* Elementwise Distribution.log_prob (normal.py:33-56, halfnormal.py:34-63):
+ * out[i] = log_prob(value[i]; loc[i|0], scale[i|0]).  loc_dev may be NULL
+ * for HalfNormal.  *_bcast = 1 means the operand is a single element.      */
+int mc_dist_log_prob(int32_t dist, int64_t n,
+                     const float* value_dev, int32_t value_bcast,
+                     const float* loc_dev, int32_t loc_bcast,
+                     const float* scale_dev, int32_t scale_bcast,
+                     float* out_dev, void* hip_stream);
+
+/* ---- per-chain state ---------------------------------------------------- */
+/* State blob layout (device memory, mc_state_bytes(prog, C) bytes):
+ *   [mc_chain_scalars x C][pad to 256 B][q: C x D f32][pad][g: C x D f32]
+ * mc_state_offsets() returns the byte offsets of q and g.                  */
+typedef struct mc_chain_scalars {
+    double  step_size;      /* epsilon (Python float in the reference)      */
+    double  step_size_bar;  /* NUTS dual averaging epsilon_bar (nuts.py:64) */
+    double  h_bar;          /* NUTS dual averaging H_bar (nuts.py:65)       */
+    double  alpha_sum;      /* NUTS: sum of per-iteration accept stats      */
+    float   mu;             /* NUTS: f32 log(10*eps0) (nuts.py:63)          */
+    float   logp;           /* log density at the current position          */
+    int32_t n_accept;       /* accepted (HMC) / alpha>0.5 (NUTS) this phase */
+    int32_t n_total;        /* iterations in this phase                     */
+    int32_t warmup_accept;  /* counters frozen at the warmup->sampling edge */
+    int32_t warmup_total;
+    int64_t depth_sum;      /* NUTS: sum of tree depths this phase          */
+    int64_t warmup_depth_sum;
+    int64_t n_grad;         /* gradient evaluations so far                  */
+    int32_t n_divergent;    /* NUTS: leaves that failed the DELTA_MAX test  */
+    int32_t reserved;
+} mc_chain_scalars;
+
+int64_t mc_state_bytes(const mc_program* prog, int64_t num_chains);
+int mc_state_offsets(const mc_program* prog, int64_t num_chains,
+                     int64_t* q_offset, int64_t* g_offset);
+/* Set q = q0, evaluate logp/grad there, step_size = eps0, counters = 0,
+ * NUTS dual-averaging state = (mu = f32 log(10 eps0), eps_bar = 1, H_bar = 0)
+ * (nuts.py:62-68, hmc.py:157).                                              */
+int mc_state_init(const mc_program* prog, int64_t num_chains,
+                  const float* q0_dev, double step_size,
+                  void* state_dev, void* hip_stream);
+
+/* ---- sampling runs ------------------------------------------------------ */
+/* Iterations are numbered globally: [0, num_warmup) is warmup, then
+ * [num_warmup, num_warmup + num_samples) is sampling.  A launch runs
+ * iterations [iter_begin, iter_begin + iter_count) for every chain, so a run
+ * may be split over several launches (progress printing, bench steps).
+ * Draws are a pure function of (seed, chain_offset + chain, iteration, ...),
+ * so results do not depend on how chains are split over launches or GPUs. */
+typedef struct mc_run_config {
+    int64_t  num_chains;       /* chains in this launch                      */
+    int64_t  chain_offset;     /* global index of chain 0 (RNG stream id)    */
+    int64_t  num_warmup;
+    int64_t  num_samples;
+    int64_t  iter_begin;
+    int64_t  iter_count;
+    int64_t  sample_begin;     /* samples buffer holds sample indices        */
+    int64_t  sample_capacity;  /*   [sample_begin, sample_begin + capacity)  */
+    uint64_t seed;
+    double   step_size;        /* initial epsilon (NUTS mu uses it)          */
+    double   target_accept;
+    int32_t  num_leapfrog_steps; /* HMC L                                    */
+    int32_t  max_tree_depth;     /* NUTS                                     */
+    int32_t  adapt_step_size;
+    int32_t  slice_mode;         /* NUTS: 0 = reference f32 exp/log (Q7),    */
+                                 /*       1 = exact double log u             */
+} mc_run_config;
+
+/* Optional per-(chain, iteration) trace; any pointer may be NULL.
+ * Arrays are [num_chains, capacity] for iterations [iter_begin, +capacity). */
+typedef struct mc_trace {
+    int64_t  iter_begin;
+    int64_t  capacity;
+    uint8_t* accepted;      /* HMC accept bit; NUTS alpha > 0.5             */
+    float*   accept_stat;   /* HMC log-accept ratio; NUTS alpha (nuts.py:287) */
+    double*  step_size;     /* epsilon used in the iteration                */
+    float*   energy;        /* HMC H_init; NUTS H0                          */
+    int32_t* tree_depth;    /* NUTS j; HMC L                                */
+    int32_t* n_leapfrog;    /* leapfrog steps (= new gradient evaluations)  */
+} mc_trace;
+
+/* HMC (hmc.py:7-206).  samples_dev: [num_chains, sample_capacity, D] f32 or
+ * NULL.  workspace: mc_hmc_workspace_bytes() bytes of device memory (may be
+ * 0 bytes when the per-chain arena fits in LDS).                            */
+int64_t mc_hmc_workspace_bytes(const mc_program* prog, int64_t num_chains);
+int mc_hmc_run(const mc_program* prog, const mc_run_config* cfg,
+               void* state_dev, float* samples_dev, const mc_trace* trace,
+               void* workspace_dev, int64_t workspace_bytes, void* hip_stream);
+
+/* NUTS (nuts.py:16-358), iterative tree building, max_tree_depth <= 16.    */
+int64_t mc_nuts_workspace_bytes(const mc_program* prog, int64_t num_chains,
+                                int32_t max_tree_depth);
+int mc_nuts_run(const mc_program* prog, const mc_run_config* cfg,
+                void* state_dev, float* samples_dev, const mc_trace* trace,
+                void* workspace_dev, int64_t workspace_bytes, void* hip_stream);
+
+/* ---- RNG (replaces mx.random for the sampler draws) --------------------- */
+/* Philox4x32-10 (Salmon et al., SC'11).  key = (seed lo, seed hi); counter =
+ * (chain, iteration, tag << 24 | sub, index).  mode 0: raw u32 words
+ * (out is uint32[n*4]); 1: f32 uniforms in (0,1) ((w >> 9) + 0.5) 2^-23;
+ * 2: f32 standard normals, double-precision Box-Muller on word pairs.
+ * Element e uses counter (chain, iteration, tag<<24 | sub, index0 + e).     */
+#define MC_RNG_TAG_MOMENTUM 1
+#define MC_RNG_TAG_ACCEPT   2
+#define MC_RNG_TAG_SLICE    3
+#define MC_RNG_TAG_DEPTH    4
+#define MC_RNG_TAG_MERGE    5
+#define MC_RNG_TAG_USER     16
+int mc_rng_fill(uint64_t seed, uint32_t chain, uint32_t iteration,
+                uint32_t tag, uint32_t sub, uint32_t index0, int64_t n,
+                int32_t mode, void* out_dev, void* hip_stream);
+
+const char* mc_last_error(void);
+int32_t mc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MCMC355_H */

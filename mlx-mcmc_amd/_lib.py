@@ -1,0 +1,211 @@
+"""ctypes binding of libmcmc355.so (include/mcmc355.h).
+
+The library is the product: there is no CPU fallback.  Loading fails loudly
+when the shared object has not been built (``make -C mlx-mcmc_amd/csrc`` or
+``__graft_entry__.build()``) and every sampling entry point raises
+``EngineUnavailable`` when no ROCm device is visible.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.realpath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmcmc355.so")
+
+
+class EngineUnavailable(RuntimeError):
+    """Raised when the HIP engine cannot run (library missing or no GPU)."""
+
+
+class EngineError(RuntimeError):
+    """A negative MC_ERR_* return code from the C-ABI."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"libmcmc355 error {code}: {message}")
+        self.code = code
+
+
+# ---- C structs (must match include/mcmc355.h) -------------------------------
+MC_OK = 0
+MC_ERR_INVALID = -1
+MC_ERR_UNSUPPORTED = -2
+MC_ERR_HIP = -3
+MC_ERR_NOMEM = -4
+
+MC_DIST_NORMAL = 0
+MC_DIST_HALFNORMAL = 1
+
+MC_OP_NONE = 0
+MC_OP_CONST = 1
+MC_OP_PSCALAR = 2
+MC_OP_DATA = 3
+MC_OP_PVEC = 4
+MC_OP_GATHER = 5
+
+MC_RNG_TAG_MOMENTUM = 1
+MC_RNG_TAG_ACCEPT = 2
+MC_RNG_TAG_SLICE = 3
+MC_RNG_TAG_DEPTH = 4
+MC_RNG_TAG_MERGE = 5
+MC_RNG_TAG_USER = 16
+
+
+class McOperand(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("param_offset", ctypes.c_int32),
+        ("pool_offset", ctypes.c_int64),
+        ("value", ctypes.c_float),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class McTerm(ctypes.Structure):
+    _fields_ = [
+        ("dist", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("n", ctypes.c_int64),
+        ("weight", ctypes.c_float),
+        ("reserved1", ctypes.c_float),
+        ("value", McOperand),
+        ("loc", McOperand),
+        ("scale", McOperand),
+    ]
+
+
+class McChainScalars(ctypes.Structure):
+    _fields_ = [
+        ("step_size", ctypes.c_double),
+        ("step_size_bar", ctypes.c_double),
+        ("h_bar", ctypes.c_double),
+        ("alpha_sum", ctypes.c_double),
+        ("mu", ctypes.c_float),
+        ("logp", ctypes.c_float),
+        ("n_accept", ctypes.c_int32),
+        ("n_total", ctypes.c_int32),
+        ("warmup_accept", ctypes.c_int32),
+        ("warmup_total", ctypes.c_int32),
+        ("depth_sum", ctypes.c_int64),
+        ("warmup_depth_sum", ctypes.c_int64),
+        ("n_grad", ctypes.c_int64),
+        ("n_divergent", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class McRunConfig(ctypes.Structure):
+    _fields_ = [
+        ("num_chains", ctypes.c_int64),
+        ("chain_offset", ctypes.c_int64),
+        ("num_warmup", ctypes.c_int64),
+        ("num_samples", ctypes.c_int64),
+        ("iter_begin", ctypes.c_int64),
+        ("iter_count", ctypes.c_int64),
+        ("sample_begin", ctypes.c_int64),
+        ("sample_capacity", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("step_size", ctypes.c_double),
+        ("target_accept", ctypes.c_double),
+        ("num_leapfrog_steps", ctypes.c_int32),
+        ("max_tree_depth", ctypes.c_int32),
+        ("adapt_step_size", ctypes.c_int32),
+        ("slice_mode", ctypes.c_int32),
+    ]
+
+
+class McTrace(ctypes.Structure):
+    _fields_ = [
+        ("iter_begin", ctypes.c_int64),
+        ("capacity", ctypes.c_int64),
+        ("accepted", ctypes.c_void_p),
+        ("accept_stat", ctypes.c_void_p),
+        ("step_size", ctypes.c_void_p),
+        ("energy", ctypes.c_void_p),
+        ("tree_depth", ctypes.c_void_p),
+        ("n_leapfrog", ctypes.c_void_p),
+    ]
+
+
+# (name, restype, argtypes) for every symbol include/mcmc355.h declares
+_VP = ctypes.c_void_p
+SIGNATURES = [
+    ("mc_program_create", ctypes.c_int,
+     [ctypes.POINTER(McTerm), ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
+      _VP, ctypes.c_int64, _VP, ctypes.c_int64, ctypes.POINTER(_VP)]),
+    ("mc_program_destroy", ctypes.c_int, [_VP]),
+    ("mc_program_num_params", ctypes.c_int32, [_VP]),
+    ("mc_program_waves_per_chain", ctypes.c_int32, [_VP]),
+    ("mc_logp_grad", ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP, _VP, _VP]),
+    ("mc_dist_log_prob", ctypes.c_int,
+     [ctypes.c_int32, ctypes.c_int64, _VP, ctypes.c_int32, _VP, ctypes.c_int32, _VP,
+      ctypes.c_int32, _VP, _VP]),
+    ("mc_state_bytes", ctypes.c_int64, [_VP, ctypes.c_int64]),
+    ("mc_state_offsets", ctypes.c_int,
+     [_VP, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    ("mc_state_init", ctypes.c_int, [_VP, ctypes.c_int64, _VP, ctypes.c_double, _VP, _VP]),
+    ("mc_hmc_workspace_bytes", ctypes.c_int64, [_VP, ctypes.c_int64]),
+    ("mc_hmc_run", ctypes.c_int,
+     [_VP, ctypes.POINTER(McRunConfig), _VP, _VP, ctypes.POINTER(McTrace), _VP,
+      ctypes.c_int64, _VP]),
+    ("mc_nuts_workspace_bytes", ctypes.c_int64, [_VP, ctypes.c_int64, ctypes.c_int32]),
+    ("mc_nuts_run", ctypes.c_int,
+     [_VP, ctypes.POINTER(McRunConfig), _VP, _VP, ctypes.POINTER(McTrace), _VP,
+      ctypes.c_int64, _VP]),
+    ("mc_rng_fill", ctypes.c_int,
+     [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.c_uint32, ctypes.c_int64, ctypes.c_int32, _VP, _VP]),
+    ("mc_last_error", ctypes.c_char_p, []),
+    ("mc_abi_version", ctypes.c_int32, []),
+]
+
+_lib = None
+
+
+def load():
+    """Load libmcmc355.so (torch first, so the process has one HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (its libamdhip64 must be the one the library binds)
+
+    if not os.path.exists(LIB_PATH):
+        raise EngineUnavailable(
+            f"{LIB_PATH} is not built; run `make -C mlx-mcmc_amd/csrc` "
+            "(or __graft_entry__.build()) — there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.mc_abi_version() != 1:
+        raise EngineUnavailable("libmcmc355.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != MC_OK:
+        msg = load().mc_last_error()
+        raise EngineError(rc, msg.decode() if msg else "")
+
+
+def require_device():
+    """Return the torch device the engine runs on; raise if there is none."""
+    import torch
+
+    load()
+    if not torch.cuda.is_available():
+        raise EngineUnavailable(
+            "no ROCm GPU visible: the MI355X engine has no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_handle():
+    import torch
+
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)

@@ -1,0 +1,491 @@
+"""Tracing a user ``log_prob(params)`` into the engine's term program.
+
+The reference differentiates the user's Python ``log_prob`` with ``mx.grad``
+(mlx_mcmc/kernels/hmc.py:53-67, nuts.py:76-87).  Here the function is called
+ONCE with symbolic parameters; ``Normal`` / ``HalfNormal`` (the distributions
+on the hot path, distributions/normal.py:33-56, halfnormal.py:34-63) record a
+*term* instead of computing, and ``mx.sum`` / ``+`` / ``mx.array([...])``
+combine terms.  The result is a program for ``mc_program_create``: the log
+density as ``lp_const + sum_t weight_t * sum_i log_prob_t(value_i; loc_i,
+scale_i)``, whose forward value and reverse-mode gradient the HIP kernels
+evaluate in one fused sweep per term.
+
+Operands a term accepts (anything else raises ``TraceError``):
+  constants (Python / NumPy scalars), data vectors (array-likes), a parameter
+  (scalar or vector), a basic slice ``p[a:b]`` or element ``p[i]`` of a vector
+  parameter, and an integer gather ``p[idx]`` (hierarchical models, e.g.
+  ``Normal(theta[group], sigma).log_prob(y)``).
+Per-observation Python loops (examples/01_simple_normal.py:46-48,
+tests/test_nuts.py:194-196) trace to many scalar terms with identical
+distribution arguments; they are folded into one vector term.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+
+
+class TraceError(TypeError):
+    """The log density uses an operation the MI355X tape does not support."""
+
+
+_UNSUPPORTED = (
+    "the MI355X tape supports log densities built from Normal / HalfNormal "
+    "terms (summed with mx.sum, +, -, scalar *) whose arguments are parameters, "
+    "parameter slices / integer gathers, data arrays or constants")
+
+
+# ---------------------------------------------------------------------------
+# symbolic values
+# ---------------------------------------------------------------------------
+class Param:
+    """A parameter (or a view of one) during tracing."""
+
+    __array_priority__ = 1000  # make NumPy defer to our operators
+
+    def __init__(self, name: str, offset: int, shape: Tuple[int, ...], view=None):
+        self.name = name
+        self.offset = offset          # flat offset of the base parameter
+        self.base_shape = shape
+        # view: None (whole param), ('elem', flat_index), ('slice', start, len),
+        # ('gather', int32 index array relative to `offset`)
+        self.view = view
+
+    @property
+    def shape(self) -> Tuple[int, ...]:
+        v = self.view
+        if v is None:
+            return self.base_shape
+        if v[0] == "elem":
+            return ()
+        if v[0] == "slice":
+            return (v[2],)
+        return tuple(v[2])
+
+    @property
+    def size(self) -> int:
+        return int(np.prod(self.shape)) if self.shape else 1
+
+    @property
+    def ndim(self) -> int:
+        return len(self.shape)
+
+    def __len__(self):
+        if not self.shape:
+            raise TypeError("len() of a scalar parameter")
+        return self.shape[0]
+
+    def __getitem__(self, idx):
+        if self.view is not None and self.view[0] != "slice":
+            raise TraceError("indexing a view of a parameter is not supported; " + _UNSUPPORTED)
+        base = 0
+        length = self.size
+        if self.view is not None:
+            base, length = self.view[1], self.view[2]
+        if len(self.base_shape) > 1 and self.view is None:
+            raise TraceError("indexing multi-dimensional parameters is not supported")
+        if isinstance(idx, (int, np.integer)):
+            i = int(idx)
+            if i < 0:
+                i += length
+            if not 0 <= i < length:
+                raise IndexError(f"index {idx} out of range for parameter '{self.name}'")
+            return Param(self.name, self.offset, self.base_shape, ("elem", base + i))
+        if isinstance(idx, slice):
+            start, stop, step = idx.indices(length)
+            if step != 1:
+                raise TraceError("strided parameter slices are not supported")
+            return Param(self.name, self.offset, self.base_shape,
+                         ("slice", base + start, max(0, stop - start)))
+        arr = np.asarray(idx)
+        if arr.dtype.kind not in "iu":
+            raise TraceError("parameters can only be gathered by an integer index array")
+        arr = arr.astype(np.int64)
+        arr = np.where(arr < 0, arr + length, arr)
+        if arr.size and (arr.min() < 0 or arr.max() >= length):
+            raise IndexError(f"gather index out of range for parameter '{self.name}'")
+        return Param(self.name, self.offset, self.base_shape,
+                     ("gather", (base + arr).astype(np.int32).ravel(), arr.shape))
+
+    def _unsupported(self, *a, **k):
+        raise TraceError(f"arithmetic on traced parameter '{self.name}': " + _UNSUPPORTED)
+
+    __add__ = __radd__ = __sub__ = __rsub__ = __mul__ = __rmul__ = _unsupported
+    __truediv__ = __rtruediv__ = __pow__ = __neg__ = __abs__ = _unsupported
+
+    def __float__(self):
+        raise TraceError(f"float() of traced parameter '{self.name}' (a Python branch on a "
+                         "parameter value cannot be traced): " + _UNSUPPORTED)
+
+    __bool__ = __int__ = __float__
+
+    def __repr__(self):
+        return f"Param({self.name}, view={self.view})"
+
+
+@dataclass
+class Operand:
+    kind: int
+    param_offset: int = 0
+    value: float = 0.0
+    data: Optional[np.ndarray] = None    # float32, DATA
+    index: Optional[np.ndarray] = None   # int32,   GATHER
+    shape: Tuple[int, ...] = ()
+
+    def key(self):
+        if self.kind == _lib.MC_OP_CONST:
+            return ("c", float(np.float32(self.value)))
+        if self.kind == _lib.MC_OP_PSCALAR:
+            return ("p", self.param_offset)
+        if self.kind == _lib.MC_OP_PVEC:
+            return ("v", self.param_offset, self.shape)
+        if self.kind == _lib.MC_OP_DATA:
+            return ("d", id(self.data))
+        if self.kind == _lib.MC_OP_GATHER:
+            return ("g", self.param_offset, id(self.index))
+        return ("n",)
+
+
+NONE_OPERAND = Operand(_lib.MC_OP_NONE)
+
+
+def to_operand(x) -> Operand:
+    """Classify a distribution argument."""
+    if isinstance(x, Param):
+        v = x.view
+        if v is None:
+            if x.base_shape == ():
+                return Operand(_lib.MC_OP_PSCALAR, param_offset=x.offset)
+            return Operand(_lib.MC_OP_PVEC, param_offset=x.offset, shape=x.base_shape)
+        if v[0] == "elem":
+            return Operand(_lib.MC_OP_PSCALAR, param_offset=x.offset + v[1])
+        if v[0] == "slice":
+            return Operand(_lib.MC_OP_PVEC, param_offset=x.offset + v[1], shape=(v[2],))
+        return Operand(_lib.MC_OP_GATHER, param_offset=x.offset, index=v[1], shape=tuple(v[2]))
+    if isinstance(x, LogProbExpr):
+        raise TraceError("a log density cannot be a distribution argument: " + _UNSUPPORTED)
+    try:
+        import torch
+
+        if isinstance(x, torch.Tensor):
+            x = x.detach().cpu().numpy()
+    except ImportError:  # pragma: no cover
+        pass
+    arr = np.asarray(x)
+    if arr.dtype == object:
+        raise TraceError("unsupported distribution argument: " + _UNSUPPORTED)
+    arr = arr.astype(np.float32)
+    if arr.ndim == 0:
+        return Operand(_lib.MC_OP_CONST, value=float(arr))
+    return Operand(_lib.MC_OP_DATA, data=np.ascontiguousarray(arr).ravel(), shape=arr.shape)
+
+
+def is_symbolic(*xs) -> bool:
+    return any(isinstance(x, (Param, LogProbExpr)) for x in xs)
+
+
+@dataclass
+class Term:
+    dist: int
+    value: Operand
+    loc: Operand
+    scale: Operand
+    n: int
+    weight: float = 1.0
+
+
+def broadcast_n(dist_name: str, ops: List[Operand]) -> Tuple[int, Tuple[int, ...]]:
+    shapes = [o.shape for o in ops if o.kind not in (_lib.MC_OP_NONE,) and o.shape != ()]
+    if not shapes:
+        return 1, ()
+    s0 = shapes[0]
+    for s in shapes[1:]:
+        if s != s0:
+            raise TraceError(f"{dist_name}: cannot broadcast operand shapes {shapes} "
+                             "(operands must be scalars or share one shape)")
+    return int(np.prod(s0)), s0
+
+
+class LogProbExpr:
+    """A bag of weighted terms plus a constant; shape () once summed."""
+
+    __array_priority__ = 1000
+
+    def __init__(self, terms: List[Term], const: float, shape: Tuple[int, ...]):
+        self.terms = terms
+        self.const = const
+        self.shape = shape
+
+    # -- arithmetic ----------------------------------------------------------
+    def _combine(self, other, sign: float):
+        if isinstance(other, LogProbExpr):
+            if self.shape != other.shape:
+                if self.shape == () or other.shape == ():
+                    raise TraceError("adding a scalar log density to an unsummed vector one "
+                                     "(sum it with mx.sum first)")
+                raise TraceError(f"shape mismatch {self.shape} vs {other.shape}")
+            terms = list(self.terms) + [_scaled(t, sign) for t in other.terms]
+            return LogProbExpr(terms, self.const + sign * other.const, self.shape)
+        if isinstance(other, Param):
+            raise TraceError("adding a raw parameter to a log density: " + _UNSUPPORTED)
+        c = _scalar_const(other)
+        if self.shape != ():
+            raise TraceError("adding a constant to an unsummed vector log density")
+        return LogProbExpr(list(self.terms), self.const + sign * c, ())
+
+    def __add__(self, other):
+        return self._combine(other, 1.0)
+
+    def __radd__(self, other):
+        return self._combine(other, 1.0)
+
+    def __sub__(self, other):
+        return self._combine(other, -1.0)
+
+    def __rsub__(self, other):
+        return (-self)._combine(other, 1.0)
+
+    def __neg__(self):
+        return self * -1.0
+
+    def __mul__(self, other):
+        c = _scalar_const(other)
+        return LogProbExpr([_scaled(t, c) for t in self.terms], self.const * c, self.shape)
+
+    __rmul__ = __mul__
+
+    def sum(self, axis=None):
+        if axis not in (None, 0) or (axis == 0 and len(self.shape) > 1):
+            raise TraceError("only full reductions of a log density are supported")
+        return LogProbExpr(list(self.terms), self.const, ())
+
+    def __float__(self):
+        raise TraceError("float() of a traced log density: " + _UNSUPPORTED)
+
+    __bool__ = __float__
+
+    def __repr__(self):
+        return f"LogProbExpr({len(self.terms)} terms, shape={self.shape})"
+
+
+def _scaled(t: Term, c: float) -> Term:
+    return Term(t.dist, t.value, t.loc, t.scale, t.n, t.weight * c)
+
+
+def _scalar_const(x) -> float:
+    if isinstance(x, (Param, LogProbExpr)):
+        raise TraceError(_UNSUPPORTED)
+    arr = np.asarray(x)
+    if arr.dtype == object or arr.size != 1:
+        raise TraceError("only scalar constants can be combined with a log density")
+    return float(arr.reshape(()))
+
+
+def make_term(dist: int, dist_name: str, value, loc, scale) -> LogProbExpr:
+    ops = [to_operand(value), NONE_OPERAND if loc is None else to_operand(loc),
+           to_operand(scale)]
+    n, shape = broadcast_n(dist_name, ops)
+    for o in ops:
+        if o.kind in (_lib.MC_OP_DATA, _lib.MC_OP_GATHER) and o.shape == ():
+            o.shape = (1,)
+    return LogProbExpr([Term(dist, ops[0], ops[1], ops[2], n)], 0.0, shape)
+
+
+def stack(items) -> LogProbExpr:
+    """mx.array([lp_1, ..., lp_k]) over traced scalar log densities."""
+    terms: List[Term] = []
+    const = 0.0
+    for it in items:
+        if isinstance(it, LogProbExpr):
+            if it.shape != ():
+                raise TraceError("mx.array of vector log densities is not supported")
+            terms += it.terms
+            const += it.const
+        else:
+            const += _scalar_const(it)
+    return LogProbExpr(terms, const, (len(items),))
+
+
+# ---------------------------------------------------------------------------
+# folding + program building
+# ---------------------------------------------------------------------------
+def fold_terms(terms: List[Term]) -> List[Term]:
+    """Merge terms that differ only in a constant/data `value`.
+
+    ``for y in data: lp += Normal(mu, sigma).log_prob(y)`` yields one scalar
+    term per observation; folding gives the single vector term the reference
+    would have written as ``mx.sum(Normal(mu, sigma).log_prob(data))``.
+    """
+    out: List[Term] = []
+    groups: Dict[tuple, int] = {}
+    for t in terms:
+        foldable = (t.value.kind in (_lib.MC_OP_CONST, _lib.MC_OP_DATA)
+                    and t.loc.kind in (_lib.MC_OP_CONST, _lib.MC_OP_PSCALAR, _lib.MC_OP_NONE)
+                    and t.scale.kind in (_lib.MC_OP_CONST, _lib.MC_OP_PSCALAR))
+        if not foldable:
+            out.append(t)
+            continue
+        key = (t.dist, float(np.float32(t.weight)), t.loc.key(), t.scale.key())
+        vals = (np.array([t.value.value], np.float32) if t.value.kind == _lib.MC_OP_CONST
+                else t.value.data)
+        if key in groups:
+            g = out[groups[key]]
+            g.value.data = np.concatenate([g.value.data, vals])
+            g.value.shape = (g.value.data.size,)
+            g.n = g.value.data.size
+        else:
+            groups[key] = len(out)
+            out.append(Term(t.dist, Operand(_lib.MC_OP_DATA, data=vals.copy(),
+                                            shape=(vals.size,)),
+                            t.loc, t.scale, int(vals.size), t.weight))
+    return out
+
+
+@dataclass
+class ParamLayout:
+    names: List[str]
+    shapes: List[Tuple[int, ...]]
+    offsets: List[int]
+    size: int
+
+    def flatten(self, params: dict) -> np.ndarray:
+        out = np.empty(self.size, np.float32)
+        for name, shp, off in zip(self.names, self.shapes, self.offsets):
+            v = np.asarray(_to_numpy(params[name]), np.float32)
+            if v.shape != shp:
+                raise ValueError(f"parameter '{name}' has shape {v.shape}, expected {shp}")
+            n = int(np.prod(shp)) if shp else 1
+            out[off:off + n] = v.ravel()
+        return out
+
+    def unflatten(self, flat: np.ndarray) -> Dict[str, np.ndarray]:
+        """flat: [..., D] -> {name: [..., *shape]}"""
+        lead = flat.shape[:-1]
+        out = {}
+        for name, shp, off in zip(self.names, self.shapes, self.offsets):
+            n = int(np.prod(shp)) if shp else 1
+            out[name] = flat[..., off:off + n].reshape(lead + shp)
+        return out
+
+
+def _to_numpy(x):
+    try:
+        import torch
+
+        if isinstance(x, torch.Tensor):
+            return x.detach().cpu().numpy()
+    except ImportError:  # pragma: no cover
+        pass
+    return x
+
+
+def layout_of(initial_params: dict) -> ParamLayout:
+    names, shapes, offsets = [], [], []
+    off = 0
+    for name, v in initial_params.items():
+        arr = np.asarray(_to_numpy(v), np.float32)
+        names.append(name)
+        shapes.append(tuple(arr.shape))
+        offsets.append(off)
+        off += int(arr.size)
+    if off == 0:
+        raise ValueError("initial_params is empty")
+    return ParamLayout(names, shapes, offsets, off)
+
+
+@dataclass
+class TracedModel:
+    layout: ParamLayout
+    terms: List[Term]
+    lp_const: float
+    # pools handed to mc_program_create
+    data: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))
+    index: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
+    c_terms: object = None
+
+
+def trace(log_prob_fn, initial_params: dict) -> TracedModel:
+    layout = layout_of(initial_params)
+    sym = {name: Param(name, off, shp)
+           for name, shp, off in zip(layout.names, layout.shapes, layout.offsets)}
+    out = log_prob_fn(sym)
+    if isinstance(out, Param):
+        raise TraceError("log_prob returned a parameter, not a log density")
+    if not isinstance(out, LogProbExpr):
+        raise TraceError("log_prob did not build its value from Normal / HalfNormal terms: "
+                         + _UNSUPPORTED)
+    if out.shape != ():
+        raise TraceError(f"log_prob must return a scalar (got shape {out.shape}); "
+                         "sum the likelihood with mx.sum as the reference does")
+    terms = fold_terms(out.terms)
+    model = TracedModel(layout, terms, float(np.float32(out.const)))
+    _build_pools(model)
+    return model
+
+
+def _build_pools(model: TracedModel) -> None:
+    data_parts: List[np.ndarray] = []
+    index_parts: List[np.ndarray] = []
+    nd = 0
+    ni = 0
+    arr = (_lib.McTerm * max(1, len(model.terms)))()
+    for k, t in enumerate(model.terms):
+        ct = arr[k]
+        ct.dist = t.dist
+        ct.n = t.n
+        ct.weight = t.weight
+        for slot, o in (("value", t.value), ("loc", t.loc), ("scale", t.scale)):
+            co = getattr(ct, slot)
+            co.kind = o.kind
+            co.param_offset = o.param_offset
+            co.value = o.value
+            if o.kind == _lib.MC_OP_DATA:
+                co.pool_offset = nd
+                data_parts.append(o.data.astype(np.float32))
+                nd += o.data.size
+            elif o.kind == _lib.MC_OP_GATHER:
+                co.pool_offset = ni
+                index_parts.append(o.index.astype(np.int32))
+                ni += o.index.size
+    model.data = (np.concatenate(data_parts) if data_parts else np.zeros(0, np.float32))
+    model.index = (np.concatenate(index_parts) if index_parts else np.zeros(0, np.int32))
+    model.c_terms = arr
+
+
+class Program:
+    """An mc_program handle owning its device copy of the model."""
+
+    def __init__(self, model: TracedModel):
+        lib = _lib.load()
+        self.model = model
+        self.layout = model.layout
+        self.D = model.layout.size
+        h = ctypes.c_void_p()
+        data = np.ascontiguousarray(model.data, np.float32)
+        index = np.ascontiguousarray(model.index, np.int32)
+        _lib.check(lib.mc_program_create(
+            model.c_terms, len(model.terms), self.D, model.lp_const,
+            data.ctypes.data_as(ctypes.c_void_p), data.size,
+            index.ctypes.data_as(ctypes.c_void_p), index.size, ctypes.byref(h)))
+        self.handle = h
+        self.waves_per_chain = lib.mc_program_waves_per_chain(h)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().mc_program_destroy(h)
+            except Exception:  # pragma: no cover - interpreter shutdown
+                pass
+            self.handle = None
+
+
+def compile_model(log_prob_fn, initial_params: dict) -> Program:
+    _lib.require_device()
+    return Program(trace(log_prob_fn, initial_params))

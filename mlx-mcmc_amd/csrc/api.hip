@@ -1,0 +1,655 @@
+// api.hip — libmcmc355.so: program builder, launchers and the C-ABI of
+// include/mcmc355.h.  One translation unit so every kernel is launched from
+// the unit that defines it.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "eval.h"
+#include "hmc.h"
+#include "internal.h"
+#include "nuts.h"
+#include "philox.h"
+
+using namespace mc;
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+
+static int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define MC_HIP_TRY(expr)                                                                \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(MC_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));      \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// program
+// ---------------------------------------------------------------------------
+struct mc_program {
+    int32_t D = 0;
+    float lp_const = 0.0f;
+    int32_t wpc = 1;
+    int64_t max_n = 0;
+    std::vector<DevTerm> terms;
+    DevTerm* d_terms = nullptr;
+    float* d_data = nullptr;
+    int32_t* d_index = nullptr;
+};
+
+static DevCtx ctx_of(const mc_program* p) {
+    DevCtx c;
+    c.terms = p->d_terms;
+    c.n_terms = (int32_t)p->terms.size();
+    c.D = p->D;
+    c.lp_const = p->lp_const;
+    c.pad = 0;
+    c.data = p->d_data;
+    c.index = p->d_index;
+    return c;
+}
+
+static bool is_vec_kind(int k) { return k == MC_OP_DATA || k == MC_OP_PVEC || k == MC_OP_GATHER; }
+static bool is_acc_vec(int k) { return k == MC_OP_PVEC || k == MC_OP_GATHER; }
+
+// f32 constants exactly as the reference forms them (normal.py:31,
+// halfnormal.py:31-32): log_norm = -0.5 * f32 log(f32(2*pi)), log2 = f32 log 2.
+static float c_log_norm() {
+    const float two_pi = (float)(2.0 * 3.141592653589793);
+    const float l = (float)std::log((double)two_pi);
+    return -0.5f * l;
+}
+static float c_log2() { return (float)std::log(2.0); }
+
+static int choose_wpc(int64_t max_n) {
+    if (max_n <= 512) return 1;
+    if (max_n <= 16384) return 4;
+    return 16;
+}
+
+extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t n_params,
+                                 float lp_const, const float* data, int64_t n_data,
+                                 const int32_t* index, int64_t n_index, mc_program** out) {
+    if (!out) return fail(MC_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    if (n_params <= 0) return fail(MC_ERR_INVALID, "n_params must be positive (got %d)", n_params);
+    if (n_terms < 0 || (n_terms > 0 && !terms)) return fail(MC_ERR_INVALID, "bad term array");
+    if (n_data < 0 || (n_data > 0 && !data)) return fail(MC_ERR_INVALID, "bad data pool");
+    if (n_index < 0 || (n_index > 0 && !index)) return fail(MC_ERR_INVALID, "bad index pool");
+
+    std::vector<float> dpool(data, data + n_data);
+    std::vector<int32_t> ipool(index, index + n_index);
+    std::vector<DevTerm> dts;
+    int64_t max_n = 0;
+
+    for (int32_t t = 0; t < n_terms; ++t) {
+        const mc_term& src = terms[t];
+        if (src.dist != MC_DIST_NORMAL && src.dist != MC_DIST_HALFNORMAL)
+            return fail(MC_ERR_INVALID, "term %d: unknown distribution %d", t, src.dist);
+        if (src.n < 1) return fail(MC_ERR_INVALID, "term %d: n must be >= 1", t);
+        const int64_t n = src.n;
+        DevTerm dt;
+        std::memset(&dt, 0, sizeof(dt));
+        dt.dist = src.dist;
+        dt.n = n;
+        dt.weight = src.weight;
+        dt.c0 = (src.dist == MC_DIST_NORMAL) ? c_log_norm() : (c_log2() + c_log_norm());
+        const mc_operand* ops[3] = {&src.value, &src.loc, &src.scale};
+        for (int a = 0; a < 3; ++a) {
+            const mc_operand& o = *ops[a];
+            DevOperand& d = dt.op[a];
+            d.kind = o.kind;
+            d.poff = o.param_offset;
+            d.pool = o.pool_offset;
+            d.cval = o.value;
+            d.unique = 1;
+            const bool need = !(a == 1 && src.dist == MC_DIST_HALFNORMAL);
+            if (!need) {
+                if (o.kind != MC_OP_NONE && o.kind != MC_OP_CONST)
+                    return fail(MC_ERR_INVALID, "term %d: HalfNormal takes no loc operand", t);
+                d.kind = MC_OP_NONE;
+                continue;
+            }
+            switch (o.kind) {
+                case MC_OP_CONST:
+                    break;
+                case MC_OP_PSCALAR:
+                    if (o.param_offset < 0 || o.param_offset >= n_params)
+                        return fail(MC_ERR_INVALID, "term %d op %d: param %d out of range", t, a,
+                                    o.param_offset);
+                    break;
+                case MC_OP_DATA:
+                    if (o.pool_offset < 0 || o.pool_offset + n > n_data)
+                        return fail(MC_ERR_INVALID, "term %d op %d: data range out of pool", t, a);
+                    break;
+                case MC_OP_PVEC:
+                    if (o.param_offset < 0 || (int64_t)o.param_offset + n > n_params)
+                        return fail(MC_ERR_INVALID, "term %d op %d: param slice out of range", t,
+                                    a);
+                    break;
+                case MC_OP_GATHER: {
+                    if (o.pool_offset < 0 || o.pool_offset + n > n_index)
+                        return fail(MC_ERR_INVALID, "term %d op %d: index range out of pool", t,
+                                    a);
+                    std::vector<int32_t> v(ipool.begin() + o.pool_offset,
+                                           ipool.begin() + o.pool_offset + n);
+                    for (int32_t x : v)
+                        if (x < 0 || (int64_t)o.param_offset + x >= n_params)
+                            return fail(MC_ERR_INVALID,
+                                        "term %d op %d: gather index %d out of range", t, a, x);
+                    std::sort(v.begin(), v.end());
+                    d.unique = (std::adjacent_find(v.begin(), v.end()) == v.end()) ? 1 : 0;
+                    break;
+                }
+                default:
+                    return fail(MC_ERR_INVALID, "term %d op %d: bad operand kind %d", t, a,
+                                o.kind);
+            }
+        }
+        // the non-injective gather, if any, orders the term
+        int primary = -1;
+        for (int a = 0; a < 3; ++a) {
+            if (dt.op[a].kind == MC_OP_GATHER && !dt.op[a].unique) {
+                if (primary >= 0)
+                    return fail(MC_ERR_UNSUPPORTED,
+                                "term %d gathers through two non-injective index arrays", t);
+                primary = a;
+            }
+        }
+        dt.primary = primary;
+        if (primary >= 0) {
+            const int64_t ip = dt.op[primary].pool;
+            bool sorted = true;
+            for (int64_t i = 1; i < n && sorted; ++i) sorted = ipool[ip + i - 1] <= ipool[ip + i];
+            if (!sorted) {
+                std::vector<int64_t> perm(n);
+                std::iota(perm.begin(), perm.end(), 0);
+                std::stable_sort(perm.begin(), perm.end(), [&](int64_t x, int64_t y) {
+                    return ipool[ip + x] < ipool[ip + y];
+                });
+                for (int a = 0; a < 3; ++a) {
+                    DevOperand& d = dt.op[a];
+                    if (d.kind == MC_OP_DATA) {
+                        const int64_t base = (int64_t)dpool.size();
+                        for (int64_t i = 0; i < n; ++i) dpool.push_back(dpool[d.pool + perm[i]]);
+                        d.pool = base;
+                    } else if (d.kind == MC_OP_GATHER) {
+                        const int64_t base = (int64_t)ipool.size();
+                        for (int64_t i = 0; i < n; ++i) ipool.push_back(ipool[d.pool + perm[i]]);
+                        d.pool = base;
+                    } else if (d.kind == MC_OP_PVEC) {
+                        const int64_t base = (int64_t)ipool.size();
+                        for (int64_t i = 0; i < n; ++i) ipool.push_back((int32_t)perm[i]);
+                        d.kind = MC_OP_GATHER;
+                        d.pool = base;
+                        d.unique = 1;
+                    }
+                }
+            }
+        }
+        // pass planning: accumulating vector operands with overlapping parameter
+        // ranges go to different sweeps
+        int64_t lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            const DevOperand& d = dt.op[a];
+            lo[a] = hi[a] = -1;
+            if (d.kind == MC_OP_PVEC) {
+                lo[a] = d.poff;
+                hi[a] = d.poff + n - 1;
+            } else if (d.kind == MC_OP_GATHER) {
+                int32_t mn = ipool[d.pool], mx = ipool[d.pool];
+                for (int64_t i = 1; i < n; ++i) {
+                    mn = std::min(mn, ipool[d.pool + i]);
+                    mx = std::max(mx, ipool[d.pool + i]);
+                }
+                lo[a] = d.poff + mn;
+                hi[a] = d.poff + mx;
+            }
+        }
+        uint32_t masks[3] = {PASS_LP, 0, 0};
+        int npass = 1;
+        for (int a = 0; a < 3; ++a) {
+            const uint32_t bit = 1u << a;
+            if (dt.op[a].kind == MC_OP_PSCALAR) {
+                masks[0] |= bit;
+                continue;
+            }
+            if (!is_acc_vec(dt.op[a].kind)) continue;
+            int placed = -1;
+            for (int ps = 0; ps < npass && placed < 0; ++ps) {
+                bool clash = false;
+                for (int b = 0; b < a; ++b)
+                    if ((masks[ps] & (1u << b)) && is_acc_vec(dt.op[b].kind) &&
+                        !(hi[a] < lo[b] || hi[b] < lo[a]))
+                        clash = true;
+                if (!clash) placed = ps;
+            }
+            if (placed < 0) placed = npass++;
+            masks[placed] |= bit;
+        }
+        dt.npass = npass;
+        for (int ps = 0; ps < 3; ++ps) dt.pass_mask[ps] = masks[ps];
+        max_n = std::max(max_n, n);
+        dts.push_back(dt);
+    }
+
+    mc_program* p = new mc_program();
+    p->D = n_params;
+    p->lp_const = lp_const;
+    p->max_n = max_n;
+    p->wpc = choose_wpc(max_n);
+    p->terms = dts;
+    hipError_t e = hipSuccess;
+    if (!dts.empty()) {
+        e = hipMalloc(&p->d_terms, dts.size() * sizeof(DevTerm));
+        if (e == hipSuccess)
+            e = hipMemcpy(p->d_terms, dts.data(), dts.size() * sizeof(DevTerm),
+                          hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess && !dpool.empty()) {
+        e = hipMalloc(&p->d_data, dpool.size() * sizeof(float));
+        if (e == hipSuccess)
+            e = hipMemcpy(p->d_data, dpool.data(), dpool.size() * sizeof(float),
+                          hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess && !ipool.empty()) {
+        e = hipMalloc(&p->d_index, ipool.size() * sizeof(int32_t));
+        if (e == hipSuccess)
+            e = hipMemcpy(p->d_index, ipool.data(), ipool.size() * sizeof(int32_t),
+                          hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+        mc_program_destroy(p);
+        return fail(e == hipErrorOutOfMemory ? MC_ERR_NOMEM : MC_ERR_HIP,
+                    "program upload failed: %s", hipGetErrorString(e));
+    }
+    *out = p;
+    return MC_OK;
+}
+
+extern "C" int mc_program_destroy(mc_program* p) {
+    if (!p) return MC_OK;
+    if (p->d_terms) (void)hipFree(p->d_terms);
+    if (p->d_data) (void)hipFree(p->d_data);
+    if (p->d_index) (void)hipFree(p->d_index);
+    delete p;
+    return MC_OK;
+}
+
+extern "C" int32_t mc_program_num_params(const mc_program* p) { return p ? p->D : -1; }
+extern "C" int32_t mc_program_waves_per_chain(const mc_program* p) { return p ? p->wpc : -1; }
+
+// ---------------------------------------------------------------------------
+// geometry helpers
+// ---------------------------------------------------------------------------
+static int cpb_of(int wpc) { return wpc >= 4 ? 1 : 4 / wpc; }
+static int block_of(int wpc) { return 64 * wpc * cpb_of(wpc); }
+static int32_t dpad_of(int32_t D) { return (D + 15) / 16 * 16; }
+static constexpr int64_t kLdsArenaBudget = 64 * 1024;  // keep >= 2 workgroups per CU
+
+static int64_t hmc_lds_floats(const mc_program* p, bool lds_arena) {
+    return group_scratch_floats(p->wpc) + (lds_arena ? 5 * (int64_t)dpad_of(p->D) : 0);
+}
+static bool hmc_use_lds(const mc_program* p) {
+    return cpb_of(p->wpc) * hmc_lds_floats(p, true) * 4 <= kLdsArenaBudget;
+}
+
+template <typename K>
+static hipError_t allow_lds(K kernel, size_t bytes) {
+    if (bytes <= 64 * 1024) return hipSuccess;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+static TraceDev trace_of(const mc_trace* t) {
+    TraceDev d;
+    std::memset(&d, 0, sizeof(d));
+    if (t) {
+        d.iter_begin = t->iter_begin;
+        d.capacity = t->capacity;
+        d.accepted = t->accepted;
+        d.accept_stat = t->accept_stat;
+        d.step_size = t->step_size;
+        d.energy = t->energy;
+        d.tree_depth = t->tree_depth;
+        d.n_leapfrog = t->n_leapfrog;
+    } else {
+        d.capacity = 0;
+    }
+    return d;
+}
+
+// ---------------------------------------------------------------------------
+// batched log density + gradient
+// ---------------------------------------------------------------------------
+template <int WPC>
+__global__ void __launch_bounds__(WPC >= 4 ? 64 * WPC : 256)
+k_logp(DevCtx P, int64_t n_points, const float* q, float* logp, float* grad, int lds_floats) {
+    constexpr int CPB = (WPC >= 4) ? 1 : 4 / WPC;
+    constexpr int T = 64 * WPC;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lc = threadIdx.x / T;
+    const int64_t c = (int64_t)blockIdx.x * CPB + lc;
+    if (c >= n_points) return;
+    Group<WPC> G;
+    SegScratch S;
+    G.tid = threadIdx.x % T;
+    carve_group<WPC>(smem + (int64_t)lc * lds_floats, G, S);
+    const float lp = eval_lp_grad<WPC>(P, q + c * P.D, grad + c * P.D, G, S);
+    if (G.tid == 0) logp[c] = lp;
+}
+
+template <int WPC>
+static int launch_logp(const mc_program* p, int64_t n, const float* q, float* lp, float* g,
+                       hipStream_t st) {
+    const int lds_floats = group_scratch_floats(WPC);
+    const size_t lds = (size_t)cpb_of(WPC) * lds_floats * 4;
+    const int64_t grid = (n + cpb_of(WPC) - 1) / cpb_of(WPC);
+    MC_HIP_TRY(allow_lds(k_logp<WPC>, lds));
+    hipLaunchKernelGGL(k_logp<WPC>, dim3((unsigned)grid), dim3(block_of(WPC)), lds, st, ctx_of(p),
+                       n, q, lp, g, lds_floats);
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+extern "C" int mc_logp_grad(const mc_program* p, int64_t n_points, const float* q, float* logp,
+                            float* grad, void* stream) {
+    if (!p) return fail(MC_ERR_INVALID, "program is NULL");
+    if (n_points < 0) return fail(MC_ERR_INVALID, "n_points < 0");
+    if (n_points == 0) return MC_OK;
+    if (!q || !logp || !grad) return fail(MC_ERR_INVALID, "NULL buffer");
+    hipStream_t st = (hipStream_t)stream;
+    switch (p->wpc) {
+        case 1: return launch_logp<1>(p, n_points, q, logp, grad, st);
+        case 4: return launch_logp<4>(p, n_points, q, logp, grad, st);
+        default: return launch_logp<16>(p, n_points, q, logp, grad, st);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// elementwise Distribution.log_prob
+// ---------------------------------------------------------------------------
+__global__ void k_dist(int dist, float c0, int64_t n, const float* v, int vb, const float* m,
+                       int mb, const float* s, int sb, float* out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float vv = v[vb ? 0 : i];
+        const float ss = s[sb ? 0 : i];
+        const float logs = logf(ss);
+        ElemOut e;
+        if (dist == MC_DIST_NORMAL) {
+            const float mm = m[mb ? 0 : i];
+            e = elem_normal(c0, vv, mm, ss, logs);
+        } else {
+            e = elem_halfnormal(c0, vv, ss, logs);
+        }
+        out[i] = e.lp;
+    }
+}
+
+extern "C" int mc_dist_log_prob(int32_t dist, int64_t n, const float* v, int32_t vb,
+                                const float* m, int32_t mb, const float* s, int32_t sb,
+                                float* out, void* stream) {
+    if (dist != MC_DIST_NORMAL && dist != MC_DIST_HALFNORMAL)
+        return fail(MC_ERR_INVALID, "unknown distribution %d", dist);
+    if (n < 0) return fail(MC_ERR_INVALID, "n < 0");
+    if (n == 0) return MC_OK;
+    if (!v || !s || !out || (dist == MC_DIST_NORMAL && !m))
+        return fail(MC_ERR_INVALID, "NULL operand");
+    const float c0 = (dist == MC_DIST_NORMAL) ? c_log_norm() : (c_log2() + c_log_norm());
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_dist, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, dist,
+                       c0, n, v, vb, m ? m : v, mb, s, sb, out);
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// state
+// ---------------------------------------------------------------------------
+static int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
+
+extern "C" int mc_state_offsets(const mc_program* p, int64_t C, int64_t* q_off, int64_t* g_off) {
+    if (!p || C < 0) return fail(MC_ERR_INVALID, "bad arguments");
+    const int64_t s = align256(C * (int64_t)sizeof(mc_chain_scalars));
+    const int64_t qb = align256(C * p->D * 4);
+    if (q_off) *q_off = s;
+    if (g_off) *g_off = s + qb;
+    return MC_OK;
+}
+
+extern "C" int64_t mc_state_bytes(const mc_program* p, int64_t C) {
+    if (!p || C < 0) return -1;
+    return align256(C * (int64_t)sizeof(mc_chain_scalars)) + 2 * align256(C * p->D * 4);
+}
+
+template <int WPC>
+__global__ void __launch_bounds__(WPC >= 4 ? 64 * WPC : 256)
+k_init(DevCtx P, int64_t C, const float* q0, double eps0, float mu, mc_chain_scalars* scal,
+       float* st_q, float* st_g, int lds_floats) {
+    constexpr int CPB = (WPC >= 4) ? 1 : 4 / WPC;
+    constexpr int T = 64 * WPC;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int lc = threadIdx.x / T;
+    const int64_t c = (int64_t)blockIdx.x * CPB + lc;
+    if (c >= C) return;
+    Group<WPC> G;
+    SegScratch S;
+    G.tid = threadIdx.x % T;
+    carve_group<WPC>(smem + (int64_t)lc * lds_floats, G, S);
+    const int D = P.D;
+    for (int j = G.tid; j < D; j += T) st_q[c * D + j] = q0[c * D + j];
+    const float lp = eval_lp_grad<WPC>(P, q0 + c * D, st_g + c * D, G, S);
+    if (G.tid == 0) {
+        mc_chain_scalars sc = {};
+        sc.step_size = eps0;
+        sc.step_size_bar = 1.0;
+        sc.h_bar = 0.0;
+        sc.mu = mu;
+        sc.logp = lp;
+        sc.n_grad = 1;
+        scal[c] = sc;
+    }
+}
+
+template <int WPC>
+static int launch_init(const mc_program* p, int64_t C, const float* q0, double eps0,
+                       void* state, hipStream_t st) {
+    int64_t qo, go;
+    mc_state_offsets(p, C, &qo, &go);
+    char* b = (char*)state;
+    const int lds_floats = group_scratch_floats(WPC);
+    const size_t lds = (size_t)cpb_of(WPC) * lds_floats * 4;
+    const int64_t grid = (C + cpb_of(WPC) - 1) / cpb_of(WPC);
+    const float mu = mc_logf_ref((float)(10.0 * eps0));  // nuts.py:63 mx.log(10 * step_size)
+    MC_HIP_TRY(allow_lds(k_init<WPC>, lds));
+    hipLaunchKernelGGL(k_init<WPC>, dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
+                       ctx_of(p), C, q0, eps0, mu, (mc_chain_scalars*)b, (float*)(b + qo),
+                       (float*)(b + go), lds_floats);
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+extern "C" int mc_state_init(const mc_program* p, int64_t C, const float* q0, double eps0,
+                             void* state, void* stream) {
+    if (!p || C < 0 || (C > 0 && (!q0 || !state))) return fail(MC_ERR_INVALID, "bad arguments");
+    if (C == 0) return MC_OK;
+    hipStream_t st = (hipStream_t)stream;
+    switch (p->wpc) {
+        case 1: return launch_init<1>(p, C, q0, eps0, state, st);
+        case 4: return launch_init<4>(p, C, q0, eps0, state, st);
+        default: return launch_init<16>(p, C, q0, eps0, state, st);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// HMC / NUTS launches
+// ---------------------------------------------------------------------------
+static int check_cfg(const mc_program* p, const mc_run_config* cfg, void* state) {
+    if (!p || !cfg || !state) return fail(MC_ERR_INVALID, "NULL program/config/state");
+    if (cfg->num_chains < 0 || cfg->iter_count < 0 || cfg->iter_begin < 0 ||
+        cfg->num_warmup < 0 || cfg->num_samples < 0)
+        return fail(MC_ERR_INVALID, "negative count in config");
+    if (cfg->chain_offset < 0 || cfg->chain_offset + cfg->num_chains > (int64_t)UINT32_MAX)
+        return fail(MC_ERR_INVALID, "chain ids must fit in 32 bits");
+    if (cfg->iter_begin + cfg->iter_count > (int64_t)UINT32_MAX)
+        return fail(MC_ERR_INVALID, "iteration ids must fit in 32 bits");
+    return MC_OK;
+}
+
+extern "C" int64_t mc_hmc_workspace_bytes(const mc_program* p, int64_t C) {
+    if (!p || C < 0) return -1;
+    if (hmc_use_lds(p)) return 0;
+    return C * 5 * (int64_t)dpad_of(p->D) * 4;
+}
+
+template <int WPC, bool LDS>
+static int launch_hmc(const mc_program* p, const mc_run_config* cfg, void* state,
+                      float* samples, const mc_trace* tr, float* ws, hipStream_t st) {
+    int64_t qo, go;
+    mc_state_offsets(p, cfg->num_chains, &qo, &go);
+    char* b = (char*)state;
+    RunArgs A;
+    A.cfg = *cfg;
+    A.dpad = dpad_of(p->D);
+    A.lds_floats = (int32_t)hmc_lds_floats(p, LDS);
+    const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
+    const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
+    MC_HIP_TRY(allow_lds(k_hmc<WPC, LDS>, lds));
+    hipLaunchKernelGGL((k_hmc<WPC, LDS>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
+                       ctx_of(p), A, (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go),
+                       samples, trace_of(tr), ws);
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* state,
+                          float* samples, const mc_trace* tr, void* ws, int64_t ws_bytes,
+                          void* stream) {
+    int rc = check_cfg(p, cfg, state);
+    if (rc) return rc;
+    if (cfg->num_leapfrog_steps < 0) return fail(MC_ERR_INVALID, "num_leapfrog_steps < 0");
+    if (cfg->num_chains == 0 || cfg->iter_count == 0) return MC_OK;
+    const bool lds = hmc_use_lds(p);
+    const int64_t need = mc_hmc_workspace_bytes(p, cfg->num_chains);
+    if (!lds && (ws == nullptr || ws_bytes < need))
+        return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
+    hipStream_t st = (hipStream_t)stream;
+    float* w = (float*)ws;
+    switch (p->wpc) {
+        case 1: return lds ? launch_hmc<1, true>(p, cfg, state, samples, tr, w, st)
+                           : launch_hmc<1, false>(p, cfg, state, samples, tr, w, st);
+        case 4: return lds ? launch_hmc<4, true>(p, cfg, state, samples, tr, w, st)
+                           : launch_hmc<4, false>(p, cfg, state, samples, tr, w, st);
+        default: return lds ? launch_hmc<16, true>(p, cfg, state, samples, tr, w, st)
+                            : launch_hmc<16, false>(p, cfg, state, samples, tr, w, st);
+    }
+}
+
+extern "C" int64_t mc_nuts_workspace_bytes(const mc_program* p, int64_t C, int32_t max_depth) {
+    if (!p || C < 0 || max_depth < 0 || max_depth > kMaxTreeDepth) return -1;
+    return C * nuts_arena_vectors(max_depth) * (int64_t)dpad_of(p->D) * 4;
+}
+
+template <int WPC>
+static int launch_nuts(const mc_program* p, const mc_run_config* cfg, void* state,
+                       float* samples, const mc_trace* tr, float* ws, hipStream_t st) {
+    int64_t qo, go;
+    mc_state_offsets(p, cfg->num_chains, &qo, &go);
+    char* b = (char*)state;
+    RunArgs A;
+    A.cfg = *cfg;
+    A.dpad = dpad_of(p->D);
+    A.lds_floats = group_scratch_floats(WPC) + kNutsLdsWords;
+    const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
+    const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
+    MC_HIP_TRY(allow_lds(k_nuts<WPC>, lds));
+    hipLaunchKernelGGL(k_nuts<WPC>, dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
+                       ctx_of(p), A, (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go),
+                       samples, trace_of(tr), ws);
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+extern "C" int mc_nuts_run(const mc_program* p, const mc_run_config* cfg, void* state,
+                           float* samples, const mc_trace* tr, void* ws, int64_t ws_bytes,
+                           void* stream) {
+    int rc = check_cfg(p, cfg, state);
+    if (rc) return rc;
+    if (cfg->max_tree_depth < 0 || cfg->max_tree_depth > kMaxTreeDepth)
+        return fail(MC_ERR_UNSUPPORTED, "max_tree_depth must be in [0, %d]", kMaxTreeDepth);
+    if (cfg->num_chains == 0 || cfg->iter_count == 0) return MC_OK;
+    const int64_t need = mc_nuts_workspace_bytes(p, cfg->num_chains, cfg->max_tree_depth);
+    if (ws == nullptr || ws_bytes < need)
+        return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
+    hipStream_t st = (hipStream_t)stream;
+    float* w = (float*)ws;
+    switch (p->wpc) {
+        case 1: return launch_nuts<1>(p, cfg, state, samples, tr, w, st);
+        case 4: return launch_nuts<4>(p, cfg, state, samples, tr, w, st);
+        default: return launch_nuts<16>(p, cfg, state, samples, tr, w, st);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// RNG fill (test hook and Distribution.sample)
+// ---------------------------------------------------------------------------
+__global__ void k_rng(uint64_t seed, uint32_t chain, uint32_t iter, uint32_t tag, uint32_t sub,
+                      uint32_t index0, int64_t n, int mode, void* out) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const mc_u32x4 r = mc_draw(seed, chain, iter, tag, sub, index0 + (uint32_t)e);
+        if (mode == 0) {
+            uint32_t* o = (uint32_t*)out + 4 * e;
+            o[0] = r.x;
+            o[1] = r.y;
+            o[2] = r.z;
+            o[3] = r.w;
+        } else if (mode == 1) {
+            float* o = (float*)out + 4 * e;
+            o[0] = mc_u01_f32(r.x);
+            o[1] = mc_u01_f32(r.y);
+            o[2] = mc_u01_f32(r.z);
+            o[3] = mc_u01_f32(r.w);
+        } else {
+            float* o = (float*)out + 4 * e;
+            mc_box_muller(r.x, r.y, &o[0], &o[1]);
+            mc_box_muller(r.z, r.w, &o[2], &o[3]);
+        }
+    }
+}
+
+extern "C" int mc_rng_fill(uint64_t seed, uint32_t chain, uint32_t iter, uint32_t tag,
+                           uint32_t sub, uint32_t index0, int64_t n, int32_t mode, void* out,
+                           void* stream) {
+    if (n < 0 || (n > 0 && !out) || mode < 0 || mode > 2)
+        return fail(MC_ERR_INVALID, "bad arguments");
+    if (n == 0) return MC_OK;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_rng, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, seed,
+                       chain, iter, tag, sub, index0, n, mode, out);
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+extern "C" const char* mc_last_error(void) { return g_last_error.c_str(); }
+extern "C" int32_t mc_abi_version(void) { return MC_ABI_VERSION; }

@@ -1,0 +1,73 @@
+// internal.h — device-side program representation shared by the host code
+// that builds it (api.hip) and the kernels that execute it (eval.h, hmc.h,
+// nuts.h).  Not part of the C-ABI.
+#pragma once
+#include <stdint.h>
+#include "../../include/mcmc355.h"
+
+namespace mc {
+
+// Operand of a fused term (see mc_operand in mcmc355.h).  `unique` is set by
+// the program builder for GATHER operands whose index is injective inside the
+// term (each parameter element receives at most one cotangent).
+struct DevOperand {
+    int32_t kind;
+    int32_t poff;
+    int64_t pool;
+    float cval;
+    int32_t unique;
+};
+
+// Pass mask bits: which cotangents a sweep over the term accumulates.  Terms
+// whose accumulating vector operands touch overlapping parameter ranges are
+// swept once per conflict-free operand group (deterministic, no atomics).
+enum : uint32_t {
+    PASS_VALUE = 1u,
+    PASS_LOC = 2u,
+    PASS_SCALE = 4u,
+    PASS_LP = 8u,
+};
+
+struct DevTerm {
+    int32_t dist;
+    int32_t primary;   // operand slot (0 value, 1 loc, 2 scale) of the
+                       // non-injective GATHER the term is sorted by, or -1
+    int64_t n;
+    float weight;
+    float c0;          // f32 normaliser: -0.5 log(2 pi)  [+ log 2 for HalfNormal]
+    int32_t npass;
+    uint32_t pass_mask[3];
+    DevOperand op[3];  // value, loc, scale
+};
+
+struct DevCtx {
+    const DevTerm* terms;
+    int32_t n_terms;
+    int32_t D;
+    float lp_const;
+    int32_t pad;
+    const float* data;
+    const int32_t* index;
+};
+
+// Per-launch constants shared by the sampler kernels.
+struct RunArgs {
+    mc_run_config cfg;
+    int32_t dpad;          // D rounded up to 16 floats (arena stride unit)
+    int32_t lds_floats;    // LDS floats per chain group
+};
+
+struct TraceDev {
+    int64_t iter_begin;
+    int64_t capacity;
+    uint8_t* accepted;
+    float* accept_stat;
+    double* step_size;
+    float* energy;
+    int32_t* tree_depth;
+    int32_t* n_leapfrog;
+};
+
+constexpr int kMaxTreeDepth = 16;
+
+}  // namespace mc

@@ -1,0 +1,87 @@
+"""High-level MCMC facade — drop-in for mlx_mcmc/inference/mcmc.py:10-246.
+
+``MCMC(log_prob_fn).run(...)`` dispatches ``method='hmc'`` / ``'nuts'`` to
+the MI355X kernels exactly as the reference's branches do (mcmc.py:83-133):
+``key`` is built from ``random_seed``, extra kwargs go to the sampler,
+samples are stored as NumPy arrays in ``.samples`` and the rate in
+``.acceptance_rate``.  ``summary`` / ``print_summary`` follow mcmc.py:191-246.
+
+``method='metropolis'`` (the reference default, mcmc.py:43,135-189) is not on
+the GPU hot path this engine covers and raises
+``NotImplementedError``; unknown methods raise ``ValueError`` (mcmc.py:138).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .. import random as _random
+from ..kernels.hmc import hmc
+from ..kernels.nuts import nuts
+
+
+class MCMC:
+    """High-level MCMC inference interface."""
+
+    def __init__(self, log_prob_fn):
+        self.log_prob_fn = log_prob_fn
+        self.samples = None
+        self.acceptance_rate = None
+        self.info = None
+
+    def run(self, initial_params, num_samples=1000, num_warmup=1000, method='metropolis',
+            proposal_scale=0.1, random_seed=0, verbose=True, **kwargs):
+        if method in ('hmc', 'nuts'):
+            if verbose:
+                print(f"\n{'=' * 70}")
+                print(f"MLX-MCMC: {method.upper()} Sampling")
+                print(f"{'=' * 70}\n")
+            sampler = hmc if method == 'hmc' else nuts
+            kwargs = dict(kwargs)
+            kwargs['return_info'] = True
+            samples, accept_rate, info = sampler(
+                self.log_prob_fn, initial_params, num_samples=num_samples,
+                num_warmup=num_warmup, key=_random.key(random_seed), **kwargs)
+            self.samples = {k: np.array(v) for k, v in samples.items()}
+            self.acceptance_rate = accept_rate
+            self.info = info
+            if verbose:
+                print(f"\n{'=' * 70}")
+                print("Sampling complete!")
+                print(f"{'=' * 70}\n")
+            return self.samples
+        if method == 'metropolis':
+            raise NotImplementedError(
+                "method='metropolis' is not implemented on the MI355X engine (its hot path is "
+                "gradient-based HMC/NUTS); use method='hmc' or method='nuts'")
+        raise ValueError(f"Unknown sampling method: {method}")
+
+    def summary(self, credible_interval=0.95):
+        if self.samples is None:
+            raise ValueError("Must run sampling first. Call run() method.")
+        alpha = 1 - credible_interval
+        lower_pct = 100 * alpha / 2
+        upper_pct = 100 * (1 - alpha / 2)
+        summary = {}
+        for name, s in self.samples.items():
+            summary[name] = {
+                'mean': float(np.mean(s)),
+                'std': float(np.std(s)),
+                'median': float(np.median(s)),
+                f'{lower_pct:.1f}%': float(np.percentile(s, lower_pct)),
+                f'{upper_pct:.1f}%': float(np.percentile(s, upper_pct)),
+            }
+        return summary
+
+    def print_summary(self, credible_interval=0.95):
+        summary = self.summary(credible_interval)
+        print("\nPosterior Summary:")
+        print("=" * 80)
+        print(f"{'Parameter':<15} {'Mean':<10} {'Std':<10} {'Median':<10} "
+              f"{f'{int(credible_interval * 100)}% CI':<20}")
+        print("-" * 80)
+        for name, st in summary.items():
+            vals = list(st.values())
+            ci = f"[{vals[3]:.3f}, {vals[4]:.3f}]"
+            print(f"{name:<15} {st['mean']:<10.3f} {st['std']:<10.3f} {st['median']:<10.3f} "
+                  f"{ci:<20}")
+        print("=" * 80)

@@ -1,0 +1,40 @@
+"""No-U-Turn Sampler on MI355X — drop-in for mlx_mcmc/kernels/nuts.py:16-358.
+
+Same signature, defaults, return value and progress output as the
+reference's ``nuts()`` (slice NUTS, Hoffman & Gelman 2014 Alg. 3, dual
+averaging).  Tree building runs iteratively inside the persistent HIP kernel
+``k_nuts`` (csrc/nuts.h), one chain per chain group.
+
+``slice_mode="reference"`` (default) reproduces the reference's float32
+slice variable, which switches the slice test off once log u < ~-103.97
+(nuts.py:236-237); ``"exact"`` keeps log u in double precision.
+Keyword-only additions as for ``hmc()``.
+"""
+from __future__ import annotations
+
+from ._driver import run_sampler
+
+DELTA_MAX = 1000.0  # nuts.py:13 (the kernel uses the same constant)
+
+
+def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_size=0.1,
+         max_tree_depth=10, adapt_step_size=True, target_accept=0.65, key=None, *,
+         num_chains=1, chain_offset=0, slice_mode="reference", progress=True,
+         return_info=False, return_trace=False, keep_on_device=False,
+         initial_positions=None):
+    """No-U-Turn Sampler (NUTS) for efficient HMC sampling.
+
+    Returns ``(samples, acceptance_rate)`` like the reference, where the rate
+    is the fraction of sampling iterations whose mean acceptance statistic
+    exceeds 0.5 (nuts.py:347).
+    """
+    samples, rate, info = run_sampler(
+        "nuts", log_prob_fn, initial_params, num_samples=num_samples, num_warmup=num_warmup,
+        step_size=step_size, target_accept=target_accept, adapt_step_size=adapt_step_size,
+        key=key, max_tree_depth=max_tree_depth, num_chains=num_chains,
+        chain_offset=chain_offset, slice_mode=slice_mode, progress=progress,
+        return_trace=return_trace, keep_on_device=keep_on_device,
+        initial_positions=initial_positions)
+    if return_info:
+        return samples, rate, info
+    return samples, rate

@@ -1,0 +1,162 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Bars (stated per test): bit-exact for integer work (Philox words), exact or
+<= 1 ulp for the draw transforms, fp32 tolerances for the tape (different
+summation order than the oracle's autograd), identical accept / tree
+decisions until the first near-tie for the sampler traces.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import workloads as W
+from oracle import philox as R
+from oracle import samplers as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from mlx_mcmc_amd import _lib
+
+    return _lib
+
+
+def _rng(gpu, seed, chain, it, tag, sub, index0, n, mode):
+    import torch
+
+    L = _lib()
+    dt = torch.int32 if mode == 0 else torch.float32
+    out = torch.empty(4 * n, dtype=dt, device=gpu)
+    L.check(L.load().mc_rng_fill(seed, chain, it, tag, sub, index0, n, mode, L.ptr(out),
+                                 L.stream_handle()))
+    return out.cpu().numpy()
+
+
+def test_philox_words_bit_exact(gpu):
+    seed = 0x123456789ABCDEF
+    got = _rng(gpu, seed, 5, 77, R.TAG_MOMENTUM, 3, 10, 4096, 0).view(np.uint32).reshape(-1, 4)
+    ref = R.draw(seed, 5, 77, R.TAG_MOMENTUM, 3, 10 + np.arange(4096))
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_uniform_and_normal_transforms(gpu):
+    seed = 42
+    u = _rng(gpu, seed, 1, 2, R.TAG_ACCEPT, 0, 0, 4096, 1).reshape(-1, 4)
+    ref_w = R.draw(seed, 1, 2, R.TAG_ACCEPT, 0, np.arange(4096))
+    np.testing.assert_array_equal(u, R.u01_f32(ref_w))          # exact
+    z = _rng(gpu, seed, 1, 2, R.TAG_ACCEPT, 0, 0, 4096, 2).reshape(-1, 4)
+    zr = R.normals4(ref_w)
+    ulp = np.abs(z.view(np.int32).astype(np.int64) - zr.view(np.int32).astype(np.int64))
+    assert ulp.max() <= 1                                        # f64 libm vs ocml
+    assert (ulp == 0).mean() > 0.999
+
+
+def _tape_case(name):
+    if name == "simple":
+        return W.simple_normal(W.ns_product()), W.simple_normal(W.ns_oracle())
+    if name == "iso":
+        return W.iso_normal(W.ns_product()), W.iso_normal(W.ns_oracle())
+    if name == "illcond":
+        return W.illcond_normal(W.ns_product()), W.illcond_normal(W.ns_oracle())
+    G, N = W.SHAPES[name]
+    return W.hierarchical(W.ns_product(), G, N), W.hierarchical(W.ns_oracle(), G, N)
+
+
+@pytest.mark.parametrize("name", ["simple", "iso", "illcond", "small", "medium", "large"])
+def test_tape_matches_autograd(gpu, name):
+    """log p and its gradient at random points: GPU tape vs torch autograd (fp32).
+
+    Tolerance: |dlp| <= 2e-6 * sum_i |lp_i| (+1e-4), grad components within
+    rtol 1e-4 + 1e-5 * max|grad| — both fp32 sums of the same terms in
+    different orders."""
+    from mlx_mcmc_amd import _engine, _trace
+
+    (plp, pinit), (olp, oinit) = _tape_case(name)
+    prog = _trace.compile_model(plp, pinit)
+    M = S.EagerModel(olp, oinit)
+    rng = np.random.default_rng(0)
+    q0 = M.flatten(oinit)
+    pts = np.stack([q0 + rng.normal(0, 0.3, q0.size).astype(np.float32) for _ in range(4)])
+    if name in ("simple",):
+        pts[:, 1] = np.abs(pts[:, 1]) + 0.5
+    if name in ("small", "medium", "large"):
+        pts[:, 1:3] = np.abs(pts[:, 1:3]) + 0.5
+    lp, g = _engine.logp_grad(prog, pts)
+    lp, g = lp.cpu().numpy(), g.cpu().numpy()
+    for i, q in enumerate(pts):
+        rl, rg = M.logp_grad(q)
+        scale = float(np.abs(rl)) + 1.0
+        assert abs(lp[i] - rl) <= 2e-6 * scale * max(1.0, np.sqrt(q.size / 100)) + 1e-4, \
+            (lp[i], rl)
+        np.testing.assert_allclose(g[i], rg, rtol=1e-4, atol=1e-5 * np.abs(rg).max() + 1e-5)
+
+
+def test_dist_log_prob_kats(gpu):
+    """tests/test_distributions.py:18-32,67-79 of the reference, on the GPU path."""
+    import mlx_mcmc_amd as m
+
+    assert np.isclose(float(m.Normal(0, 1).log_prob(0.0)), -0.5 * np.log(2 * np.pi),
+                      rtol=1e-5)
+    assert np.isclose(float(m.Normal(0, 1).log_prob(1.0)), float(m.Normal(0, 1).log_prob(-1.0)),
+                      rtol=1e-5)
+    assert float(m.HalfNormal(1.0).log_prob(-1.0)) == -np.inf
+    assert np.isclose(float(m.HalfNormal(1.0).log_prob(0.0)),
+                      np.log(2.0) - 0.5 * np.log(2 * np.pi), rtol=1e-5)
+    assert float(m.HalfNormal(1.0).log_prob(0.5)) < 0
+
+
+def _first_divergence(a, b):
+    for i, (x, y) in enumerate(zip(a, b)):
+        if bool(x) != bool(y):
+            return i
+    return None
+
+
+def test_hmc_trace_parity_simple(gpu):
+    """Config 1: same draws -> same accept decisions and bit-identical eps
+    sequence, until a near-tie (|log u - ratio| within fp32 noise)."""
+    import mlx_mcmc_amd as m
+
+    plp, pinit = W.simple_normal(W.ns_product())
+    olp, oinit = W.simple_normal(W.ns_oracle())
+    n_w, n_s = 100, 100
+    _, _, info = m.hmc(plp, pinit, num_samples=n_s, num_warmup=n_w, key=m.random.key(3),
+                       progress=False, return_info=True, return_trace=True)
+    ref = S.hmc(olp, oinit, num_samples=n_s, num_warmup=n_w, seed=3)
+    ga = info.trace["accepted"][0].astype(bool)
+    d = _first_divergence(ga, ref.trace["accepted"])
+    upto = len(ga) if d is None else d
+    assert upto >= 50, f"decisions diverged at iteration {d}"
+    np.testing.assert_array_equal(info.trace["step_size"][0][:upto],
+                                  np.array(ref.trace["step_size"][:upto]))
+    np.testing.assert_allclose(info.trace["accept_stat"][0][:upto],
+                               np.array(ref.trace["ratio"][:upto]), rtol=1e-3, atol=2e-3)
+
+
+def test_nuts_trace_parity_illcond(gpu):
+    """Config 5 (kappa = 1000, slice active): identical tree depths and leaf
+    counts until the first near-tie."""
+    import mlx_mcmc_amd as m
+
+    plp, pinit = W.illcond_normal(W.ns_product())
+    olp, oinit = W.illcond_normal(W.ns_oracle())
+    n_w, n_s = 30, 10
+    _, _, info = m.nuts(plp, pinit, num_samples=n_s, num_warmup=n_w, key=m.random.key(11),
+                        progress=False, return_info=True, return_trace=True)
+    ref = S.nuts(olp, oinit, num_samples=n_s, num_warmup=n_w, seed=11)
+    depth = info.trace["tree_depth"][0]
+    leaves = info.trace["n_leapfrog"][0]
+    same = 0
+    for i in range(n_w + n_s):
+        if depth[i] != ref.trace["depth"][i] or leaves[i] != ref.trace["leaves"][i]:
+            break
+        same += 1
+    assert same >= 10, f"trees diverged at iteration {same}"
+    # alpha feeds dual averaging, so fp32 differences in H (summation order)
+    # are amplified iteration by iteration; the first iterations agree closely
+    np.testing.assert_allclose(info.trace["accept_stat"][0][:8],
+                               np.array(ref.trace["alpha"][:8]), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(info.trace["step_size"][0][:8],
+                               np.array(ref.trace["step_size"][:8]), rtol=3e-4)  # x sqrt(m+1)/gamma gain

@@ -1,0 +1,106 @@
+"""Synthetic workloads of BASELINE.json's configs, as model factories.
+
+Each factory takes a namespace ``ns`` with ``Normal``, ``HalfNormal`` and ``sum``
+— the product (``ns_product()``: mlx_mcmc_amd) or the CPU oracle
+(``ns_oracle()``: oracle.ns) — and returns ``(log_prob_fn, initial_params)``,
+so the same model definition is traced for the GPU and differentiated by
+autograd on the CPU.  Data are fixed synthetic draws (no datasets).
+"""
+from __future__ import annotations
+
+from types import SimpleNamespace
+
+import numpy as np
+
+
+def ns_product():
+    import mlx_mcmc_amd as m
+    import mlx_mcmc_amd.core as mx
+
+    return SimpleNamespace(Normal=m.Normal, HalfNormal=m.HalfNormal, sum=mx.sum,
+                           array=mx.array, name="product")
+
+
+def ns_oracle():
+    from oracle import ns
+
+    return SimpleNamespace(Normal=ns.Normal, HalfNormal=ns.HalfNormal, sum=ns.sum,
+                           array=ns.array, name="oracle")
+
+
+# ---- config 1: examples/01_simple_normal.py:26-50 (vectorised as in
+#      examples/02_hmc_comparison.py:40-52) ------------------------------------
+def simple_normal_data(n=100):
+    np.random.seed(42)
+    return np.random.normal(5.0, 2.0, n)
+
+
+def simple_normal(ns, n=100):
+    data = simple_normal_data(n)
+
+    def log_prob(params):
+        mu = params["mu"]
+        sigma = params["sigma"]
+        lp = ns.Normal(0, 10).log_prob(mu) + ns.HalfNormal(5).log_prob(sigma)
+        return lp + ns.sum(ns.Normal(mu, sigma).log_prob(ns.array(data)))
+
+    return log_prob, {"mu": 0.0, "sigma": 1.0}
+
+
+# ---- config 2: isotropic D-dim standard normal --------------------------------
+def iso_normal(ns, D=100):
+    def log_prob(params):
+        return ns.sum(ns.Normal(0, 1).log_prob(params["x"]))
+
+    return log_prob, {"x": np.zeros(D, np.float32)}
+
+
+# ---- configs 3/4: hierarchical Normal (README "Large" row) ---------------------
+SHAPES = {"small": (7, 1_000), "medium": (97, 10_000), "large": (997, 100_000)}
+
+
+def hierarchical_data(G, N, seed=0):
+    rng = np.random.default_rng(seed)
+    group = (np.arange(N, dtype=np.int64) * G) // N
+    theta_true = rng.normal(1.0, 2.0, G)
+    y = rng.normal(theta_true[group], 1.0).astype(np.float32)
+    return y, group.astype(np.int32)
+
+
+def hierarchical(ns, G=997, N=100_000, seed=0):
+    y, group = hierarchical_data(G, N, seed)
+
+    def log_prob(params):
+        mu, tau, sigma, theta = params["mu"], params["tau"], params["sigma"], params["theta"]
+        lp = ns.Normal(0, 10).log_prob(mu)
+        lp = lp + ns.HalfNormal(5).log_prob(tau)
+        lp = lp + ns.HalfNormal(5).log_prob(sigma)
+        lp = lp + ns.sum(ns.Normal(mu, tau).log_prob(theta))
+        lp = lp + ns.sum(ns.Normal(theta[group], sigma).log_prob(y))
+        return lp
+
+    sums = np.bincount(group, weights=y, minlength=G)
+    counts = np.bincount(group, minlength=G)
+    gm = (sums / np.maximum(counts, 1)).astype(np.float32)
+    init = {"mu": np.float32(gm.mean()), "tau": np.float32(gm.std()),
+            "sigma": np.float32(1.0), "theta": gm}
+    return log_prob, init
+
+
+def hierarchical_flops_per_step(G, N):
+    """SURVEY §8d canonical algorithmic FP32 flops per chain-leapfrog-step."""
+    return 5 * N + 13 * (G + 3)
+
+
+# ---- config 5: ill-conditioned diagonal Gaussian (kappa = 1000) ----------------
+def illcond_scales(D=100):
+    return (10.0 ** (-1.5 * np.arange(D) / (D - 1))).astype(np.float32)
+
+
+def illcond_normal(ns, D=100):
+    scales = illcond_scales(D)
+
+    def log_prob(params):
+        return ns.sum(ns.Normal(0, scales).log_prob(params["x"]))
+
+    return log_prob, {"x": np.zeros(D, np.float32)}
