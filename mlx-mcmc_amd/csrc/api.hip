@@ -86,6 +86,128 @@ static int choose_wpc(int64_t max_n) {
     return 16;
 }
 
+// Segment-tiled layout of a term sorted by its primary (non-injective) gather
+// index; see DevTerm in internal.h.  Runs of equal index ("segments") are
+// split into at most ceil(len / Lt) near-equal virtual segments so that a
+// chain group of T threads has ~2T lanes of work even for few, long groups;
+// with >= 2T segments nothing is split and each lane writes its group's
+// gradient directly.
+static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<int32_t>& ipool,
+                          int T) {
+    const int a = dt.primary;
+    const int64_t n = dt.n;
+    const int64_t ip = dt.op[a].pool;
+    std::vector<int64_t> sstart;
+    std::vector<int32_t> sk;
+    for (int64_t i = 0; i < n; ++i)
+        if (i == 0 || ipool[ip + i] != ipool[ip + i - 1]) {
+            sstart.push_back(i);
+            sk.push_back(ipool[ip + i]);
+        }
+    const int64_t G = (int64_t)sstart.size();
+    sstart.push_back(n);
+    const int64_t Lt = (G >= 2 * (int64_t)T) ? INT64_MAX
+                                             : std::max<int64_t>(1, (n + 2 * T - 1) / (2 * T));
+    struct V {
+        int32_t k;
+        int64_t start;
+        int32_t len;
+    };
+    std::vector<V> vs;
+    std::vector<int32_t> comb;
+    bool split = false;
+    for (int64_t g = 0; g < G; ++g) {
+        const int64_t len = sstart[g + 1] - sstart[g];
+        const int64_t pieces = (Lt == INT64_MAX) ? 1 : (len + Lt - 1) / Lt;
+        if (pieces > 1) split = true;
+        const int64_t base = len / pieces, rem = len % pieces;
+        comb.push_back(sk[g]);
+        comb.push_back((int32_t)vs.size());
+        comb.push_back((int32_t)pieces);
+        int64_t st = sstart[g];
+        for (int64_t pc = 0; pc < pieces; ++pc) {
+            const int64_t pl = base + (pc < rem ? 1 : 0);
+            if (pl > INT32_MAX) return fail(MC_ERR_UNSUPPORTED, "segment too long");
+            vs.push_back({sk[g], st, (int32_t)pl});
+            st += pl;
+        }
+    }
+    const int64_t nv = (int64_t)vs.size();
+    const int64_t ntiles = (nv + 63) / 64;
+    std::vector<int32_t> tiles(3 * ntiles), lanes(2 * nv);
+    int64_t total = 0;
+    for (int64_t t = 0; t < ntiles; ++t) {
+        int32_t lmax = 0, lmin = INT32_MAX;
+        for (int l = 0; l < 64; ++l) {
+            const int64_t v = t * 64 + l;
+            const int32_t len = v < nv ? vs[v].len : 0;
+            lmax = std::max(lmax, len);
+            lmin = std::min(lmin, len);
+        }
+        const int32_t lpad = (lmax + 3) / 4 * 4;
+        if (total > INT32_MAX - 64 * (int64_t)lpad)
+            return fail(MC_ERR_UNSUPPORTED, "segmented term too large");
+        tiles[3 * t] = (int32_t)total;
+        tiles[3 * t + 1] = lpad;
+        tiles[3 * t + 2] = lmin;
+        total += 64 * (int64_t)lpad;
+    }
+    for (int64_t v = 0; v < nv; ++v) {
+        lanes[2 * v] = vs[v].k;
+        lanes[2 * v + 1] = vs[v].len;
+    }
+    // parameter slices become identity gathers so that they can be tiled too
+    for (int b = 0; b < 3; ++b) {
+        DevOperand& d = dt.op[b];
+        if (b == a || d.kind != MC_OP_PVEC) continue;
+        const int64_t base = (int64_t)ipool.size();
+        for (int64_t i = 0; i < n; ++i) ipool.push_back((int32_t)i);
+        d.kind = MC_OP_GATHER;
+        d.pool = base;
+        d.unique = 1;
+    }
+    // tiled copies of every other vector operand
+    for (int b = 0; b < 3; ++b) {
+        DevOperand& d = dt.op[b];
+        if (b == a || (d.kind != MC_OP_DATA && d.kind != MC_OP_GATHER)) continue;
+        if (d.kind == MC_OP_DATA) {
+            while (dpool.size() % 64) dpool.push_back(0.0f);
+            const int64_t base = (int64_t)dpool.size();
+            dpool.resize(base + total, 0.0f);
+            for (int64_t v = 0; v < nv; ++v) {
+                const int64_t t = v / 64, l = v % 64;
+                for (int32_t u = 0; u < vs[v].len; ++u)
+                    dpool[base + tiles[3 * t] + (u >> 2) * 256 + l * 4 + (u & 3)] =
+                        dpool[d.pool + vs[v].start + u];
+            }
+            d.pool = base;
+        } else {
+            while (ipool.size() % 64) ipool.push_back(0);
+            const int64_t base = (int64_t)ipool.size();
+            ipool.resize(base + total, 0);
+            for (int64_t v = 0; v < nv; ++v) {
+                const int64_t t = v / 64, l = v % 64;
+                for (int32_t u = 0; u < vs[v].len; ++u)
+                    ipool[base + tiles[3 * t] + (u >> 2) * 256 + l * 4 + (u & 3)] =
+                        ipool[d.pool + vs[v].start + u];
+            }
+            d.pool = base;
+        }
+    }
+    dt.ntiles = (int32_t)ntiles;
+    dt.nvirt = (int32_t)nv;
+    dt.ncomb = split ? (int32_t)G : 0;
+    dt.tile_base = (int64_t)ipool.size();
+    ipool.insert(ipool.end(), tiles.begin(), tiles.end());
+    dt.lane_base = (int64_t)ipool.size();
+    ipool.insert(ipool.end(), lanes.begin(), lanes.end());
+    dt.comb_base = (int64_t)ipool.size();
+    if (split) ipool.insert(ipool.end(), comb.begin(), comb.end());
+    if (nv > 4 * (int64_t)T && split)
+        return fail(MC_ERR_UNSUPPORTED, "internal: too many virtual segments");
+    return MC_OK;
+}
+
 extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t n_params,
                                  float lp_const, const float* data, int64_t n_data,
                                  const int32_t* index, int64_t n_index, mc_program** out) {
@@ -100,6 +222,8 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
     std::vector<int32_t> ipool(index, index + n_index);
     std::vector<DevTerm> dts;
     int64_t max_n = 0;
+    for (int32_t t = 0; t < n_terms; ++t) max_n = std::max<int64_t>(max_n, terms[t].n);
+    const int wpc = choose_wpc(max_n);
 
     for (int32_t t = 0; t < n_terms; ++t) {
         const mc_term& src = terms[t];
@@ -248,7 +372,10 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
         }
         dt.npass = npass;
         for (int ps = 0; ps < 3; ++ps) dt.pass_mask[ps] = masks[ps];
-        max_n = std::max(max_n, n);
+        if (primary >= 0) {
+            const int rc = build_segments(dt, dpool, ipool, 64 * wpc);
+            if (rc) return rc;
+        }
         dts.push_back(dt);
     }
 
@@ -256,7 +383,7 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
     p->D = n_params;
     p->lp_const = lp_const;
     p->max_n = max_n;
-    p->wpc = choose_wpc(max_n);
+    p->wpc = wpc;
     p->terms = dts;
     hipError_t e = hipSuccess;
     if (!dts.empty()) {

@@ -10,6 +10,20 @@
 // with one sweep per term: forward value and hand-written VJP in the same
 // loop, cotangents reduced in registers / LDS in a fixed order (no float
 // atomics, so every evaluation is bit-reproducible).
+//
+// Two element mappings:
+//   strided    element i -> thread i mod T (coalesced), for terms without a
+//              non-injective gather;
+//   segmented  terms gathered through a sorted group index (hierarchical
+//              likelihoods): each lane owns one run of one group in a
+//              host-built tiled layout, keeps theta_group in a register and
+//              sums the group's cotangent in a register (csrc/api.hip
+//              build_segments).
+// Terms with a broadcast (uniform) scale accumulate moments per lane —
+// count, sum d, sum d^2 with d = value - loc — and form log p and every
+// cotangent from them once per lane: the per-element work is 3 VALU ops and
+// there is no per-element division.  This is the same arithmetic as the
+// per-element formulas up to fp32 rounding order.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "internal.h"
@@ -60,12 +74,10 @@ struct Group {
     }
 };
 
-// LDS scratch used by the deterministic segmented sum of a sorted gather.
+// LDS scratch of a chain group beyond the reduction slots: the per-virtual-
+// segment partial cotangents of a split segmented term (<= 4T floats).
 struct SegScratch {
-    int* kf;    // first run's segment of each thread's piece (-1: empty)
-    float* af;  // its partial cotangent
-    int* kl;    // last run's segment (== kf when the piece has one run)
-    float* al;
+    float* vpart;
 };
 
 struct ElemOut {
@@ -116,8 +128,74 @@ MC_DEV float uniform_value(const DevOperand& o, const float* q) {
     return 0.0f;
 }
 
-MC_DEV int gidx(const DevOperand& o, const DevCtx& P, int64_t i) {
-    return P.index[o.pool + i];
+// Per-lane moments of d = value - loc (Normal) or of the value (HalfNormal)
+// for a term with a broadcast scale.
+struct Moments {
+    float cnt, s1, s2;
+    bool neg;  // HalfNormal: some value < 0 (log p = -inf)
+};
+
+// log p and the broadcast-operand cotangents from the moments (per lane).
+MC_DEV void finish_moments(const DevTerm& T, uint32_t mask, float s, float logs,
+                           const Moments& M, float& lp_acc, float& pv, float& pm, float& ps) {
+    const float w = T.weight;
+    const float var = s * s;
+    if (mask & PASS_LP) {
+        const float lpt = M.neg ? -__builtin_inff() : (M.cnt * (T.c0 - logs) - (0.5f * M.s2) / var);
+        lp_acc += w * lpt;
+    }
+    if ((mask & PASS_VALUE) && T.op[0].kind == MC_OP_PSCALAR) pv += -(w * (M.s1 / var));
+    if ((mask & PASS_LOC) && T.op[1].kind == MC_OP_PSCALAR) pm += w * (M.s1 / var);
+    if ((mask & PASS_SCALE) && T.op[2].kind == MC_OP_PSCALAR)
+        ps += w * (M.s2 / (var * s) - M.cnt / s);
+}
+
+// ---------------------------------------------------------------------------
+// strided mapping
+// ---------------------------------------------------------------------------
+// VK / LK: 0 broadcast, 1 DATA, 2 PVEC.  Broadcast scale.
+template <int DIST, int VK, int LK>
+MC_DEV void strided_uscale(const DevTerm& T, const DevCtx& P, const float* q, float* g, int tid,
+                           int nthr, uint32_t mask, float uv, float um, float var, Moments& M) {
+    const float* vd = (VK == 1) ? P.data + T.op[0].pool : (VK == 2 ? q + T.op[0].poff : nullptr);
+    const float* ld = (LK == 1) ? P.data + T.op[1].pool : (LK == 2 ? q + T.op[1].poff : nullptr);
+    float* gv = (VK == 2 && (mask & PASS_VALUE)) ? g + T.op[0].poff : nullptr;
+    float* gl = (LK == 2 && (mask & PASS_LOC)) ? g + T.op[1].poff : nullptr;
+    const float w = T.weight;
+    const int64_t n = T.n;
+    float s1 = 0.0f, s2 = 0.0f, cnt = 0.0f;
+    bool neg = false;
+    for (int64_t i = tid; i < n; i += nthr) {
+        const float v = (VK == 0) ? uv : vd[i];
+        if constexpr (DIST == MC_DIST_NORMAL) {
+            const float m = (LK == 0) ? um : ld[i];
+            const float d = v - m;
+            s2 = fmaf(d, d, s2);
+            s1 += d;
+            if (VK == 2 && gv) gv[i] += -((w * d) / var);
+            if (LK == 2 && gl) gl[i] += (w * d) / var;
+        } else {
+            if (v >= 0.0f) {
+                s2 = fmaf(v, v, s2);
+                s1 += v;
+                cnt += 1.0f;
+                if (VK == 2 && gv) gv[i] += -((w * v) / var);
+            } else {
+                neg = true;
+            }
+        }
+    }
+    if constexpr (DIST == MC_DIST_NORMAL) {
+        cnt = (tid < n) ? (float)((n - 1 - tid) / nthr + 1) : 0.0f;
+    }
+    M.s1 += s1;
+    M.s2 += s2;
+    M.cnt += cnt;
+    M.neg = M.neg || neg;
+}
+
+MC_DEV int fast_kind(int kind) {
+    return kind == MC_OP_DATA ? 1 : (kind == MC_OP_PVEC ? 2 : (is_vec(kind) ? -1 : 0));
 }
 
 MC_DEV float fetch(const DevOperand& o, int64_t i, float uni, const float* q, const DevCtx& P) {
@@ -127,13 +205,13 @@ MC_DEV float fetch(const DevOperand& o, int64_t i, float uni, const float* q, co
         case MC_OP_PVEC:
             return q[o.poff + i];
         case MC_OP_GATHER:
-            return q[o.poff + gidx(o, P, i)];
+            return q[o.poff + P.index[o.pool + i]];
         default:
             return uni;
     }
 }
 
-// Accumulate a per-element cotangent for operand o (not the sorted primary).
+// Accumulate a per-element cotangent for operand o (never the primary).
 MC_DEV void accum(const DevOperand& o, int64_t i, float c, float& scalar_part, float* g,
                   const DevCtx& P) {
     switch (o.kind) {
@@ -144,13 +222,185 @@ MC_DEV void accum(const DevOperand& o, int64_t i, float c, float& scalar_part, f
             g[o.poff + i] += c;
             break;
         case MC_OP_GATHER:
-            g[o.poff + gidx(o, P, i)] += c;
+            g[o.poff + P.index[o.pool + i]] += c;
             break;
         default:
             break;
     }
 }
 
+// Generic per-element path (vector scale, injective gathers): full formulas.
+MC_DEV void strided_generic(const DevTerm& T, const DevCtx& P, const float* q, float* g, int tid,
+                            int nthr, uint32_t mask, float uv, float um, float us, float ulogs,
+                            float& lp_acc, float& pv, float& pm, float& ps) {
+    const bool scale_vec = is_vec(T.op[2].kind);
+    const bool normal = (T.dist == MC_DIST_NORMAL);
+    const float w = T.weight;
+    for (int64_t i = tid; i < T.n; i += nthr) {
+        const float v = fetch(T.op[0], i, uv, q, P);
+        const float m = fetch(T.op[1], i, um, q, P);
+        const float s = fetch(T.op[2], i, us, q, P);
+        const float logs = scale_vec ? logf(s) : ulogs;
+        const ElemOut e = normal ? elem_normal(T.c0, v, m, s, logs)
+                                 : elem_halfnormal(T.c0, v, s, logs);
+        if (mask & PASS_LP) lp_acc += w * e.lp;
+        if (mask & PASS_VALUE) accum(T.op[0], i, w * e.dv, pv, g, P);
+        if (mask & PASS_LOC) accum(T.op[1], i, w * e.dm, pm, g, P);
+        if (mask & PASS_SCALE) accum(T.op[2], i, w * e.ds, ps, g, P);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// segmented mapping (terms grouped by a sorted, non-injective gather)
+// ---------------------------------------------------------------------------
+MC_DEV int64_t seg_elem(int off, int u, int lane) {
+    return (int64_t)off + (u >> 2) * 256 + lane * 4 + (u & 3);
+}
+
+// Fast path: Normal, broadcast scale, primary in slot PV (0 value, 1 loc),
+// the other of value/loc a DATA vector.  Per element: d, d^2 FMA, sum d.
+template <int WPC, int PV>
+MC_DEV void seg_normal_uscale(const DevTerm& T, const DevCtx& P, const float* q, float* g,
+                              const Group<WPC>& G, uint32_t mask, float var, Moments& M,
+                              float* vpart) {
+    const int wave = G.tid >> 6;
+    const int lane = G.tid & 63;
+    const DevOperand& po = T.op[PV];
+    const DevOperand& od = T.op[1 - PV];
+    const int* tiles = P.index + T.tile_base;
+    const int* lanes = P.index + T.lane_base;
+    const float* data = P.data + od.pool;
+    const bool acc_prim = (mask & (1u << PV)) != 0;
+    const bool split = T.ncomb > 0;
+    const float w = T.weight;
+    float s1_all = 0.0f, s2_all = 0.0f, cnt_all = 0.0f;
+    for (int t = wave; t < T.ntiles; t += WPC) {
+        const int off = tiles[3 * t];
+        const int lpad = tiles[3 * t + 1];
+        const int lmin = tiles[3 * t + 2];
+        const int v = t * 64 + lane;
+        const bool valid = v < T.nvirt;
+        const int k = valid ? lanes[2 * v] : 0;
+        const int len = valid ? lanes[2 * v + 1] : 0;
+        const float th = q[po.poff + k];
+        const float4* base = reinterpret_cast<const float4*>(data + off) + lane;
+        float s1 = 0.0f, s2 = 0.0f;
+        int u4 = 0;
+        const int full4 = lmin >> 2;
+        // d = value - loc: x - th when loc is the primary, th - x when value is
+#pragma unroll 4
+        for (; u4 < full4; ++u4) {
+            const float4 x = base[u4 * 64];
+            const float d0 = PV == 1 ? x.x - th : th - x.x;
+            const float d1 = PV == 1 ? x.y - th : th - x.y;
+            const float d2 = PV == 1 ? x.z - th : th - x.z;
+            const float d3 = PV == 1 ? x.w - th : th - x.w;
+            s2 = fmaf(d0, d0, s2);
+            s1 += d0;
+            s2 = fmaf(d1, d1, s2);
+            s1 += d1;
+            s2 = fmaf(d2, d2, s2);
+            s1 += d2;
+            s2 = fmaf(d3, d3, s2);
+            s1 += d3;
+        }
+        for (; 4 * u4 < lpad; ++u4) {
+            const float4 x = base[u4 * 64];
+            const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (4 * u4 + e < len) {
+                    const float d = PV == 1 ? xs[e] - th : th - xs[e];
+                    s2 = fmaf(d, d, s2);
+                    s1 += d;
+                }
+            }
+        }
+        s1_all += s1;
+        s2_all += s2;
+        cnt_all += (float)len;
+        if (valid && acc_prim) {
+            const float c = PV == 1 ? w * (s1 / var) : -(w * (s1 / var));
+            if (split) vpart[v] = c;
+            else g[po.poff + k] += c;
+        }
+    }
+    M.s1 += s1_all;
+    M.s2 += s2_all;
+    M.cnt += cnt_all;
+}
+
+MC_DEV float seg_fetch(const DevOperand& o, int64_t e, float uni, float prim, bool is_prim,
+                       const float* q, const DevCtx& P) {
+    if (is_prim) return prim;
+    switch (o.kind) {
+        case MC_OP_DATA:
+            return P.data[o.pool + e];
+        case MC_OP_GATHER:
+            return q[o.poff + P.index[o.pool + e]];
+        default:
+            return uni;
+    }
+}
+
+// Generic segmented path: full per-element formulas.
+template <int WPC>
+MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float* g,
+                        const Group<WPC>& G, uint32_t mask, float uv, float um, float us,
+                        float ulogs, float& lp_acc, float& pv, float& pm, float& ps,
+                        float* vpart) {
+    const int wave = G.tid >> 6;
+    const int lane = G.tid & 63;
+    const int a = T.primary;
+    const DevOperand po = a == 0 ? T.op[0] : (a == 1 ? T.op[1] : T.op[2]);
+    const int* tiles = P.index + T.tile_base;
+    const int* lanes = P.index + T.lane_base;
+    const bool acc_prim = (mask & (1u << a)) != 0;
+    const bool split = T.ncomb > 0;
+    const bool scale_vec = is_vec(T.op[2].kind);
+    const bool normal = (T.dist == MC_DIST_NORMAL);
+    const float w = T.weight;
+    for (int t = wave; t < T.ntiles; t += WPC) {
+        const int off = tiles[3 * t];
+        const int lpad = tiles[3 * t + 1];
+        const int v = t * 64 + lane;
+        const bool valid = v < T.nvirt;
+        const int k = valid ? lanes[2 * v] : 0;
+        const int len = valid ? lanes[2 * v + 1] : 0;
+        const float th = q[po.poff + k];
+        float cp = 0.0f;
+        for (int u = 0; u < lpad; ++u) {
+            if (u < len) {
+                const int64_t e = seg_elem(off, u, lane);
+                const float vv = seg_fetch(T.op[0], e, uv, th, a == 0, q, P);
+                const float m = seg_fetch(T.op[1], e, um, th, a == 1, q, P);
+                const float s = seg_fetch(T.op[2], e, us, th, a == 2, q, P);
+                const float logs = (scale_vec || a == 2) ? logf(s) : ulogs;
+                const ElemOut o = normal ? elem_normal(T.c0, vv, m, s, logs)
+                                         : elem_halfnormal(T.c0, vv, s, logs);
+                if (mask & PASS_LP) lp_acc += w * o.lp;
+                if (mask & PASS_VALUE) {
+                    if (a == 0) cp += w * o.dv;
+                    else accum(T.op[0], e, w * o.dv, pv, g, P);
+                }
+                if (mask & PASS_LOC) {
+                    if (a == 1) cp += w * o.dm;
+                    else accum(T.op[1], e, w * o.dm, pm, g, P);
+                }
+                if (mask & PASS_SCALE) {
+                    if (a == 2) cp += w * o.ds;
+                    else accum(T.op[2], e, w * o.ds, ps, g, P);
+                }
+            }
+        }
+        if (valid && acc_prim) {
+            if (split) vpart[v] = cp;
+            else g[po.poff + k] += cp;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 template <int WPC>
 MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* g,
                       const Group<WPC>& G, float& lp_acc, const SegScratch& S) {
@@ -159,115 +409,76 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
     const float us = uniform_value(T.op[2], q);
     const bool scale_vec = is_vec(T.op[2].kind);
     const float ulogs = scale_vec ? 0.0f : logf(us);
-    const float w = T.weight;
+    const float var = us * us;
     const bool normal = (T.dist == MC_DIST_NORMAL);
 
     for (int pass = 0; pass < T.npass; ++pass) {
         const uint32_t mask =
             pass == 0 ? T.pass_mask[0] : (pass == 1 ? T.pass_mask[1] : T.pass_mask[2]);
         float pv = 0.0f, pm = 0.0f, ps = 0.0f;
-
-        // one element: forward + VJP, accumulate everything except the
-        // sorted primary gather; returns the primary's cotangent.
-        auto element = [&](int64_t i) -> float {
-            const float v = fetch(T.op[0], i, uv, q, P);
-            const float m = fetch(T.op[1], i, um, q, P);
-            const float s = fetch(T.op[2], i, us, q, P);
-            const float logs = scale_vec ? logf(s) : ulogs;
-            const ElemOut e = normal ? elem_normal(T.c0, v, m, s, logs)
-                                     : elem_halfnormal(T.c0, v, s, logs);
-            if (mask & PASS_LP) lp_acc += w * e.lp;
-            const float cv = w * e.dv, cm = w * e.dm, cs = w * e.ds;
-            float cprim = 0.0f;
-            if (mask & PASS_VALUE) {
-                if (T.primary == 0) cprim = cv;
-                else accum(T.op[0], i, cv, pv, g, P);
-            }
-            if (mask & PASS_LOC) {
-                if (T.primary == 1) cprim = cm;
-                else accum(T.op[1], i, cm, pm, g, P);
-            }
-            if (mask & PASS_SCALE) {
-                if (T.primary == 2) cprim = cs;
-                else accum(T.op[2], i, cs, ps, g, P);
-            }
-            return cprim;
-        };
+        Moments M = {0.0f, 0.0f, 0.0f, false};
+        bool moments = false;
 
         if (T.primary < 0) {
-            for (int64_t i = G.tid; i < T.n; i += G.T) (void)element(i);
-        } else {
-            // Elements are sorted by the primary index: each thread takes a
-            // contiguous piece and sums runs of equal index in registers.
-            // Runs strictly inside a piece are owned by the thread; the first
-            // and last run of each piece are combined in thread order below.
-            const DevOperand po =
-                T.primary == 0 ? T.op[0] : (T.primary == 1 ? T.op[1] : T.op[2]);
-            const bool acc_prim = (mask & (1u << T.primary)) != 0;
-            const int64_t n = T.n;
-            const int tact = (int)(n < (int64_t)G.T ? n : (int64_t)G.T);
-            int kf = -1, kl = -1;
-            float af = 0.0f, al = 0.0f;
-            if (G.tid < tact) {
-                const int64_t b = (n * G.tid) / tact;
-                const int64_t e = (n * (G.tid + 1)) / tact;
-                int kcur = -1, nruns = 0;
-                float acc = 0.0f;
-                for (int64_t i = b; i < e; ++i) {
-                    const float c = element(i);
-                    if (acc_prim) {
-                        const int k = gidx(po, P, i);
-                        if (k != kcur) {
-                            if (kcur >= 0) {
-                                if (nruns == 1) {
-                                    kf = kcur;
-                                    af = acc;
-                                } else {
-                                    g[po.poff + kcur] += acc;
-                                }
-                            }
-                            kcur = k;
-                            acc = 0.0f;
-                            ++nruns;
-                        }
-                        acc += c;
-                    }
+            const int fv = fast_kind(T.op[0].kind);
+            const int fl = normal ? fast_kind(T.op[1].kind) : 0;
+            if (!scale_vec && fv >= 0 && fl >= 0) {
+                moments = true;
+                const int code = normal ? (fv * 3 + fl) : (9 + fv);
+                switch (code) {
+#define MC_SU(c, D_, V_, L_)                                                                \
+    case c:                                                                                 \
+        strided_uscale<D_, V_, L_>(T, P, q, g, G.tid, G.T, mask, uv, um, var, M);           \
+        break;
+                    MC_SU(0, MC_DIST_NORMAL, 0, 0)
+                    MC_SU(1, MC_DIST_NORMAL, 0, 1)
+                    MC_SU(2, MC_DIST_NORMAL, 0, 2)
+                    MC_SU(3, MC_DIST_NORMAL, 1, 0)
+                    MC_SU(4, MC_DIST_NORMAL, 1, 1)
+                    MC_SU(5, MC_DIST_NORMAL, 1, 2)
+                    MC_SU(6, MC_DIST_NORMAL, 2, 0)
+                    MC_SU(7, MC_DIST_NORMAL, 2, 1)
+                    MC_SU(8, MC_DIST_NORMAL, 2, 2)
+                    MC_SU(9, MC_DIST_HALFNORMAL, 0, 0)
+                    MC_SU(10, MC_DIST_HALFNORMAL, 1, 0)
+                    MC_SU(11, MC_DIST_HALFNORMAL, 2, 0)
+#undef MC_SU
+                    default:
+                        break;
                 }
-                if (acc_prim) {
-                    if (nruns == 1) {
-                        kf = kcur;
-                        af = acc;
-                    }
-                    kl = kcur;
-                    al = acc;
-                }
+            } else {
+                strided_generic(T, P, q, g, G.tid, G.T, mask, uv, um, us, ulogs, lp_acc, pv, pm,
+                                ps);
             }
-            if (acc_prim) {
-                S.kf[G.tid] = kf;
-                S.af[G.tid] = af;
-                S.kl[G.tid] = kl;
-                S.al[G.tid] = al;
+        } else {
+            float* vpart = S.vpart;
+            const int other_kind = T.primary == 1 ? T.op[0].kind : T.op[1].kind;
+            const bool fast = normal && !scale_vec && T.primary <= 1 && other_kind == MC_OP_DATA;
+            if (fast) {
+                moments = true;
+                if (T.primary == 1)
+                    seg_normal_uscale<WPC, 1>(T, P, q, g, G, mask, var, M, vpart);
+                else
+                    seg_normal_uscale<WPC, 0>(T, P, q, g, G, mask, var, M, vpart);
+            } else {
+                seg_generic<WPC>(T, P, q, g, G, mask, uv, um, us, ulogs, lp_acc, pv, pm, ps,
+                                 vpart);
+            }
+            if (T.ncomb > 0 && (mask & (1u << T.primary))) {
+                // split segments: add the virtual partials in order
                 G.sync();
-                if (G.tid < tact) {
-                    const bool single = (kf == kl);
-                    const bool lead_f = (G.tid == 0) || (S.kl[G.tid - 1] != kf);
-                    // a leader sums the pieces that continue its segment, in order
-                    auto chain = [&](int k, float s) -> float {
-                        for (int t2 = G.tid + 1; t2 < tact && S.kf[t2] == k; ++t2) {
-                            s += S.af[t2];
-                            if (S.kl[t2] != S.kf[t2]) break;
-                        }
-                        return s;
-                    };
-                    if (single) {
-                        if (lead_f) g[po.poff + kf] += chain(kf, af);
-                    } else {
-                        if (lead_f) g[po.poff + kf] += af;
-                        g[po.poff + kl] += chain(kl, al);
-                    }
+                const DevOperand po =
+                    T.primary == 0 ? T.op[0] : (T.primary == 1 ? T.op[1] : T.op[2]);
+                const int* comb = P.index + T.comb_base;
+                for (int c = G.tid; c < T.ncomb; c += G.T) {
+                    const int k = comb[3 * c], vf = comb[3 * c + 1], vc = comb[3 * c + 2];
+                    float s = vpart[vf];
+                    for (int j = 1; j < vc; ++j) s += vpart[vf + j];
+                    g[po.poff + k] += s;
                 }
             }
         }
+        if (moments) finish_moments(T, mask, us, ulogs, M, lp_acc, pv, pm, ps);
 
         // broadcast-parameter cotangents: fixed-order group reduction
         if ((mask & PASS_VALUE) && T.op[0].kind == MC_OP_PSCALAR) {
@@ -295,23 +506,19 @@ MC_DEV float eval_lp_grad(const DevCtx& P, const float* q, float* g, const Group
     G.sync();
     float lp_acc = 0.0f;
     for (int t = 0; t < P.n_terms; ++t) {
-        const DevTerm T = P.terms[t];
+        const DevTerm& T = P.terms[t];
         eval_term<WPC>(T, P, q, g, G, lp_acc, S);
     }
     return G.sum(lp_acc) + P.lp_const;
 }
 
-// LDS floats a chain group needs for reductions + segmented-sum scratch.
+// LDS floats a chain group needs for reductions + segment partials.
 __host__ __device__ constexpr int group_scratch_floats(int wpc) { return 16 + 4 * 64 * wpc; }
 
 template <int WPC>
 MC_DEV void carve_group(float* base, Group<WPC>& G, SegScratch& S) {
-    constexpr int T = 64 * WPC;
     G.red = base;
-    S.kf = reinterpret_cast<int*>(base + 16);
-    S.af = base + 16 + T;
-    S.kl = reinterpret_cast<int*>(base + 16 + 2 * T);
-    S.al = base + 16 + 3 * T;
+    S.vpart = base + 16;
 }
 
 }  // namespace mc

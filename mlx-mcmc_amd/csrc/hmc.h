@@ -47,14 +47,14 @@ k_hmc(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, flo
     float* gB = arena + 3 * Dp;
     float* p = arena + 4 * Dp;
 
-    mc_chain_scalars sc = scal[c];
+    float lp = scal[c].logp;
+    double eps = scal[c].step_size;
+    int n_acc = scal[c].n_accept, n_tot = scal[c].n_total;
+    int warm_acc = scal[c].warmup_accept, warm_tot = scal[c].warmup_total;
     for (int j = G.tid; j < D; j += T) {
         qA[j] = st_q[c * D + j];
         gA[j] = st_g[c * D + j];
     }
-    float lp = sc.logp;
-    double eps = sc.step_size;
-    int n_acc = sc.n_accept, n_tot = sc.n_total;
     G.sync();
 
     const uint32_t chain_id = (uint32_t)(cfg.chain_offset + c);
@@ -62,8 +62,8 @@ k_hmc(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, flo
     const int64_t it_end = cfg.iter_begin + cfg.iter_count;
     for (int64_t it = cfg.iter_begin; it < it_end; ++it) {
         if (it == cfg.num_warmup) {  // hmc.py:175-180
-            sc.warmup_accept = n_acc;
-            sc.warmup_total = n_tot;
+            warm_acc = n_acc;
+            warm_tot = n_tot;
             n_acc = 0;
             n_tot = 0;
         }
@@ -158,12 +158,14 @@ k_hmc(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, flo
         st_g[c * D + j] = gA[j];
     }
     if (G.tid == 0) {
+        mc_chain_scalars& sc = scal[c];
         sc.logp = lp;
         sc.step_size = eps;
         sc.n_accept = n_acc;
         sc.n_total = n_tot;
+        sc.warmup_accept = warm_acc;
+        sc.warmup_total = warm_tot;
         sc.n_grad += cfg.iter_count * (int64_t)L;
-        scal[c] = sc;
     }
 }
 

@@ -31,13 +31,26 @@ enum : uint32_t {
 struct DevTerm {
     int32_t dist;
     int32_t primary;   // operand slot (0 value, 1 loc, 2 scale) of the
-                       // non-injective GATHER the term is sorted by, or -1
+                       // non-injective GATHER the term is grouped by, or -1
     int64_t n;
     float weight;
     float c0;          // f32 normaliser: -0.5 log(2 pi)  [+ log 2 for HalfNormal]
     int32_t npass;
     uint32_t pass_mask[3];
     DevOperand op[3];  // value, loc, scale
+    // ---- segment-tiled layout (primary >= 0) --------------------------------
+    // Elements are grouped by the primary index into runs ("segments"), long
+    // runs split into virtual segments; 64 virtual segments form a tile, one
+    // per lane.  Every vector operand of the term is stored tiled: element u
+    // of lane l of tile t lives at  tile_off[t] + (u/4)*256 + l*4 + u%4,
+    // so a lane walks its own run with coalesced 16-byte loads.
+    int32_t ntiles;
+    int32_t nvirt;
+    int32_t ncomb;        // > 0: segments were split, partials combined in order
+    int32_t pad0;
+    int64_t tile_base;    // index pool: per tile {off, len_pad, len_min}
+    int64_t lane_base;    // index pool: per virtual segment {k, len}
+    int64_t comb_base;    // index pool: per segment {k, vfirst, vcount}
 };
 
 struct DevCtx {
