@@ -49,6 +49,8 @@ struct mc_program {
     int32_t D = 0;
     float lp_const = 0.0f;
     int32_t wpc = 1;
+    int32_t nslots = 1;
+    int64_t sfin_base = 0;
     int64_t max_n = 0;
     std::vector<DevTerm> terms;
     DevTerm* d_terms = nullptr;
@@ -62,9 +64,10 @@ static DevCtx ctx_of(const mc_program* p) {
     c.n_terms = (int32_t)p->terms.size();
     c.D = p->D;
     c.lp_const = p->lp_const;
-    c.pad = 0;
+    c.nslots = p->nslots;
     c.data = p->d_data;
     c.index = p->d_index;
+    c.sfin_base = p->sfin_base;
     return c;
 }
 
@@ -83,7 +86,7 @@ static float c_log2() { return (float)std::log(2.0); }
 static int choose_wpc(int64_t max_n) {
     if (max_n <= 512) return 1;
     if (max_n <= 16384) return 4;
-    return 16;
+    return 8;
 }
 
 // Segment-tiled layout of a term sorted by its primary (non-injective) gather
@@ -106,8 +109,10 @@ static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<in
         }
     const int64_t G = (int64_t)sstart.size();
     sstart.push_back(n);
-    const int64_t Lt = (G >= 2 * (int64_t)T) ? INT64_MAX
-                                             : std::max<int64_t>(1, (n + 2 * T - 1) / (2 * T));
+    // split only when there are fewer groups than lanes (then ~T virtual
+    // segments, one tile per wave); otherwise each lane owns whole groups
+    const int64_t Lt = (G >= (int64_t)T) ? INT64_MAX
+                                         : std::max<int64_t>(1, (n + T - 1) / T);
     struct V {
         int32_t k;
         int64_t start;
@@ -140,9 +145,9 @@ static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<in
         int32_t lmax = 0, lmin = INT32_MAX;
         for (int l = 0; l < 64; ++l) {
             const int64_t v = t * 64 + l;
-            const int32_t len = v < nv ? vs[v].len : 0;
-            lmax = std::max(lmax, len);
-            lmin = std::min(lmin, len);
+            if (v >= nv) break;  // lanes past the end are masked off in-kernel
+            lmax = std::max(lmax, vs[v].len);
+            lmin = std::min(lmin, vs[v].len);
         }
         const int32_t lpad = (lmax + 3) / 4 * 4;
         if (total > INT32_MAX - 64 * (int64_t)lpad)
@@ -199,6 +204,7 @@ static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<in
     dt.ncomb = split ? (int32_t)G : 0;
     dt.tile_base = (int64_t)ipool.size();
     ipool.insert(ipool.end(), tiles.begin(), tiles.end());
+    while (ipool.size() % 2) ipool.push_back(0);  // lane records are read as int2
     dt.lane_base = (int64_t)ipool.size();
     ipool.insert(ipool.end(), lanes.begin(), lanes.end());
     dt.comb_base = (int64_t)ipool.size();
@@ -371,7 +377,10 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
             masks[placed] |= bit;
         }
         dt.npass = npass;
-        for (int ps = 0; ps < 3; ++ps) dt.pass_mask[ps] = masks[ps];
+        dt.pass_masks = masks[0] | (masks[1] << 4) | (masks[2] << 8);
+        dt.wave_task = -1;
+        dt.clogs = (dt.op[2].kind == MC_OP_CONST) ? (float)std::log((double)dt.op[2].cval) : 0.0f;
+        dt.prim_poff = primary >= 0 ? dt.op[primary].poff : 0;
         if (primary >= 0) {
             const int rc = build_segments(dt, dpool, ipool, 64 * wpc);
             if (rc) return rc;
@@ -379,8 +388,78 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
         dts.push_back(dt);
     }
 
+    // broadcast-parameter cotangent slots and their fixed-order finalize list
+    int32_t nslot = 0;
+    std::vector<std::pair<int32_t, int32_t>> uses;  // (param, slot)
+    for (DevTerm& dt : dts)
+        for (int a = 0; a < 3; ++a)
+            if (dt.op[a].kind == MC_OP_PSCALAR) {
+                dt.op[a].slot = nslot;
+                uses.push_back({dt.op[a].poff, nslot});
+                ++nslot;
+            }
+    std::stable_sort(uses.begin(), uses.end(),
+                     [](const std::pair<int32_t, int32_t>& x,
+                        const std::pair<int32_t, int32_t>& y) { return x.first < y.first; });
+    std::vector<int32_t> fin_hdr, fin_ids;
+    for (size_t i = 0; i < uses.size();) {
+        size_t j = i;
+        while (j < uses.size() && uses[j].first == uses[i].first) ++j;
+        fin_hdr.push_back(uses[i].first);
+        fin_hdr.push_back((int32_t)fin_ids.size());
+        fin_hdr.push_back((int32_t)(j - i));
+        for (size_t k = i; k < j; ++k) fin_ids.push_back(uses[k].second);
+        i = j;
+    }
+    const int64_t sfin_base = (int64_t)ipool.size();
+    ipool.push_back((int32_t)(fin_hdr.size() / 3));
+    ipool.insert(ipool.end(), fin_hdr.begin(), fin_hdr.end());
+    ipool.insert(ipool.end(), fin_ids.begin(), fin_ids.end());
+    // small terms whose only cotangents are broadcast parameters run as wave
+    // tasks: one wave each, round robin, concurrently with the other waves
+    {
+        int next = 0;
+        for (DevTerm& dt : dts) {
+            bool vec_param = false;
+            for (int a = 0; a < 3; ++a)
+                if (dt.op[a].kind == MC_OP_PVEC || dt.op[a].kind == MC_OP_GATHER) vec_param = true;
+            if (dt.primary < 0 && dt.npass == 1 && dt.n <= 64 && !vec_param)
+                dt.wave_task = (next++) % wpc;
+        }
+    }
+    // evaluate all-wave terms first and the wave tasks last: a wave task only
+    // writes its own cotangent slots, so its position is free, and at the end
+    // it overlaps the other waves' share of the last all-wave term
+    std::stable_partition(dts.begin(), dts.end(),
+                          [](const DevTerm& dt) { return dt.wave_task < 0; });
+    // barriers between terms whose gradient writes overlap (vector operands)
+    {
+        std::vector<std::pair<int64_t, int64_t>> open_ranges;
+        for (DevTerm& dt : dts) {
+            std::vector<std::pair<int64_t, int64_t>> mine;
+            for (int a = 0; a < 3; ++a) {
+                const DevOperand& d = dt.op[a];
+                if (d.kind == MC_OP_PVEC) {
+                    mine.push_back({d.poff, d.poff + dt.n - 1});
+                } else if (d.kind == MC_OP_GATHER) {
+                    // conservative: the whole parameter vector
+                    mine.push_back({0, (int64_t)n_params - 1});
+                }
+            }
+            bool clash = false;
+            for (auto& r : mine)
+                for (auto& o : open_ranges)
+                    if (!(r.second < o.first || o.second < r.first)) clash = true;
+            dt.sync_before = clash ? 1 : 0;
+            if (clash) open_ranges.clear();
+            open_ranges.insert(open_ranges.end(), mine.begin(), mine.end());
+        }
+    }
+
     mc_program* p = new mc_program();
     p->D = n_params;
+    p->nslots = nslot + 1;
+    p->sfin_base = sfin_base;
     p->lp_const = lp_const;
     p->max_n = max_n;
     p->wpc = wpc;
@@ -433,8 +512,12 @@ static int block_of(int wpc) { return 64 * wpc * cpb_of(wpc); }
 static int32_t dpad_of(int32_t D) { return (D + 15) / 16 * 16; }
 static constexpr int64_t kLdsArenaBudget = 64 * 1024;  // keep >= 2 workgroups per CU
 
+static int scratch_of(const mc_program* p) {
+    // keep every chain group's region 16-byte aligned
+    return (group_scratch_floats(p->wpc, p->nslots) + 3) / 4 * 4;
+}
 static int64_t hmc_lds_floats(const mc_program* p, bool lds_arena) {
-    return group_scratch_floats(p->wpc) + (lds_arena ? 5 * (int64_t)dpad_of(p->D) : 0);
+    return scratch_of(p) + (lds_arena ? 5 * (int64_t)dpad_of(p->D) : 0);
 }
 static bool hmc_use_lds(const mc_program* p) {
     return cpb_of(p->wpc) * hmc_lds_floats(p, true) * 4 <= kLdsArenaBudget;
@@ -488,7 +571,7 @@ k_logp(DevCtx P, int64_t n_points, const float* q, float* logp, float* grad, int
 template <int WPC>
 static int launch_logp(const mc_program* p, int64_t n, const float* q, float* lp, float* g,
                        hipStream_t st) {
-    const int lds_floats = group_scratch_floats(WPC);
+    const int lds_floats = scratch_of(p);
     const size_t lds = (size_t)cpb_of(WPC) * lds_floats * 4;
     const int64_t grid = (n + cpb_of(WPC) - 1) / cpb_of(WPC);
     MC_HIP_TRY(allow_lds(k_logp<WPC>, lds));
@@ -508,7 +591,7 @@ extern "C" int mc_logp_grad(const mc_program* p, int64_t n_points, const float* 
     switch (p->wpc) {
         case 1: return launch_logp<1>(p, n_points, q, logp, grad, st);
         case 4: return launch_logp<4>(p, n_points, q, logp, grad, st);
-        default: return launch_logp<16>(p, n_points, q, logp, grad, st);
+        default: return launch_logp<8>(p, n_points, q, logp, grad, st);
     }
 }
 
@@ -604,7 +687,7 @@ static int launch_init(const mc_program* p, int64_t C, const float* q0, double e
     int64_t qo, go;
     mc_state_offsets(p, C, &qo, &go);
     char* b = (char*)state;
-    const int lds_floats = group_scratch_floats(WPC);
+    const int lds_floats = scratch_of(p);
     const size_t lds = (size_t)cpb_of(WPC) * lds_floats * 4;
     const int64_t grid = (C + cpb_of(WPC) - 1) / cpb_of(WPC);
     const float mu = mc_logf_ref((float)(10.0 * eps0));  // nuts.py:63 mx.log(10 * step_size)
@@ -624,7 +707,7 @@ extern "C" int mc_state_init(const mc_program* p, int64_t C, const float* q0, do
     switch (p->wpc) {
         case 1: return launch_init<1>(p, C, q0, eps0, state, st);
         case 4: return launch_init<4>(p, C, q0, eps0, state, st);
-        default: return launch_init<16>(p, C, q0, eps0, state, st);
+        default: return launch_init<8>(p, C, q0, eps0, state, st);
     }
 }
 
@@ -659,6 +742,7 @@ static int launch_hmc(const mc_program* p, const mc_run_config* cfg, void* state
     A.cfg = *cfg;
     A.dpad = dpad_of(p->D);
     A.lds_floats = (int32_t)hmc_lds_floats(p, LDS);
+    A.scratch_floats = scratch_of(p);
     const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
     const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
     MC_HIP_TRY(allow_lds(k_hmc<WPC, LDS>, lds));
@@ -687,8 +771,8 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
                            : launch_hmc<1, false>(p, cfg, state, samples, tr, w, st);
         case 4: return lds ? launch_hmc<4, true>(p, cfg, state, samples, tr, w, st)
                            : launch_hmc<4, false>(p, cfg, state, samples, tr, w, st);
-        default: return lds ? launch_hmc<16, true>(p, cfg, state, samples, tr, w, st)
-                            : launch_hmc<16, false>(p, cfg, state, samples, tr, w, st);
+        default: return lds ? launch_hmc<8, true>(p, cfg, state, samples, tr, w, st)
+                            : launch_hmc<8, false>(p, cfg, state, samples, tr, w, st);
     }
 }
 
@@ -706,7 +790,8 @@ static int launch_nuts(const mc_program* p, const mc_run_config* cfg, void* stat
     RunArgs A;
     A.cfg = *cfg;
     A.dpad = dpad_of(p->D);
-    A.lds_floats = group_scratch_floats(WPC) + kNutsLdsWords;
+    A.scratch_floats = scratch_of(p);
+    A.lds_floats = A.scratch_floats + kNutsLdsWords;
     const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
     const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
     MC_HIP_TRY(allow_lds(k_nuts<WPC>, lds));
@@ -733,7 +818,7 @@ extern "C" int mc_nuts_run(const mc_program* p, const mc_run_config* cfg, void* 
     switch (p->wpc) {
         case 1: return launch_nuts<1>(p, cfg, state, samples, tr, w, st);
         case 4: return launch_nuts<4>(p, cfg, state, samples, tr, w, st);
-        default: return launch_nuts<16>(p, cfg, state, samples, tr, w, st);
+        default: return launch_nuts<8>(p, cfg, state, samples, tr, w, st);
     }
 }
 
@@ -777,6 +862,20 @@ extern "C" int mc_rng_fill(uint64_t seed, uint32_t chain, uint32_t iter, uint32_
     MC_HIP_TRY(hipGetLastError());
     return MC_OK;
 }
+
+#ifdef MC_STAMPS
+// diagnostic build only: copy out / reset the section stamp accumulators
+extern "C" int mc_debug_stamps(unsigned long long* acc, unsigned long long* cnt, int reset) {
+    if (acc) MC_HIP_TRY(hipMemcpyFromSymbol(acc, HIP_SYMBOL(mc_stamp_acc), sizeof(mc_stamp_acc)));
+    if (cnt) MC_HIP_TRY(hipMemcpyFromSymbol(cnt, HIP_SYMBOL(mc_stamp_cnt), sizeof(mc_stamp_cnt)));
+    if (reset) {
+        unsigned long long z[16 * 32] = {0};
+        MC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mc_stamp_acc), z, sizeof(z)));
+        MC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mc_stamp_cnt), z, sizeof(z)));
+    }
+    return MC_OK;
+}
+#endif
 
 extern "C" const char* mc_last_error(void) { return g_last_error.c_str(); }
 extern "C" int32_t mc_abi_version(void) { return MC_ABI_VERSION; }

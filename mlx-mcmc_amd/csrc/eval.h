@@ -32,12 +32,105 @@
 
 namespace mc {
 
+// The program tables (terms, tile/lane/finalize tables) are read-only for the
+// whole launch: reading them through the constant address space lets the
+// compiler use scalar (SMEM) loads for wave-uniform fields instead of vector
+// loads that it must re-issue after every store it cannot disambiguate.
+#define MC_CONST __attribute__((address_space(4)))
+// ---- diagnostic stamps (separate build with -DMC_STAMPS; never in the
+// product library): wave 0 of workgroup 0 accumulates s_memtime deltas per
+// section into mc_stamp_acc, read back with mc_debug_stamps().
+#ifdef MC_STAMPS
+__device__ unsigned long long mc_stamp_acc[16 * 32];  // [wave][section]
+__device__ unsigned long long mc_stamp_cnt[16 * 32];
+struct StampClock {
+    unsigned long long last;
+};
+MC_DEV unsigned long long mc_now() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+MC_DEV void stamp(StampClock& c, int sec) {
+    const unsigned long long t = mc_now();
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && threadIdx.x < 16 * 64) {
+        mc_stamp_acc[(threadIdx.x >> 6) * 32 + sec] += t - c.last;
+        mc_stamp_cnt[(threadIdx.x >> 6) * 32 + sec] += 1;
+    }
+    c.last = mc_now();
+}
+#define MC_STAMP_DECL StampClock mc_clk{mc_now()};
+#define MC_STAMP(sec) stamp(mc_clk, sec)
+#else
+#define MC_STAMP_DECL
+#define MC_STAMP(sec)
+#endif
+
+template <typename T>
+MC_DEV const MC_CONST T* cptr(const T* p) {
+    return (const MC_CONST T*)p;
+}
+
+// A term descriptor read field by field from the constant address space
+// (uniform index -> scalar loads into SGPRs).
+MC_DEV DevOperand load_op(const MC_CONST DevOperand* p) {
+    DevOperand o;
+    o.kind = p->kind;
+    o.poff = p->poff;
+    o.pool = p->pool;
+    o.cval = p->cval;
+    o.unique = p->unique;
+    o.slot = p->slot;
+    o.pad = 0;
+    return o;
+}
+
+MC_DEV DevTerm load_term(const MC_CONST DevTerm* p) {
+    DevTerm t;
+    t.dist = p->dist;
+    t.primary = p->primary;
+    t.n = p->n;
+    t.weight = p->weight;
+    t.c0 = p->c0;
+    t.npass = p->npass;
+    t.pass_masks = p->pass_masks;
+    t.prim_poff = p->prim_poff;
+    t.wave_task = p->wave_task;
+    t.clogs = p->clogs;
+    t.pad2 = 0.0f;
+    t.op[0] = load_op(&p->op[0]);
+    t.op[1] = load_op(&p->op[1]);
+    t.op[2] = load_op(&p->op[2]);
+    t.ntiles = p->ntiles;
+    t.nvirt = p->nvirt;
+    t.ncomb = p->ncomb;
+    t.sync_before = p->sync_before;
+    t.tile_base = p->tile_base;
+    t.lane_base = p->lane_base;
+    t.comb_base = p->comb_base;
+    return t;
+}
+
+// Wave-wide float sum, bit-identical in every lane.  Inside each 16-lane row
+// a DPP butterfly (quad_perm xor 1, xor 2, half-row mirror, row mirror: each
+// stage adds a pair in both orders, and fp add is commutative) leaves the row
+// sum in all 16 lanes; the four row sums are then added in fixed order from
+// SGPRs.  ~4 DPP adds + 4 readlanes, no LDS traffic.
+template <int CTRL>
+MC_DEV float dpp_row(float x) {
+    return __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
 MC_DEV float wave_sum(float x) {
-    // xor butterfly: every lane ends with the bit-identical total
-    // (each stage adds a pair in both orders; fp add is commutative).
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
+    x += dpp_row<0xB1>(x);   // quad_perm [1,0,3,2]
+    x += dpp_row<0x4E>(x);   // quad_perm [2,3,0,1]
+    x += dpp_row<0x141>(x);  // row_half_mirror
+    x += dpp_row<0x140>(x);  // row_mirror
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 48));
+    return ((r0 + r1) + r2) + r3;
 }
 
 // A chain group: WPC wavefronts that together own one chain.  With WPC == 1
@@ -46,7 +139,9 @@ template <int WPC>
 struct Group {
     static constexpr int T = 64 * WPC;
     int tid;
-    float* red;  // LDS scratch, WPC floats
+    float* red;   // LDS scratch, WPC floats (sum())
+    float* sred;  // LDS: per-wave partials of the broadcast-parameter cotangents
+                  // and of log p, [slot][wave]
 
     MC_DEV void sync() const {
         if constexpr (WPC == 1) {
@@ -73,6 +168,22 @@ struct Group {
         }
     }
 };
+
+// Deposit a wave's partial of cotangent slot `slot` (no barrier: the slots are
+// summed in a fixed order once per evaluation, see eval_lp_grad).
+template <int WPC>
+MC_DEV void flush_slot(const Group<WPC>& G, int slot, float x) {
+    x = wave_sum(x);
+    if ((G.tid & 63) == 0) G.sred[slot * WPC + (G.tid >> 6)] = x;
+}
+
+// The same for a wave task: the one wave owns every entry of the slot.
+template <int WPC>
+MC_DEV void flush_slot_task(const Group<WPC>& G, int slot, float x) {
+    x = wave_sum(x);
+    const int lane = G.tid & 63;
+    if (lane < WPC) G.sred[slot * WPC + lane] = (lane == 0) ? x : 0.0f;
+}
 
 // LDS scratch of a chain group beyond the reduction slots: the per-virtual-
 // segment partial cotangents of a split segmented term (<= 4T floats).
@@ -163,6 +274,7 @@ MC_DEV void strided_uscale(const DevTerm& T, const DevCtx& P, const float* q, fl
     float* gl = (LK == 2 && (mask & PASS_LOC)) ? g + T.op[1].poff : nullptr;
     const float w = T.weight;
     const int64_t n = T.n;
+    const float inv_var = 1.0f / var;
     float s1 = 0.0f, s2 = 0.0f, cnt = 0.0f;
     bool neg = false;
     for (int64_t i = tid; i < n; i += nthr) {
@@ -172,14 +284,14 @@ MC_DEV void strided_uscale(const DevTerm& T, const DevCtx& P, const float* q, fl
             const float d = v - m;
             s2 = fmaf(d, d, s2);
             s1 += d;
-            if (VK == 2 && gv) gv[i] += -((w * d) / var);
-            if (LK == 2 && gl) gl[i] += (w * d) / var;
+            if (VK == 2 && gv) gv[i] += -(w * d) * inv_var;
+            if (LK == 2 && gl) gl[i] += (w * d) * inv_var;
         } else {
             if (v >= 0.0f) {
                 s2 = fmaf(v, v, s2);
                 s1 += v;
                 cnt += 1.0f;
-                if (VK == 2 && gv) gv[i] += -((w * v) / var);
+                if (VK == 2 && gv) gv[i] += -(w * v) * inv_var;
             } else {
                 neg = true;
             }
@@ -265,44 +377,86 @@ MC_DEV void seg_normal_uscale(const DevTerm& T, const DevCtx& P, const float* q,
                               float* vpart) {
     const int wave = G.tid >> 6;
     const int lane = G.tid & 63;
-    const DevOperand& po = T.op[PV];
     const DevOperand& od = T.op[1 - PV];
-    const int* tiles = P.index + T.tile_base;
+    const MC_CONST int* tiles = cptr(P.index) + T.tile_base;
     const int* lanes = P.index + T.lane_base;
     const float* data = P.data + od.pool;
     const bool acc_prim = (mask & (1u << PV)) != 0;
     const bool split = T.ncomb > 0;
     const float w = T.weight;
     float s1_all = 0.0f, s2_all = 0.0f, cnt_all = 0.0f;
-    for (int t = wave; t < T.ntiles; t += WPC) {
+    // software pipeline over this wave's tiles: the next tile's lane record is
+    // loaded while the current tile streams, and a tile's first data batch is
+    // issued before its dependent theta read.
+    int t = wave;
+    int2 rec_n = make_int2(0, 0);
+    if (t < T.ntiles && t * 64 + lane < T.nvirt)
+        rec_n = reinterpret_cast<const int2*>(lanes)[t * 64 + lane];
+    for (; t < T.ntiles; t += WPC) {
         const int off = tiles[3 * t];
         const int lpad = tiles[3 * t + 1];
         const int lmin = tiles[3 * t + 2];
         const int v = t * 64 + lane;
         const bool valid = v < T.nvirt;
-        const int k = valid ? lanes[2 * v] : 0;
-        const int len = valid ? lanes[2 * v + 1] : 0;
-        const float th = q[po.poff + k];
+        const int k = rec_n.x;
+        const int len = rec_n.y;
+        const int tn = t + WPC;
+        rec_n = make_int2(0, 0);
+        if (tn < T.ntiles && tn * 64 + lane < T.nvirt)
+            rec_n = reinterpret_cast<const int2*>(lanes)[tn * 64 + lane];
+        const float th = q[T.prim_poff + k];
         const float4* base = reinterpret_cast<const float4*>(data + off) + lane;
         float s1 = 0.0f, s2 = 0.0f;
-        int u4 = 0;
         const int full4 = lmin >> 2;
-        // d = value - loc: x - th when loc is the primary, th - x when value is
-#pragma unroll 4
-        for (; u4 < full4; ++u4) {
-            const float4 x = base[u4 * 64];
+        float s1b = 0.0f, s2b = 0.0f;  // two accumulator chains
+        auto acc4 = [&](const float4 x) {
             const float d0 = PV == 1 ? x.x - th : th - x.x;
             const float d1 = PV == 1 ? x.y - th : th - x.y;
             const float d2 = PV == 1 ? x.z - th : th - x.z;
             const float d3 = PV == 1 ? x.w - th : th - x.w;
             s2 = fmaf(d0, d0, s2);
             s1 += d0;
-            s2 = fmaf(d1, d1, s2);
-            s1 += d1;
+            s2b = fmaf(d1, d1, s2b);
+            s1b += d1;
             s2 = fmaf(d2, d2, s2);
             s1 += d2;
-            s2 = fmaf(d3, d3, s2);
-            s1 += d3;
+            s2b = fmaf(d3, d3, s2b);
+            s1b += d3;
+        };
+        // batches of kBatch independent 16-byte loads in flight per lane; the
+        // next batch is issued before the current one is consumed
+        constexpr int kBatch = 4;
+        const int nb = full4 / kBatch;
+        float4 cur[kBatch];
+        if (nb > 0) {
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) cur[b] = base[b * 64];
+        }
+        for (int bi = 0; bi < nb; ++bi) {
+            float4 nxt[kBatch];
+            const bool more = bi + 1 < nb;
+            if (more) {
+#pragma unroll
+                for (int b = 0; b < kBatch; ++b) nxt[b] = base[((bi + 1) * kBatch + b) * 64];
+            }
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) acc4(cur[b]);
+            if (more) {
+#pragma unroll
+                for (int b = 0; b < kBatch; ++b) cur[b] = nxt[b];
+            }
+        }
+        int u4 = nb * kBatch;
+        if (u4 < full4) {
+            const int r = full4 - u4;
+            float4 x[kBatch];
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b)
+                if (b < r) x[b] = base[(u4 + b) * 64];
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b)
+                if (b < r) acc4(x[b]);
+            u4 = full4;
         }
         for (; 4 * u4 < lpad; ++u4) {
             const float4 x = base[u4 * 64];
@@ -316,13 +470,19 @@ MC_DEV void seg_normal_uscale(const DevTerm& T, const DevCtx& P, const float* q,
                 }
             }
         }
+        s1 += s1b;
+        s2 += s2b;
+        if (!valid) {  // lanes past the last virtual segment read padding
+            s1 = 0.0f;
+            s2 = 0.0f;
+        }
         s1_all += s1;
         s2_all += s2;
         cnt_all += (float)len;
         if (valid && acc_prim) {
             const float c = PV == 1 ? w * (s1 / var) : -(w * (s1 / var));
             if (split) vpart[v] = c;
-            else g[po.poff + k] += c;
+            else g[T.prim_poff + k] += c;
         }
     }
     M.s1 += s1_all;
@@ -352,8 +512,8 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
     const int wave = G.tid >> 6;
     const int lane = G.tid & 63;
     const int a = T.primary;
-    const DevOperand po = a == 0 ? T.op[0] : (a == 1 ? T.op[1] : T.op[2]);
-    const int* tiles = P.index + T.tile_base;
+    const int prim_poff = T.prim_poff;
+    const MC_CONST int* tiles = cptr(P.index) + T.tile_base;
     const int* lanes = P.index + T.lane_base;
     const bool acc_prim = (mask & (1u << a)) != 0;
     const bool split = T.ncomb > 0;
@@ -367,7 +527,7 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
         const bool valid = v < T.nvirt;
         const int k = valid ? lanes[2 * v] : 0;
         const int len = valid ? lanes[2 * v + 1] : 0;
-        const float th = q[po.poff + k];
+        const float th = q[prim_poff + k];
         float cp = 0.0f;
         for (int u = 0; u < lpad; ++u) {
             if (u < len) {
@@ -395,7 +555,7 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
         }
         if (valid && acc_prim) {
             if (split) vpart[v] = cp;
-            else g[po.poff + k] += cp;
+            else g[prim_poff + k] += cp;
         }
     }
 }
@@ -404,17 +564,21 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
 template <int WPC>
 MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* g,
                       const Group<WPC>& G, float& lp_acc, const SegScratch& S) {
+    const bool task = T.wave_task >= 0;
+    if (task && (G.tid >> 6) != T.wave_task) return;  // another wave owns it
+    const int tid = task ? (G.tid & 63) : G.tid;
+    const int nthr = task ? 64 : G.T;
     const float uv = uniform_value(T.op[0], q);
     const float um = uniform_value(T.op[1], q);
     const float us = uniform_value(T.op[2], q);
     const bool scale_vec = is_vec(T.op[2].kind);
-    const float ulogs = scale_vec ? 0.0f : logf(us);
+    const float ulogs =
+        scale_vec ? 0.0f : (T.op[2].kind == MC_OP_CONST ? T.clogs : logf(us));
     const float var = us * us;
     const bool normal = (T.dist == MC_DIST_NORMAL);
 
     for (int pass = 0; pass < T.npass; ++pass) {
-        const uint32_t mask =
-            pass == 0 ? T.pass_mask[0] : (pass == 1 ? T.pass_mask[1] : T.pass_mask[2]);
+        const uint32_t mask = (T.pass_masks >> (4 * pass)) & 0xFu;
         float pv = 0.0f, pm = 0.0f, ps = 0.0f;
         Moments M = {0.0f, 0.0f, 0.0f, false};
         bool moments = false;
@@ -428,7 +592,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                 switch (code) {
 #define MC_SU(c, D_, V_, L_)                                                                \
     case c:                                                                                 \
-        strided_uscale<D_, V_, L_>(T, P, q, g, G.tid, G.T, mask, uv, um, var, M);           \
+        strided_uscale<D_, V_, L_>(T, P, q, g, tid, nthr, mask, uv, um, var, M);            \
         break;
                     MC_SU(0, MC_DIST_NORMAL, 0, 0)
                     MC_SU(1, MC_DIST_NORMAL, 0, 1)
@@ -447,7 +611,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                         break;
                 }
             } else {
-                strided_generic(T, P, q, g, G.tid, G.T, mask, uv, um, us, ulogs, lp_acc, pv, pm,
+                strided_generic(T, P, q, g, tid, nthr, mask, uv, um, us, ulogs, lp_acc, pv, pm,
                                 ps);
             }
         } else {
@@ -467,58 +631,92 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
             if (T.ncomb > 0 && (mask & (1u << T.primary))) {
                 // split segments: add the virtual partials in order
                 G.sync();
-                const DevOperand po =
-                    T.primary == 0 ? T.op[0] : (T.primary == 1 ? T.op[1] : T.op[2]);
+                const int prim_poff = T.prim_poff;
                 const int* comb = P.index + T.comb_base;
                 for (int c = G.tid; c < T.ncomb; c += G.T) {
                     const int k = comb[3 * c], vf = comb[3 * c + 1], vc = comb[3 * c + 2];
                     float s = vpart[vf];
                     for (int j = 1; j < vc; ++j) s += vpart[vf + j];
-                    g[po.poff + k] += s;
+                    g[prim_poff + k] += s;
                 }
             }
         }
         if (moments) finish_moments(T, mask, us, ulogs, M, lp_acc, pv, pm, ps);
 
-        // broadcast-parameter cotangents: fixed-order group reduction
-        if ((mask & PASS_VALUE) && T.op[0].kind == MC_OP_PSCALAR) {
-            const float t = G.sum(pv);
-            if (G.tid == 0) g[T.op[0].poff] += t;
-        }
-        if ((mask & PASS_LOC) && T.op[1].kind == MC_OP_PSCALAR) {
-            const float t = G.sum(pm);
-            if (G.tid == 0) g[T.op[1].poff] += t;
-        }
-        if ((mask & PASS_SCALE) && T.op[2].kind == MC_OP_PSCALAR) {
-            const float t = G.sum(ps);
-            if (G.tid == 0) g[T.op[2].poff] += t;
-        }
-        G.sync();
+        // broadcast-parameter cotangents: per-wave partials into their slots
+        auto flush = [&](int slot, float x) {
+            if (task) flush_slot_task(G, slot, x);
+            else flush_slot(G, slot, x);
+        };
+        if ((mask & PASS_VALUE) && T.op[0].kind == MC_OP_PSCALAR) flush(T.op[0].slot, pv);
+        if ((mask & PASS_LOC) && T.op[1].kind == MC_OP_PSCALAR) flush(T.op[1].slot, pm);
+        if ((mask & PASS_SCALE) && T.op[2].kind == MC_OP_PSCALAR) flush(T.op[2].slot, ps);
+        if (pass + 1 < T.npass) G.sync();  // passes exist because their writes overlap
     }
 }
 
 // Log density at q and its gradient into g (g may not alias q).  Every thread
-// of the group returns the same value.
+// of the group returns the same value.  Barriers: one after zeroing g (skipped
+// when the caller zeroed it in its own sweep), one before a term whose vector
+// writes overlap an earlier term's since the last barrier (host-computed
+// sync_before), one before and one after the fixed-order slot reduction.
 template <int WPC>
 MC_DEV float eval_lp_grad(const DevCtx& P, const float* q, float* g, const Group<WPC>& G,
-                          const SegScratch& S) {
-    for (int j = G.tid; j < P.D; j += G.T) g[j] = 0.0f;
-    G.sync();
-    float lp_acc = 0.0f;
-    for (int t = 0; t < P.n_terms; ++t) {
-        const DevTerm& T = P.terms[t];
-        eval_term<WPC>(T, P, q, g, G, lp_acc, S);
+                          const SegScratch& S, bool g_zeroed = false) {
+    MC_STAMP_DECL
+    if (!g_zeroed) {
+        for (int j = G.tid; j < P.D; j += G.T) g[j] = 0.0f;
+        G.sync();
     }
-    return G.sum(lp_acc) + P.lp_const;
+    float lp_acc = 0.0f;
+    const MC_CONST DevTerm* terms = cptr(P.terms);
+    for (int t = 0; t < P.n_terms; ++t) {
+        const DevTerm T = load_term(terms + t);
+        if (T.sync_before) G.sync();
+        MC_STAMP(2 + 2 * (t < 7 ? t : 7));
+        eval_term<WPC>(T, P, q, g, G, lp_acc, S);
+        MC_STAMP(3 + 2 * (t < 7 ? t : 7));
+    }
+    const int lp_slot = P.nslots - 1;
+    flush_slot(G, lp_slot, lp_acc);
+    G.sync();
+    MC_STAMP(18);
+    // broadcast parameters: sum their slots in (slot, wave) order
+    const MC_CONST int* fin = cptr(P.index) + P.sfin_base;
+    const int nsp = fin[0];
+    const MC_CONST int* ids = fin + 1 + 3 * nsp;
+    for (int i = G.tid; i < nsp; i += G.T) {
+        const int poff = fin[1 + 3 * i], first = fin[2 + 3 * i], cnt = fin[3 + 3 * i];
+        float t = 0.0f;
+        for (int c = 0; c < cnt; ++c) {
+            const float* sl = G.sred + ids[first + c] * WPC;
+            float u = sl[0];
+#pragma unroll
+            for (int w = 1; w < WPC; ++w) u += sl[w];
+            t = (c == 0) ? u : t + u;
+        }
+        g[poff] += t;
+    }
+    const float* ls = G.sred + lp_slot * WPC;
+    float lp = ls[0];
+#pragma unroll
+    for (int w = 1; w < WPC; ++w) lp += ls[w];
+    G.sync();
+    MC_STAMP(19);
+    return lp + P.lp_const;
 }
 
-// LDS floats a chain group needs for reductions + segment partials.
-__host__ __device__ constexpr int group_scratch_floats(int wpc) { return 16 + 4 * 64 * wpc; }
+// LDS floats of a chain group's evaluator scratch: reduction slots (16),
+// segment partials (4T), cotangent slots (nslots x WPC).
+__host__ __device__ constexpr int group_scratch_floats(int wpc, int nslots) {
+    return 16 + 4 * 64 * wpc + nslots * wpc;
+}
 
 template <int WPC>
 MC_DEV void carve_group(float* base, Group<WPC>& G, SegScratch& S) {
     G.red = base;
     S.vpart = base + 16;
+    G.sred = base + 16 + 4 * 64 * WPC;
 }
 
 }  // namespace mc

@@ -40,7 +40,7 @@ k_hmc(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, flo
     carve_group<WPC>(base, G, S);
     const int D = P.D;
     const int Dp = A.dpad;
-    float* arena = LDS_ARENA ? (base + group_scratch_floats(WPC)) : (ws + c * 5 * (int64_t)Dp);
+    float* arena = LDS_ARENA ? (base + A.scratch_floats) : (ws + c * 5 * (int64_t)Dp);
     float* qA = arena;
     float* gA = arena + Dp;
     float* qB = arena + 2 * Dp;
@@ -96,6 +96,7 @@ k_hmc(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, flo
         const float* cg = gA;
         float lpn = lp;
         for (int l = 0; l < L; ++l) {
+            MC_STAMP_DECL
             for (int j = G.tid; j < D; j += T) {
                 const float gj = cg[j];
                 float pj = p[j];
@@ -103,9 +104,12 @@ k_hmc(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, flo
                 pj = pj + h * gj;             // first half kick of step l
                 p[j] = pj;
                 qB[j] = cq[j] + e * pj;
+                gB[j] = 0.0f;  // the evaluator accumulates into a zeroed gradient
             }
             G.sync();
-            lpn = eval_lp_grad<WPC>(P, qB, gB, G, S);
+            MC_STAMP(0);
+            lpn = eval_lp_grad<WPC>(P, qB, gB, G, S, true);
+            MC_STAMP(1);
             cq = qB;
             cg = gB;
         }

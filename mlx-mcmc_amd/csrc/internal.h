@@ -16,6 +16,8 @@ struct DevOperand {
     int64_t pool;
     float cval;
     int32_t unique;
+    int32_t slot;     // PSCALAR: LDS slot of its per-wave partial cotangent
+    int32_t pad;
 };
 
 // Pass mask bits: which cotangents a sweep over the term accumulates.  Terms
@@ -36,7 +38,14 @@ struct DevTerm {
     float weight;
     float c0;          // f32 normaliser: -0.5 log(2 pi)  [+ log 2 for HalfNormal]
     int32_t npass;
-    uint32_t pass_mask[3];
+    uint32_t pass_masks;  // 4 bits per sweep: PASS_* of sweep p at bits 4p..4p+3
+    int32_t prim_poff;    // param offset of the primary operand (no runtime
+                          // indexing of op[]: it would force T into scratch)
+    int32_t wave_task;    // >= 0: a small term with only broadcast-parameter
+                          // cotangents, evaluated by this one wave while the
+                          // other waves move on (-1: every wave)
+    float clogs;          // CONST scale: f32 log(scale), precomputed
+    float pad2;
     DevOperand op[3];  // value, loc, scale
     // ---- segment-tiled layout (primary >= 0) --------------------------------
     // Elements are grouped by the primary index into runs ("segments"), long
@@ -47,7 +56,7 @@ struct DevTerm {
     int32_t ntiles;
     int32_t nvirt;
     int32_t ncomb;        // > 0: segments were split, partials combined in order
-    int32_t pad0;
+    int32_t sync_before;  // a barrier is needed before this term's writes
     int64_t tile_base;    // index pool: per tile {off, len_pad, len_min}
     int64_t lane_base;    // index pool: per virtual segment {k, len}
     int64_t comb_base;    // index pool: per segment {k, vfirst, vcount}
@@ -58,9 +67,11 @@ struct DevCtx {
     int32_t n_terms;
     int32_t D;
     float lp_const;
-    int32_t pad;
+    int32_t nslots;       // PSCALAR cotangent slots (+1 for log p)
     const float* data;
     const int32_t* index;
+    int64_t sfin_base;    // index pool: {n_sparams, then per param {poff, first, count}},
+                          // then the slot ids, grouped by parameter
 };
 
 // Per-launch constants shared by the sampler kernels.
@@ -68,6 +79,8 @@ struct RunArgs {
     mc_run_config cfg;
     int32_t dpad;          // D rounded up to 16 floats (arena stride unit)
     int32_t lds_floats;    // LDS floats per chain group
+    int32_t scratch_floats;  // of which the evaluator's scratch (arena follows)
+    int32_t pad;
 };
 
 struct TraceDev {

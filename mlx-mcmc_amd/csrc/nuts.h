@@ -83,7 +83,7 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
     G.tid = threadIdx.x % T;
     float* base = smem + (int64_t)lc * A.lds_floats;
     carve_group<WPC>(base, G, S);
-    int* pend_idx = reinterpret_cast<int*>(base + group_scratch_floats(WPC));
+    int* pend_idx = reinterpret_cast<int*>(base + A.scratch_floats);
     int* pend_n = pend_idx + 32;
     float* pool_lp = reinterpret_cast<float*>(pend_idx + 64);
 
@@ -199,9 +199,10 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
                     const float pj = Er[jj] + h * Eg[jj];
                     Er[jj] = pj;
                     Eq[jj] = Eq[jj] + e * pj;
+                    Eg[jj] = 0.0f;  // the evaluator accumulates into a zeroed gradient
                 }
                 G.sync();
-                const float lpl = eval_lp_grad<WPC>(P, Eq, Eg, G, S);
+                const float lpl = eval_lp_grad<WPC>(P, Eq, Eg, G, S, true);
                 float kl = 0.0f;
                 for (int jj = G.tid; jj < D; jj += T) {
                     const float pj = Er[jj] + h * Eg[jj];
