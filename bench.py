@@ -121,6 +121,7 @@ def main():
     m = _ensure_pkg()
     import workloads as W
     from mlx_mcmc_amd import _engine, _trace
+    from mlx_mcmc_amd.distributed import gather_to_root, max_over_ranks, shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -140,7 +141,8 @@ def main():
     prog = _trace.compile_model(lp_fn, init)
     chains = _engine.ChainSet(prog, C, prog.layout.flatten(init), args.step_size, device=dev)
     samples = torch.empty((C, max(K, 1), D), dtype=torch.float32, device=dev)
-    cfg = dict(chain_offset=rank * C, num_warmup=Wm, num_samples=K, sample_begin=0,
+    chain_offset, _ = shard(C * world, world, rank)   # weak scaling: C chains per GPU
+    cfg = dict(chain_offset=chain_offset, num_warmup=Wm, num_samples=K, sample_begin=0,
                sample_capacity=K, seed=args.seed, step_size=args.step_size,
                target_accept=0.8, num_leapfrog_steps=L, adapt_step_size=True)
 
@@ -166,10 +168,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if K else float("nan")
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    elapsed = float(t_max.item())
+    elapsed = max_over_ranks(elapsed, device=dev)
 
     sc = chains.scalars()
     accept = float(np.mean(sc["n_accept"] / np.maximum(sc["n_total"], 1)))
@@ -180,12 +179,9 @@ def main():
     all_samples = samples
     if world > 1:
         tg = time.perf_counter()
-        bufs = [torch.empty_like(samples) for _ in range(world)] if rank == 0 else None
-        dist.gather(samples, gather_list=bufs, dst=0)
+        all_samples = gather_to_root(samples)   # RCCL, the only collective
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
-        if rank == 0:
-            all_samples = torch.cat(bufs, dim=0)
 
     if rank == 0:
         total_chains = C * world

@@ -118,6 +118,7 @@ class Param:
 
     __add__ = __radd__ = __sub__ = __rsub__ = __mul__ = __rmul__ = _unsupported
     __truediv__ = __rtruediv__ = __pow__ = __neg__ = __abs__ = _unsupported
+    __lt__ = __le__ = __gt__ = __ge__ = _unsupported
 
     def __float__(self):
         raise TraceError(f"float() of traced parameter '{self.name}' (a Python branch on a "

@@ -1,0 +1,113 @@
+"""Host logic without a GPU: tracing user models into the term program."""
+import numpy as np
+import pytest
+
+import mlx_mcmc_amd as m
+import mlx_mcmc_amd.core as mx
+import workloads as W
+from mlx_mcmc_amd import _lib, _trace
+
+
+def kinds(t):
+    return (t.dist, t.value.kind, t.loc.kind, t.scale.kind, t.n)
+
+
+def test_config1_model_traces_to_three_terms():
+    lp, init = W.simple_normal(W.ns_product())
+    tm = _trace.trace(lp, init)
+    assert tm.layout.names == ["mu", "sigma"] and tm.layout.size == 2
+    got = [kinds(t) for t in tm.terms]
+    assert got == [
+        (_lib.MC_DIST_NORMAL, _lib.MC_OP_PSCALAR, _lib.MC_OP_CONST, _lib.MC_OP_CONST, 1),
+        (_lib.MC_DIST_HALFNORMAL, _lib.MC_OP_PSCALAR, _lib.MC_OP_NONE, _lib.MC_OP_CONST, 1),
+        (_lib.MC_DIST_NORMAL, _lib.MC_OP_DATA, _lib.MC_OP_PSCALAR, _lib.MC_OP_PSCALAR, 100),
+    ]
+    np.testing.assert_array_equal(tm.data, W.simple_normal_data().astype(np.float32))
+
+
+def test_per_observation_loop_is_folded():
+    """examples/01_simple_normal.py:46-48 and tests/test_nuts.py:194-196 style."""
+    y = W.simple_normal_data()
+
+    def loop_model(p):
+        lp = m.Normal(0, 10).log_prob(p["mu"]) + m.HalfNormal(5).log_prob(p["sigma"])
+        ll = mx.array(0.0)
+        for yi in y:
+            ll = ll + m.Normal(p["mu"], p["sigma"]).log_prob(mx.array(yi))
+        return lp + ll
+
+    def stacked_model(p):
+        lp = m.Normal(0, 10).log_prob(p["mu"]) + m.HalfNormal(5).log_prob(p["sigma"])
+        return lp + mx.sum(mx.array([m.Normal(p["mu"], p["sigma"]).log_prob(mx.array(v))
+                                     for v in y]))
+
+    for fn in (loop_model, stacked_model):
+        tm = _trace.trace(fn, {"mu": 0.0, "sigma": 1.0})
+        assert len(tm.terms) == 3
+        assert tm.terms[2].n == 100
+        np.testing.assert_array_equal(tm.terms[2].value.data, y.astype(np.float32))
+
+
+def test_hierarchical_gather_operands():
+    G, N = W.SHAPES["small"]
+    lp, init = W.hierarchical(W.ns_product(), G, N)
+    tm = _trace.trace(lp, init)
+    assert tm.layout.size == G + 3
+    lik = tm.terms[-1]
+    assert kinds(lik) == (_lib.MC_DIST_NORMAL, _lib.MC_OP_DATA, _lib.MC_OP_GATHER,
+                          _lib.MC_OP_PSCALAR, N)
+    _, group = W.hierarchical_data(G, N)
+    np.testing.assert_array_equal(lik.loc.index, group)
+    assert lik.loc.param_offset == tm.layout.offsets[tm.layout.names.index("theta")]
+    prior = tm.terms[-2]
+    assert kinds(prior) == (_lib.MC_DIST_NORMAL, _lib.MC_OP_PVEC, _lib.MC_OP_PSCALAR,
+                            _lib.MC_OP_PSCALAR, G)
+
+
+def test_slices_elements_and_weights():
+    def model(p):
+        x = p["x"]
+        lp = m.Normal(x[0], 1.0).log_prob(x[1:4])           # element + slice
+        lp = mx.sum(lp) - 0.5 * mx.sum(m.Normal(0, 2).log_prob(x))
+        return lp + 3.0
+    tm = _trace.trace(model, {"x": np.zeros(5, np.float32)})
+    a, b = tm.terms
+    assert (a.loc.kind, a.loc.param_offset) == (_lib.MC_OP_PSCALAR, 0)
+    assert (a.value.kind, a.value.param_offset, a.n) == (_lib.MC_OP_PVEC, 1, 3)
+    assert b.weight == -0.5 and tm.lp_const == 3.0
+
+
+@pytest.mark.parametrize("bad", [
+    lambda p: m.Normal(0, 1).log_prob(p["x"] * 2.0),          # arithmetic on a param
+    lambda p: m.Normal(0, 1).log_prob(p["x"]) if p["x"] > 0 else 0,  # Python branch
+    lambda p: mx.log(p["x"]),                                   # unsupported primitive
+    lambda p: m.Normal(0, 1).log_prob(p["v"]),                  # unsummed vector
+])
+def test_unsupported_models_raise(bad):
+    with pytest.raises(_trace.TraceError):
+        _trace.trace(bad, {"x": 1.0, "v": np.zeros(3, np.float32)})
+
+
+def test_layout_roundtrip():
+    init = {"a": 1.0, "b": np.arange(6, dtype=np.float32).reshape(2, 3), "c": 2.0}
+    lay = _trace.layout_of(init)
+    flat = lay.flatten(init)
+    np.testing.assert_array_equal(flat, [1, 0, 1, 2, 3, 4, 5, 2])
+    back = lay.unflatten(np.stack([flat, flat + 1]))
+    assert back["b"].shape == (2, 2, 3) and back["a"].shape == (2,)
+
+
+def test_random_keys_are_deterministic():
+    k = m.random.key(42)
+    assert m.random.split(k, 3) == m.random.split(m.random.key(42), 3)
+    assert len(set(x.seed for x in m.random.split(k, 8))) == 8
+
+
+def test_mcmc_method_errors():
+    mc = m.MCMC(lambda p: m.Normal(0, 1).log_prob(p["x"]))
+    with pytest.raises(ValueError):
+        mc.run({"x": 0.0}, method="gibbs")
+    with pytest.raises(NotImplementedError):
+        mc.run({"x": 0.0}, method="metropolis")
+    with pytest.raises(ValueError):
+        mc.summary()
