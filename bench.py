@@ -216,12 +216,14 @@ def main():
                              f"D={D}, N={N}, L={L}, {C} chains per GPU"),
                 "num_params": D, "num_obs": N, "leapfrog_steps": L, "chains_per_gpu": C,
                 "total_chains": total_chains, "parallelism": f"chains sharded {C}/GPU",
-                "waves_per_chain": prog.waves_per_chain,
+                "waves_per_chain": prog.waves_per_chain, "slices": prog.num_slices,
             },
             "roofline": {
                 "bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
-                "kernel": f"k_hmc<{prog.waves_per_chain}>", "kernel_ms": kern_ms,
+                "kernel": (f"k_hmc_sl<{16 if C > 8 else 8}> (S={prog.num_slices} slices)"
+                           if prog.num_slices > 1 else f"k_hmc<{prog.waves_per_chain}>"),
+                "kernel_ms": kern_ms,
                 "flops_per_launch": flops_per_launch,
                 "note": ("fp32 compute bound (vector FP32 peak = f32-MFMA peak 157.3 TF); "
                          "F = 5N + 13D flops per chain-leapfrog-step, C*L per launch"),

@@ -52,6 +52,8 @@ extern "C" {
 #define MC_ERR_UNSUPPORTED -2  /* well-formed but outside what the kernels do */
 #define MC_ERR_HIP        -3   /* HIP runtime error                          */
 #define MC_ERR_NOMEM      -4   /* device allocation failed                   */
+#define MC_ERR_TIMEOUT    -5   /* a sliced launch's cross-workgroup exchange  */
+                               /* did not complete (see mc_workspace_status)  */
 
 /* ---- the tape: a log density as a sum of fused distribution terms ------- */
 /* A term is  weight * sum_i dist(loc_i, scale_i).log_prob(value_i)  over n
@@ -104,6 +106,22 @@ int mc_program_destroy(mc_program* prog);
 int32_t mc_program_num_params(const mc_program* prog);
 /* The launch geometry the engine picked: waves per chain (1, 4 or 16).     */
 int32_t mc_program_waves_per_chain(const mc_program* prog);
+
+/* Sliced layout (HMC only; hmc.py:7-206 with a different work split).  A
+ * program whose terms each have at most one per-element parameter operand
+ * can be split into S data slices: parameters touched by one slice only
+ * become private to it, broadcast parameters are replicated, and one
+ * workgroup evaluates one slice for a block of 8 or 16 chains; the slices of
+ * a block exchange their log p / broadcast-cotangent / kinetic partials once
+ * per leapfrog step.  Results equal the chain-per-workgroup kernel's up to
+ * fp32 summation order and do not depend on how chains are split over
+ * launches or GPUs.  num_slices: 0 = automatic (the default chosen by
+ * mc_program_create: 16 for >= 65536 elements, 8 for >= 16384, else off),
+ * 1 = off, 2..64 = that many (MC_ERR_UNSUPPORTED if the program does not
+ * qualify).  NUTS, mc_logp_grad and mc_state_init always use the
+ * chain-per-workgroup kernels.                                              */
+int mc_program_set_slices(mc_program* prog, int32_t num_slices);
+int32_t mc_program_num_slices(const mc_program* prog);
 
 /* Batched tape evaluation: for every point p, logp[p] = log density at
  * q[p, :] and grad[p, :] = its gradient (replaces hmc.py:53-67 mx.grad).   */
@@ -195,6 +213,11 @@ typedef struct mc_trace {
  * NULL.  workspace: mc_hmc_workspace_bytes() bytes of device memory (may be
  * 0 bytes when the per-chain arena fits in LDS).                            */
 int64_t mc_hmc_workspace_bytes(const mc_program* prog, int64_t num_chains);
+/* After a sliced mc_hmc_run: MC_OK, or MC_ERR_TIMEOUT if an exchange timed
+ * out (the launch then left its chains' state unchanged or partial).
+ * Synchronises the stream.  Always MC_OK for an unsliced program.         */
+int mc_workspace_status(const mc_program* prog, const void* workspace_dev,
+                        int64_t workspace_bytes, void* hip_stream);
 int mc_hmc_run(const mc_program* prog, const mc_run_config* cfg,
                void* state_dev, float* samples_dev, const mc_trace* trace,
                void* workspace_dev, int64_t workspace_bytes, void* hip_stream);

@@ -144,6 +144,16 @@ class ChainSet:
             ctypes.byref(tr) if tr is not None else None, _lib.ptr(ws),
             ws.numel() if ws is not None else 0, _lib.stream_handle()))
 
+    def check_status(self) -> None:
+        """Raise if a sliced HMC launch's cross-workgroup exchange timed out
+        (synchronises the stream; a no-op for unsliced programs)."""
+        ws = self._ws
+        if ws is None:
+            return
+        _lib.check(self.lib.mc_workspace_status(
+            self.program.handle, _lib.ptr(ws), ws.numel() if ws is not None else 0,
+            _lib.stream_handle()))
+
     def run_nuts(self, *, samples=None, trace: Optional[Trace] = None, **cfg):
         c = self._config(**cfg)
         need = self.lib.mc_nuts_workspace_bytes(self.program.handle, self.C, c.max_tree_depth)

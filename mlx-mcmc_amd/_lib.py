@@ -136,6 +136,8 @@ SIGNATURES = [
     ("mc_program_destroy", ctypes.c_int, [_VP]),
     ("mc_program_num_params", ctypes.c_int32, [_VP]),
     ("mc_program_waves_per_chain", ctypes.c_int32, [_VP]),
+    ("mc_program_set_slices", ctypes.c_int, [_VP, ctypes.c_int32]),
+    ("mc_program_num_slices", ctypes.c_int32, [_VP]),
     ("mc_logp_grad", ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP, _VP, _VP]),
     ("mc_dist_log_prob", ctypes.c_int,
      [ctypes.c_int32, ctypes.c_int64, _VP, ctypes.c_int32, _VP, ctypes.c_int32, _VP,
@@ -145,6 +147,7 @@ SIGNATURES = [
      [_VP, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     ("mc_state_init", ctypes.c_int, [_VP, ctypes.c_int64, _VP, ctypes.c_double, _VP, _VP]),
     ("mc_hmc_workspace_bytes", ctypes.c_int64, [_VP, ctypes.c_int64]),
+    ("mc_workspace_status", ctypes.c_int, [_VP, _VP, ctypes.c_int64, _VP]),
     ("mc_hmc_run", ctypes.c_int,
      [_VP, ctypes.POINTER(McRunConfig), _VP, _VP, ctypes.POINTER(McTrace), _VP,
       ctypes.c_int64, _VP]),

@@ -476,6 +476,14 @@ class Program:
             index.ctypes.data_as(ctypes.c_void_p), index.size, ctypes.byref(h)))
         self.handle = h
         self.waves_per_chain = lib.mc_program_waves_per_chain(h)
+        self.num_slices = lib.mc_program_num_slices(h)
+
+    def set_slices(self, num_slices: int) -> None:
+        """HMC work split (include/mcmc355.h mc_program_set_slices): 0 automatic,
+        1 one chain per workgroup, >= 2 that many data slices per chain."""
+        lib = _lib.load()
+        _lib.check(lib.mc_program_set_slices(self.handle, int(num_slices)))
+        self.num_slices = lib.mc_program_num_slices(self.handle)
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -487,6 +495,9 @@ class Program:
             self.handle = None
 
 
-def compile_model(log_prob_fn, initial_params: dict) -> Program:
+def compile_model(log_prob_fn, initial_params: dict, slices: int = 0) -> Program:
     _lib.require_device()
-    return Program(trace(log_prob_fn, initial_params))
+    prog = Program(trace(log_prob_fn, initial_params))
+    if slices:
+        prog.set_slices(slices)
+    return prog

@@ -17,6 +17,7 @@
 #include "internal.h"
 #include "nuts.h"
 #include "philox.h"
+#include "sliced.h"
 
 using namespace mc;
 
@@ -45,6 +46,23 @@ static int fail(int code, const char* fmt, ...) {
 // ---------------------------------------------------------------------------
 // program
 // ---------------------------------------------------------------------------
+// Host copy of a sliced layout (sliced.h) and its device tables.
+struct SlicePlan {
+    int S = 1, Lp = 0, Pmax = 0, Dsh = 0, nitems = 0, sdata_floats = 0, nb_max = 0, combine = 0;
+    std::vector<SlTerm> terms;
+    std::vector<SlTerm> sterms;  // scalar terms (after the exchange)
+    std::vector<float> data;
+    std::vector<int32_t> index;
+    std::vector<int64_t> blocks;
+    std::vector<int32_t> gidx;
+    SlTerm* d_terms = nullptr;
+    SlTerm* d_sterms = nullptr;
+    float* d_data = nullptr;
+    int32_t* d_index = nullptr;
+    int64_t* d_blocks = nullptr;
+    int32_t* d_gidx = nullptr;
+};
+
 struct mc_program {
     int32_t D = 0;
     float lp_const = 0.0f;
@@ -56,6 +74,12 @@ struct mc_program {
     DevTerm* d_terms = nullptr;
     float* d_data = nullptr;
     int32_t* d_index = nullptr;
+    // terms as validated (before the chain-per-workgroup tiling) and the host
+    // pools they point into: the input of the slice planner
+    std::vector<DevTerm> raw;
+    std::vector<float> h_data;
+    std::vector<int32_t> h_index;
+    SlicePlan sl;
 };
 
 static DevCtx ctx_of(const mc_program* p) {
@@ -214,6 +238,469 @@ static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<in
     return MC_OK;
 }
 
+// ---------------------------------------------------------------------------
+// sliced layout planner (sliced.h)
+// ---------------------------------------------------------------------------
+static void free_slices(SlicePlan& P) {
+    if (P.d_terms) (void)hipFree(P.d_terms);
+    if (P.d_sterms) (void)hipFree(P.d_sterms);
+    if (P.d_data) (void)hipFree(P.d_data);
+    if (P.d_index) (void)hipFree(P.d_index);
+    if (P.d_blocks) (void)hipFree(P.d_blocks);
+    if (P.d_gidx) (void)hipFree(P.d_gidx);
+    P = SlicePlan();
+}
+
+static SlCtx slctx_of(const mc_program* p) {
+    SlCtx c;
+    std::memset(&c, 0, sizeof(c));
+    const SlicePlan& P = p->sl;
+    c.terms = P.d_terms;
+    c.data = P.d_data;
+    c.index = P.d_index;
+    c.blocks = P.d_blocks;
+    c.gidx = P.d_gidx;
+    c.n_terms = (int32_t)p->raw.size();
+    c.S = P.S;
+    c.Lp = P.Lp;
+    c.Pmax = P.Pmax;
+    c.Dsh = P.Dsh;
+    c.D = p->D;
+    c.nitems = P.nitems;
+    c.sdata_floats = P.sdata_floats;
+    c.lp_const = p->lp_const;
+    c.combine = P.combine;
+    c.sterms = P.d_sterms;
+    c.n_sterms = (int32_t)P.sterms.size();
+    return c;
+}
+
+static int sl_lds_bytes(const mc_program* p, int nb) {
+    const SlCtx c = slctx_of(p);
+    return 4 * (nb == 16 ? SlLayout<16>(c).total : SlLayout<8>(c).total);
+}
+
+static constexpr int kSlLdsBudget = 150 * 1024;
+
+static int64_t pp_index(const DevTerm& t, int a, int64_t i, const std::vector<int32_t>& ip) {
+    const DevOperand& o = t.op[a];
+    return o.kind == MC_OP_PVEC ? (int64_t)o.poff + i : (int64_t)o.poff + ip[o.pool + i];
+}
+
+static int plan_slices(mc_program* p, int S, SlicePlan& P) {
+    const std::vector<DevTerm>& raw = p->raw;
+    const std::vector<float>& dp = p->h_data;
+    const std::vector<int32_t>& ip = p->h_index;
+    const int D = p->D;
+    const int nT = (int)raw.size();
+    const int T = kSlLanes;  // run slots per chain pair
+    std::vector<int> ppr(nT, -1);
+    for (int t = 0; t < nT; ++t)
+        for (int a = 0; a < 3; ++a)
+            if (raw[t].op[a].kind == MC_OP_PVEC || raw[t].op[a].kind == MC_OP_GATHER) {
+                if (ppr[t] >= 0)
+                    return fail(MC_ERR_UNSUPPORTED,
+                                "term %d has two per-element parameter operands: not sliceable", t);
+                ppr[t] = a;
+            }
+    // shared (broadcast) parameters and the private parameters' costs
+    std::vector<char> shared(D, 0);
+    for (const DevTerm& t : raw)
+        for (int a = 0; a < 3; ++a)
+            if (t.op[a].kind == MC_OP_PSCALAR) shared[t.op[a].poff] = 1;
+    std::vector<int64_t> cost(D, 1);
+    for (int t = 0; t < nT; ++t)
+        if (ppr[t] >= 0)
+            for (int64_t i = 0; i < raw[t].n; ++i) {
+                const int64_t j = pp_index(raw[t], ppr[t], i, ip);
+                if (!shared[j]) cost[j] += 1;
+            }
+    int64_t total = 0;
+    for (int j = 0; j < D; ++j)
+        if (!shared[j]) total += cost[j];
+    std::vector<int> owner(D, 0), lidx(D, 0), jsh(D, -1);
+    std::vector<std::vector<int>> priv(S);
+    std::vector<int> shl;
+    {
+        int64_t run = 0;
+        for (int j = 0; j < D; ++j) {
+            if (shared[j]) {
+                jsh[j] = (int)shl.size();
+                shl.push_back(j);
+                continue;
+            }
+            const int s = (int)std::min<int64_t>(S - 1, (2 * run + cost[j]) * S / (2 * std::max<int64_t>(total, 1)));
+            owner[j] = s;
+            lidx[j] = (int)priv[s].size();
+            priv[s].push_back(j);
+            run += cost[j];
+        }
+    }
+    P.S = S;
+    P.Dsh = (int)shl.size();
+    P.Pmax = 0;
+    for (int s = 0; s < S; ++s) P.Pmax = std::max<int>(P.Pmax, (int)priv[s].size());
+    P.Lp = std::max(4, (P.Pmax + P.Dsh + 3) / 4 * 4);
+    P.nitems = P.Dsh + 3;
+    P.gidx.assign((size_t)S * P.Lp, -1);
+    for (int s = 0; s < S; ++s)
+        for (size_t k = 0; k < priv[s].size(); ++k) P.gidx[(size_t)s * P.Lp + k] = priv[s][k];
+    for (int s = 0; s < S; ++s)
+        for (int j = 0; j < P.Dsh; ++j) P.gidx[(size_t)s * P.Lp + P.Pmax + j] = shl[j];
+    P.terms.assign((size_t)S * nT, SlTerm());
+    P.blocks.assign(3 * (size_t)S, 0);
+    P.sdata_floats = 0;
+
+    // operand kinds of a slice term (SK_*)
+    auto make_slterm = [&](const DevTerm& rt, int t) {
+        SlTerm st;
+        std::memset(&st, 0, sizeof(st));
+        st.dist = rt.dist;
+        st.pp = ppr[t];
+        st.weight = rt.weight;
+        st.c0 = rt.c0;
+        if (rt.op[2].kind == MC_OP_CONST) {
+            const float c = rt.op[2].cval;
+            st.clogs = (float)std::log((double)c);
+            st.cinv = 1.0f / c;
+            st.cinv2 = 1.0f / (c * c);
+        }
+        for (int a = 0; a < 3; ++a) {
+            const DevOperand& o = rt.op[a];
+            st.kloc[a] = -1;
+            switch (o.kind) {
+                case MC_OP_CONST: st.kind[a] = SK_CONST; st.cval[a] = o.cval; break;
+                case MC_OP_PSCALAR:
+                    st.kind[a] = SK_SHARED;
+                    st.jsh[a] = jsh[o.poff];
+                    st.kloc[a] = P.Pmax + jsh[o.poff];
+                    break;
+                case MC_OP_DATA: st.kind[a] = SK_DATA; break;
+                case MC_OP_PVEC:
+                case MC_OP_GATHER: st.kind[a] = SK_PP; break;
+                default: st.kind[a] = SK_NONE; break;
+            }
+        }
+        st.mode = (st.kind[2] == SK_DATA || st.kind[2] == SK_PP) ? 1 : 0;
+        return st;
+    };
+    // scalar terms (only constants and broadcast parameters): evaluated once
+    // per chain after every exchange, in every slice, not split into slices
+    std::vector<char> scalar(nT, 0);
+    P.sterms.clear();
+    for (int t = 0; t < nT; ++t) {
+        bool sc = true;
+        for (int a = 0; a < 3; ++a) {
+            const int k = raw[t].op[a].kind;
+            if (k != MC_OP_CONST && k != MC_OP_PSCALAR && k != MC_OP_NONE) sc = false;
+        }
+        scalar[t] = sc;
+        if (sc) {
+            SlTerm st = make_slterm(raw[t], t);
+            if (raw[t].n > INT32_MAX) return fail(MC_ERR_UNSUPPORTED, "scalar term too long");
+            st.niter = (int32_t)raw[t].n;  // element count
+            P.sterms.push_back(st);
+        }
+    }
+
+    // element -> slice
+    std::vector<std::vector<std::vector<int64_t>>> elems(S, std::vector<std::vector<int64_t>>(nT));
+    for (int t = 0; t < nT; ++t) {
+        if (scalar[t]) continue;
+        const int64_t n = raw[t].n;
+        for (int64_t i = 0; i < n; ++i) {
+            int s;
+            if (ppr[t] >= 0) {
+                const int64_t j = pp_index(raw[t], ppr[t], i, ip);
+                s = shared[j] ? 0 : owner[j];
+            } else if (n < 256) {
+                s = t % S;  // small terms go whole to one slice, round robin
+            } else {
+                s = (int)(i * S / n);
+            }
+            elems[s][t].push_back(i);
+        }
+    }
+
+    struct Run {
+        int32_t k;
+        int64_t first;
+        int32_t len;
+    };
+    for (int s = 0; s < S; ++s) {
+        while (P.data.size() % 4) P.data.push_back(0.0f);
+        const int64_t blk0 = (int64_t)P.data.size();
+        // ---- runs of every term of this slice ----
+        std::vector<std::vector<Run>> runs(nT);
+        std::vector<char> direct(nT, 0);
+        for (int t = 0; t < nT; ++t) {
+            const DevTerm& rt = raw[t];
+            const std::vector<int64_t>& E = elems[s][t];
+            const int64_t nE = (int64_t)E.size();
+            std::vector<Run>& R = runs[t];
+            if (nE > 0 && ppr[t] >= 0) {
+                std::vector<Run> nat;
+                for (int64_t e = 0; e < nE; ++e) {
+                    const int64_t j = pp_index(rt, ppr[t], E[e], ip);
+                    const int32_t k = shared[j] ? P.Pmax + jsh[j] : lidx[j];
+                    if (e > 0 && nat.back().k == k && nat.back().len < INT32_MAX) {
+                        ++nat.back().len;
+                    } else {
+                        nat.push_back({k, e, 1});
+                    }
+                }
+                // few long runs: split them so that the lanes get near-equal
+                // work (m runs per lane); otherwise keep whole runs
+                int64_t Lt = INT64_MAX;
+                const int64_t nn = (int64_t)nat.size();
+                if (nn <= 4 * T) {
+                    const int64_t m = (nn + T - 1) / T;
+                    int64_t lo = 1, hi = 1;
+                    for (const Run& r : nat) hi = std::max<int64_t>(hi, r.len);
+                    while (lo < hi) {
+                        const int64_t mid = (lo + hi) / 2;
+                        int64_t pieces = 0;
+                        for (const Run& r : nat) pieces += (r.len + mid - 1) / mid;
+                        if (pieces <= T * m) hi = mid; else lo = mid + 1;
+                    }
+                    Lt = lo;
+                }
+                for (const Run& r : nat) {
+                    const int64_t pieces = (Lt == INT64_MAX) ? 1 : (r.len + Lt - 1) / Lt;
+                    const int64_t base = r.len / pieces, rem = r.len % pieces;
+                    int64_t f = r.first;
+                    for (int64_t pc = 0; pc < pieces; ++pc) {
+                        const int32_t pl = (int32_t)(base + (pc < rem ? 1 : 0));
+                        R.push_back({r.k, f, pl});
+                        f += pl;
+                    }
+                }
+                std::vector<int32_t> ks;
+                for (const Run& r : R) ks.push_back(r.k);
+                std::sort(ks.begin(), ks.end());
+                direct[t] = std::adjacent_find(ks.begin(), ks.end()) == ks.end();
+            } else if (nE > 0) {
+                const int64_t nch = std::min<int64_t>(T, nE);
+                int64_t f = 0;
+                for (int64_t c = 0; c < nch; ++c) {
+                    const int32_t pl = (int32_t)(nE / nch + (c < nE % nch ? 1 : 0));
+                    R.push_back({-1, f, pl});
+                    f += pl;
+                }
+            }
+            if ((int64_t)R.size() > INT32_MAX / 4)
+                return fail(MC_ERR_UNSUPPORTED, "slice term too large");
+        }
+        // ---- runs -> lanes.  A parameter's direct runs share one lane in
+        // every term (so direct-write terms need no barrier between them):
+        // the map is built from the largest direct term first, longest run
+        // first onto the least loaded lane; other runs likewise per term ----
+        std::vector<std::vector<int32_t>> rl(nT), rit(nT);
+        std::vector<int32_t> lane_of_k(P.Lp, -1);
+        {
+            std::vector<int> order(nT);
+            std::iota(order.begin(), order.end(), 0);
+            auto total = [&](int t) {
+                int64_t x = 0;
+                for (const Run& r : runs[t]) x += r.len;
+                return x;
+            };
+            std::stable_sort(order.begin(), order.end(),
+                             [&](int a2, int b2) { return total(a2) > total(b2); });
+            std::vector<int64_t> kload(T, 0);  // load of the shared k->lane map
+            for (int t : order) {
+                const std::vector<Run>& R = runs[t];
+                const int64_t nr = (int64_t)R.size();
+                rl[t].assign(nr, 0);
+                rit[t].assign(nr, 0);
+                std::vector<int64_t> ord(nr);
+                std::iota(ord.begin(), ord.end(), 0);
+                std::stable_sort(ord.begin(), ord.end(),
+                                 [&](int64_t a2, int64_t b2) { return R[a2].len > R[b2].len; });
+                std::vector<int64_t> load(T, 0);
+                std::vector<int32_t> cnt(T, 0);
+                for (int64_t r : ord) {
+                    int lane;
+                    if (direct[t] && lane_of_k[R[r].k] >= 0) {
+                        lane = lane_of_k[R[r].k];
+                    } else {
+                        std::vector<int64_t>& L = direct[t] ? kload : load;
+                        lane = 0;
+                        for (int l = 1; l < T; ++l)
+                            if (L[l] < L[lane]) lane = l;
+                        if (direct[t]) lane_of_k[R[r].k] = lane;
+                    }
+                    if (direct[t]) kload[lane] += R[r].len;
+                    load[lane] += R[r].len;
+                    rl[t][r] = lane;
+                    rit[t][r] = cnt[lane]++;
+                }
+            }
+        }
+        // ---- per-term tables and tiled data, in program order ----
+        for (int t = 0; t < nT; ++t) {
+            const DevTerm& rt = raw[t];
+            const std::vector<int64_t>& E = elems[s][t];
+            const std::vector<Run>& R = runs[t];
+            const int64_t nr = (int64_t)R.size();
+            SlTerm st = make_slterm(rt, t);
+            st.direct = direct[t];
+            int32_t niter = 0;
+            for (int64_t r = 0; r < nr; ++r) niter = std::max(niter, rit[t][r] + 1);
+            st.niter = scalar[t] ? 0 : niter;
+            // tiles per iteration
+            std::vector<int32_t> tiles(3 * (size_t)niter, 0);
+            std::vector<int64_t> toff(niter, 0);
+            {
+                std::vector<int32_t> lmax(niter, 0), lmin(niter, INT32_MAX);
+                for (int64_t r = 0; r < nr; ++r) {
+                    const int32_t it = rit[t][r];
+                    lmax[it] = std::max(lmax[it], R[r].len);
+                    lmin[it] = std::min(lmin[it], R[r].len);
+                }
+                int64_t tot = 0;
+                for (int32_t it = 0; it < niter; ++it) {
+                    const int64_t lpad = (lmax[it] + 3) / 4 * 4;
+                    toff[it] = tot;
+                    tiles[3 * it + 1] = lmax[it];
+                    tiles[3 * it + 2] = lmax[it] > 0 ? lmin[it] / 4 : 0;
+                    tot += (int64_t)T * lpad;
+                }
+                // tiled data operands (offsets relative to the slice block)
+                for (int a = 0; a < 3; ++a) {
+                    if (st.kind[a] != SK_DATA) continue;
+                    while (P.data.size() % 4) P.data.push_back(0.0f);
+                    const int64_t base = (int64_t)P.data.size();
+                    P.data.resize(base + tot, 0.0f);
+                    const int64_t src = rt.op[a].pool;
+                    for (int64_t r = 0; r < nr; ++r) {
+                        const int64_t o = base + toff[rit[t][r]] + rl[t][r] * 4;
+                        for (int32_t u = 0; u < R[r].len; ++u)
+                            P.data[o + (u >> 2) * (4 * T) + (u & 3)] =
+                                dp[src + E[R[r].first + u]];
+                    }
+                    st.doff[a] = (int32_t)(base - blk0);
+                }
+                for (int32_t it = 0; it < niter; ++it) {
+                    if (toff[it] > INT32_MAX / 2)
+                        return fail(MC_ERR_UNSUPPORTED, "slice data too large");
+                    tiles[3 * it] = (int32_t)toff[it];
+                }
+            }
+            // lane records per (iteration, lane); empty {-1, 0}
+            std::vector<int32_t> lanes(2 * (size_t)niter * T, 0);
+            for (int64_t x = 0; x < (int64_t)niter * T; ++x) lanes[2 * x] = -1;
+            for (int64_t r = 0; r < nr; ++r) {
+                const int64_t x = (int64_t)rit[t][r] * T + rl[t][r];
+                lanes[2 * x] = R[r].k;
+                lanes[2 * x + 1] = R[r].len;
+            }
+            // combine entries per round of kSlItr iterations (split runs only):
+            // the runs of one parameter, positions in run order
+            std::vector<int32_t> roff, ents, plist;
+            const int32_t nrounds = (niter + kSlItr - 1) / kSlItr;
+            for (int32_t rd = 0; rd < nrounds; ++rd) {
+                roff.push_back((int32_t)(ents.size() / 3));
+                if (st.direct || ppr[t] < 0) continue;
+                for (int64_t r = 0; r < nr;) {
+                    int64_t q = r;
+                    while (q < nr && R[q].k == R[r].k) ++q;
+                    std::vector<int32_t> ps;
+                    for (int64_t x = r; x < q; ++x)
+                        if (rit[t][x] / kSlItr == rd)
+                            ps.push_back((int32_t)((rit[t][x] % kSlItr) * T + rl[t][x]));
+                    if (!ps.empty()) {
+                        ents.push_back(R[r].k);
+                        ents.push_back((int32_t)plist.size());
+                        ents.push_back((int32_t)ps.size());
+                        plist.insert(plist.end(), ps.begin(), ps.end());
+                    }
+                    r = q;
+                }
+            }
+            roff.push_back((int32_t)(ents.size() / 3));
+            // the tables go into the slice block as int32 words
+            auto put = [&](const std::vector<int32_t>& v, bool even) -> int32_t {
+                while (P.data.size() % (even ? 2 : 1)) P.data.push_back(0.0f);
+                const int64_t o = (int64_t)P.data.size();
+                P.data.resize(o + v.size());
+                if (!v.empty()) std::memcpy(&P.data[o], v.data(), v.size() * 4);
+                return (int32_t)(o - blk0);
+            };
+            st.tile_off = put(tiles, false);
+            st.lane_off = put(lanes, true);
+            st.round_off = put(roff, false);
+            st.comb_off = put(ents, false);
+            st.pos_off = put(plist, false);
+            if (st.pp >= 0 && !st.direct && st.niter > 0) P.combine = 1;
+            P.terms[(size_t)s * nT + t] = st;
+        }
+        while (P.data.size() % 4) P.data.push_back(0.0f);
+        const int64_t blen = (int64_t)P.data.size() - blk0;
+        P.blocks[3 * s] = blk0;
+        P.blocks[3 * s + 1] = blen;
+        P.blocks[3 * s + 2] = (int64_t)priv[s].size();
+        if (blen > INT32_MAX / 8) return fail(MC_ERR_UNSUPPORTED, "slice data too large");
+        P.sdata_floats = std::max<int>(P.sdata_floats, (int)blen);
+    }
+    if (P.index.empty()) P.index.push_back(0);
+    if (P.data.empty()) P.data.assign(4, 0.0f);
+    return MC_OK;
+}
+
+template <typename T>
+static hipError_t upload(T** dst, const std::vector<T>& v) {
+    hipError_t e = hipMalloc(dst, v.size() * sizeof(T));
+    if (e == hipSuccess) e = hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+    return e;
+}
+
+static int auto_slices(const mc_program* p) {
+    int64_t n = 0;
+    for (const DevTerm& t : p->raw) n += t.n;
+    if (n >= 65536) return 16;
+    if (n >= 16384) return 8;
+    return 1;
+}
+
+extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
+    if (!p) return fail(MC_ERR_INVALID, "program is NULL");
+    if (S < 0 || S > 64) return fail(MC_ERR_INVALID, "num_slices must be in [0, 64]");
+    const bool automatic = (S == 0);
+    if (automatic) S = auto_slices(p);
+    free_slices(p->sl);
+    if (S <= 1) return MC_OK;
+    SlicePlan P;
+    int rc = plan_slices(p, S, P);
+    if (rc == MC_OK) {
+        p->sl = P;  // host tables; geometry below needs them in place
+        p->sl.nb_max = sl_lds_bytes(p, 16) <= kSlLdsBudget ? 16
+                     : (sl_lds_bytes(p, 8) <= kSlLdsBudget ? 8 : 0);
+        if (p->sl.nb_max == 0)
+            rc = fail(MC_ERR_UNSUPPORTED, "slice state (%d bytes) exceeds the LDS budget",
+                      sl_lds_bytes(p, 8));
+    }
+    if (rc != MC_OK) {
+        free_slices(p->sl);
+        return automatic ? MC_OK : rc;  // automatic: stay on the unsliced kernels
+    }
+    SlicePlan& Q = p->sl;
+    hipError_t e = upload(&Q.d_terms, Q.terms);
+    if (e == hipSuccess && !Q.sterms.empty()) e = upload(&Q.d_sterms, Q.sterms);
+    if (e == hipSuccess) e = upload(&Q.d_data, Q.data);
+    if (e == hipSuccess) e = upload(&Q.d_index, Q.index);
+    if (e == hipSuccess) e = upload(&Q.d_blocks, Q.blocks);
+    if (e == hipSuccess) e = upload(&Q.d_gidx, Q.gidx);
+    if (e != hipSuccess) {
+        free_slices(p->sl);
+        return fail(e == hipErrorOutOfMemory ? MC_ERR_NOMEM : MC_ERR_HIP,
+                    "slice upload failed: %s", hipGetErrorString(e));
+    }
+    return MC_OK;
+}
+
+extern "C" int32_t mc_program_num_slices(const mc_program* p) { return p ? p->sl.S : -1; }
+
 extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t n_params,
                                  float lp_const, const float* data, int64_t n_data,
                                  const int32_t* index, int64_t n_index, mc_program** out) {
@@ -226,7 +713,7 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
 
     std::vector<float> dpool(data, data + n_data);
     std::vector<int32_t> ipool(index, index + n_index);
-    std::vector<DevTerm> dts;
+    std::vector<DevTerm> dts, raws;
     int64_t max_n = 0;
     for (int32_t t = 0; t < n_terms; ++t) max_n = std::max<int64_t>(max_n, terms[t].n);
     const int wpc = choose_wpc(max_n);
@@ -336,6 +823,7 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
                 }
             }
         }
+        raws.push_back(dt);
         // pass planning: accumulating vector operands with overlapping parameter
         // ranges go to different sweeps
         int64_t lo[3], hi[3];
@@ -464,6 +952,9 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
     p->max_n = max_n;
     p->wpc = wpc;
     p->terms = dts;
+    p->raw = raws;
+    p->h_data = dpool;
+    p->h_index = ipool;
     hipError_t e = hipSuccess;
     if (!dts.empty()) {
         e = hipMalloc(&p->d_terms, dts.size() * sizeof(DevTerm));
@@ -488,12 +979,20 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
         return fail(e == hipErrorOutOfMemory ? MC_ERR_NOMEM : MC_ERR_HIP,
                     "program upload failed: %s", hipGetErrorString(e));
     }
+    {
+        const int rc = mc_program_set_slices(p, 0);
+        if (rc != MC_OK) {
+            mc_program_destroy(p);
+            return rc;
+        }
+    }
     *out = p;
     return MC_OK;
 }
 
 extern "C" int mc_program_destroy(mc_program* p) {
     if (!p) return MC_OK;
+    free_slices(p->sl);
     if (p->d_terms) (void)hipFree(p->d_terms);
     if (p->d_data) (void)hipFree(p->d_data);
     if (p->d_index) (void)hipFree(p->d_index);
@@ -726,8 +1225,85 @@ static int check_cfg(const mc_program* p, const mc_run_config* cfg, void* state)
     return MC_OK;
 }
 
+// ---- sliced launches ---------------------------------------------------------
+static int device_cus() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (cached[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 0;
+        cached[dev] = n;
+    }
+    return cached[dev];
+}
+static bool sliced(const mc_program* p) { return p->sl.S >= 2 && p->sl.d_terms != nullptr; }
+static int sl_nb_for(const mc_program* p, int64_t C) {
+    return (p->sl.nb_max >= 16 && C > 8) ? 16 : 8;
+}
+// chain blocks per launch: every workgroup of a launch must be resident at
+// once (the slices of a block wait for each other), one workgroup per CU
+static int64_t sl_groups_per_launch(const mc_program* p, int64_t C) {
+    const int nb = sl_nb_for(p, C);
+    const int64_t groups = (C + nb - 1) / nb;
+    const int64_t cap = std::max<int64_t>(1, device_cus() / p->sl.S);
+    return std::min(groups, cap);
+}
+static constexpr int64_t kSlStatusBytes = 256;
+static int64_t sl_workspace_bytes(const mc_program* p, int64_t C) {
+    const int nb = sl_nb_for(p, C);
+    return kSlStatusBytes +
+           2 * sl_groups_per_launch(p, C) * p->sl.S * (int64_t)p->sl.nitems * nb * 8;
+}
+
+template <int NB>
+static int launch_hmc_sl(const mc_program* p, const mc_run_config* cfg, void* state,
+                         float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
+    int64_t qo, go;
+    mc_state_offsets(p, cfg->num_chains, &qo, &go);
+    char* b = (char*)state;
+    RunArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.cfg = *cfg;
+    const SlCtx ctx = slctx_of(p);
+    const size_t lds = (size_t)SlLayout<NB>(ctx).total * 4;
+    MC_HIP_TRY(allow_lds(k_hmc_sl<NB>, lds));
+    const int64_t C = cfg->num_chains;
+    const int64_t groups = (C + NB - 1) / NB;
+    const int64_t gpl = sl_groups_per_launch(p, C);
+    const int64_t used = sl_workspace_bytes(p, C);
+    int* status = (int*)ws;
+    unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
+    for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
+        const int64_t ng = std::min(gpl, groups - g0);
+        // the exchange tags restart at 1 in every launch: clear the granules
+        // (and, first, the status word) ahead of it
+        MC_HIP_TRY(hipMemsetAsync(g0 == 0 ? ws : (void*)xch, 0,
+                                  g0 == 0 ? used : used - kSlStatusBytes, st));
+        hipLaunchKernelGGL(k_hmc_sl<NB>, dim3((unsigned)(ng * p->sl.S)), dim3(kSlLanes * NB / 2), lds, st, ctx,
+                           A, g0 * NB, ng, (mc_chain_scalars*)b, (float*)(b + qo),
+                           (float*)(b + go), samples, trace_of(tr), xch, status);
+        MC_HIP_TRY(hipGetLastError());
+    }
+    return MC_OK;
+}
+
+extern "C" int mc_workspace_status(const mc_program* p, const void* ws, int64_t bytes,
+                                   void* stream) {
+    if (!p) return fail(MC_ERR_INVALID, "program is NULL");
+    if (!sliced(p)) return MC_OK;
+    if (!ws || bytes < kSlStatusBytes) return fail(MC_ERR_INVALID, "bad workspace");
+    int v = 0;
+    MC_HIP_TRY(hipMemcpyAsync(&v, ws, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    MC_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    if (v != 0) return fail(MC_ERR_TIMEOUT, "sliced HMC: a cross-workgroup exchange timed out");
+    return MC_OK;
+}
+
 extern "C" int64_t mc_hmc_workspace_bytes(const mc_program* p, int64_t C) {
     if (!p || C < 0) return -1;
+    if (sliced(p)) return sl_workspace_bytes(p, C);
     if (hmc_use_lds(p)) return 0;
     return C * 5 * (int64_t)dpad_of(p->D) * 4;
 }
@@ -760,6 +1336,15 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
     if (rc) return rc;
     if (cfg->num_leapfrog_steps < 0) return fail(MC_ERR_INVALID, "num_leapfrog_steps < 0");
     if (cfg->num_chains == 0 || cfg->iter_count == 0) return MC_OK;
+    if (sliced(p)) {
+        const int64_t need = sl_workspace_bytes(p, cfg->num_chains);
+        if (ws == nullptr || ws_bytes < need)
+            return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
+        if (device_cus() <= 0) return fail(MC_ERR_HIP, "no HIP device");
+        return sl_nb_for(p, cfg->num_chains) == 16
+                   ? launch_hmc_sl<16>(p, cfg, state, samples, tr, ws, (hipStream_t)stream)
+                   : launch_hmc_sl<8>(p, cfg, state, samples, tr, ws, (hipStream_t)stream);
+    }
     const bool lds = hmc_use_lds(p);
     const int64_t need = mc_hmc_workspace_bytes(p, cfg->num_chains);
     if (!lds && (ws == nullptr || ws_bytes < need))

@@ -51,19 +51,45 @@ MC_DEV unsigned long long mc_now() {
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     return t;
 }
+// per-workgroup accumulators in LDS (a global read-modify-write per stamp
+// would be waited for by every later barrier and inflate those sections)
+MC_DEV unsigned long long* mc_stamp_lds() {
+    __shared__ unsigned long long acc[2 * 16 * 32];
+    return acc;
+}
+MC_DEV void stamp_init() {
+    unsigned long long* a = mc_stamp_lds();
+    for (int i = threadIdx.x; i < 2 * 16 * 32; i += blockDim.x) a[i] = 0;
+    __syncthreads();
+}
 MC_DEV void stamp(StampClock& c, int sec) {
     const unsigned long long t = mc_now();
-    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && threadIdx.x < 16 * 64) {
-        mc_stamp_acc[(threadIdx.x >> 6) * 32 + sec] += t - c.last;
-        mc_stamp_cnt[(threadIdx.x >> 6) * 32 + sec] += 1;
+    if ((threadIdx.x & 63) == 0 && threadIdx.x < 16 * 64) {
+        unsigned long long* a = mc_stamp_lds();
+        a[(threadIdx.x >> 6) * 32 + sec] += t - c.last;
+        a[512 + (threadIdx.x >> 6) * 32 + sec] += 1;
     }
     c.last = mc_now();
 }
+MC_DEV void stamp_flush() {
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && threadIdx.x < 16 * 64) {
+        const unsigned long long* a = mc_stamp_lds();
+        const int w = threadIdx.x >> 6;
+        for (int s = 0; s < 32; ++s) {
+            mc_stamp_acc[w * 32 + s] += a[w * 32 + s];
+            mc_stamp_cnt[w * 32 + s] += a[512 + w * 32 + s];
+        }
+    }
+}
+#define MC_STAMP_INIT stamp_init();
+#define MC_STAMP_FLUSH stamp_flush();
 #define MC_STAMP_DECL StampClock mc_clk{mc_now()};
 #define MC_STAMP(sec) stamp(mc_clk, sec)
 #else
 #define MC_STAMP_DECL
 #define MC_STAMP(sec)
+#define MC_STAMP_INIT
+#define MC_STAMP_FLUSH
 #endif
 
 template <typename T>

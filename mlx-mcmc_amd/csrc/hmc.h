@@ -47,6 +47,7 @@ k_hmc(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, flo
     float* gB = arena + 3 * Dp;
     float* p = arena + 4 * Dp;
 
+    MC_STAMP_INIT
     float lp = scal[c].logp;
     double eps = scal[c].step_size;
     int n_acc = scal[c].n_accept, n_tot = scal[c].n_total;
@@ -161,6 +162,7 @@ k_hmc(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, flo
         st_q[c * D + j] = qA[j];
         st_g[c * D + j] = gA[j];
     }
+    MC_STAMP_FLUSH
     if (G.tid == 0) {
         mc_chain_scalars& sc = scal[c];
         sc.logp = lp;

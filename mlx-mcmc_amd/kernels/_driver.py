@@ -54,7 +54,7 @@ def run_sampler(algorithm: str, log_prob_fn, initial_params, *, num_samples: int
                 max_tree_depth: int = 10, num_chains: int = 1, chain_offset: int = 0,
                 slice_mode: str = "reference", progress: bool = True,
                 progress_every: Optional[int] = None, return_trace: bool = False,
-                keep_on_device: bool = False, initial_positions=None):
+                keep_on_device: bool = False, initial_positions=None, num_slices: int = 0):
     import torch
 
     if algorithm not in ("hmc", "nuts"):
@@ -62,7 +62,7 @@ def run_sampler(algorithm: str, log_prob_fn, initial_params, *, num_samples: int
     if num_samples < 0 or num_warmup < 0:
         raise ValueError("num_samples and num_warmup must be non-negative")
     k = _as_key(key)
-    program = _trace.compile_model(log_prob_fn, initial_params)
+    program = _trace.compile_model(log_prob_fn, initial_params, slices=num_slices)
     layout = program.layout
     C = int(num_chains)
     if C < 1:
@@ -112,6 +112,7 @@ def run_sampler(algorithm: str, log_prob_fn, initial_params, *, num_samples: int
                 out(f"  Iteration {b}/{num_warmup} (accept: {100 * rate:.1f}%, "
                     f"avg_depth: {depth:.1f}, step_size: {eps:.4f})")
     torch.cuda.synchronize()
+    chains.check_status()
     t1 = time.perf_counter()
     s = stats()
     if num_warmup == 0:
@@ -144,6 +145,7 @@ def run_sampler(algorithm: str, log_prob_fn, initial_params, *, num_samples: int
                 depth = float(np.mean(s2["depth_sum"])) / (b - num_warmup)
                 out(f"  Iteration {b - num_warmup}/{num_samples} (avg_depth: {depth:.2f})")
     torch.cuda.synchronize()
+    chains.check_status()
     t2 = time.perf_counter()
     s = stats()
     n_tot = s["n_total"].astype(np.int64)

@@ -9,6 +9,8 @@ Additions (keyword-only): ``num_chains`` runs independent chains in one
 launch (samples gain a leading chain axis), ``chain_offset`` selects the RNG
 streams (for sharding chains over GPUs), ``return_info`` also returns a
 ``RunInfo`` with per-chain step sizes, timings and an optional trace.
+``num_slices`` picks the work split of large models (0 automatic, 1 one
+chain per workgroup, >= 2 data slices per chain: csrc/sliced.h).
 Vector-valued parameters are supported (the reference's ``float()`` store,
 hmc.py:192, rejects them — SURVEY Q6).
 """
@@ -20,7 +22,7 @@ from ._driver import run_sampler
 def hmc(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_size=0.1,
         num_leapfrog_steps=10, adapt_step_size=True, target_accept=0.8, key=None, *,
         num_chains=1, chain_offset=0, progress=True, return_info=False, return_trace=False,
-        keep_on_device=False, initial_positions=None):
+        keep_on_device=False, initial_positions=None, num_slices=0):
     """Hamiltonian Monte Carlo sampler using gradient information.
 
     Returns ``(samples, acceptance_rate)`` like the reference: ``samples`` maps
@@ -34,7 +36,8 @@ def hmc(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_siz
         step_size=step_size, target_accept=target_accept, adapt_step_size=adapt_step_size,
         key=key, num_leapfrog_steps=num_leapfrog_steps, num_chains=num_chains,
         chain_offset=chain_offset, progress=progress, return_trace=return_trace,
-        keep_on_device=keep_on_device, initial_positions=initial_positions)
+        keep_on_device=keep_on_device, initial_positions=initial_positions,
+        num_slices=num_slices)
     if return_info:
         return samples, rate, info
     return samples, rate

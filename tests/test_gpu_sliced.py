@@ -1,0 +1,181 @@
+"""Sliced HMC (csrc/sliced.h): a chain's log density split over S workgroups.
+
+The sliced kernel runs the same sampler as k_hmc (reference hmc.py:7-206);
+only fp32 summation order differs (per-slice partial sums, combined in slice
+order).  Parity bars:
+  * accept decisions and step sizes identical to the unsliced kernel on every
+    chain for the whole (short) run, positions within rtol 1e-3 — on models
+    that cover every operand combination the planner handles (shared-only
+    terms, per-element value / loc / scale parameters, data operands,
+    HalfNormal, small terms placed whole in one slice);
+  * bit-identical results across runs, across chain splits (chain_offset) and
+    across chain-block sizes (8 vs 16 chains per workgroup);
+  * the golden HMC trace of tests/golden/hmc_simple.json (oracle) reproduced;
+  * at the Large shape (bench.py workload) decisions match the unsliced kernel.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _m():
+    import mlx_mcmc_amd as m
+
+    return m
+
+
+# ---------------------------------------------------------------- models --
+def model_iid(ns):
+    """Only broadcast parameters: every term is shared-only (Pmax = 0)."""
+    rng = np.random.default_rng(3)
+    y = rng.normal(1.5, 2.0, 3000).astype(np.float32)
+
+    def lp(p):
+        return (ns.Normal(0.0, 10.0).log_prob(p["mu"])
+                + ns.HalfNormal(5.0).log_prob(p["sigma"])
+                + ns.sum(ns.Normal(p["mu"], p["sigma"]).log_prob(ns.array(y))))
+
+    return lp, {"mu": 0.0, "sigma": 1.0}
+
+
+def model_scale_vec(ns):
+    """Per-element scale parameter (elementwise mode) + HalfNormal value pp."""
+    rng = np.random.default_rng(4)
+    n = 300
+    s_true = rng.uniform(0.5, 2.0, n)
+    y = (rng.normal(0.0, 1.0, n) * s_true + 0.3).astype(np.float32)
+
+    def lp(p):
+        return (ns.Normal(0.0, 5.0).log_prob(p["mu"])
+                + ns.sum(ns.HalfNormal(2.0).log_prob(p["s"]))
+                + ns.sum(ns.Normal(p["mu"], p["s"]).log_prob(ns.array(y))))
+
+    return lp, {"mu": 0.0, "s": np.ones(n, np.float32)}
+
+
+def model_value_pp(ns):
+    """Per-element value parameter against data loc, and a HalfNormal on data."""
+    rng = np.random.default_rng(5)
+    n = 500
+    m0 = rng.normal(0.0, 1.0, n).astype(np.float32)
+    z = np.abs(rng.normal(0.0, 1.5, 200)).astype(np.float32)
+
+    def lp(p):
+        return (ns.sum(ns.Normal(ns.array(m0), p["tau"]).log_prob(p["theta"]))
+                + ns.HalfNormal(1.0).log_prob(p["tau"])
+                + ns.sum(ns.HalfNormal(p["tau"]).log_prob(ns.array(z))))
+
+    return lp, {"theta": np.zeros(n, np.float32), "tau": 1.0}
+
+
+def model_hier_small(ns):
+    G, N = W.SHAPES["small"]
+    return W.hierarchical(ns, G, N)
+
+
+MODELS = {"iid": model_iid, "scale_vec": model_scale_vec, "value_pp": model_value_pp,
+          "hier_small": model_hier_small}
+
+
+def _run(lp, init, slices, C=8, warm=10, samp=10, L=8, eps=0.02, seed=3, chain_offset=0):
+    m = _m()
+    s, rate, info = m.hmc(lp, init, num_samples=samp, num_warmup=warm, step_size=eps,
+                          num_leapfrog_steps=L, key=m.random.key(seed), num_chains=C,
+                          chain_offset=chain_offset, progress=False, return_info=True,
+                          return_trace=True, num_slices=slices)
+    return s, info
+
+
+# ----------------------------------------------------------------- tests --
+def test_auto_slicing_large_and_small(gpu):
+    from mlx_mcmc_amd import _trace
+
+    G, N = W.SHAPES["large"]
+    big = _trace.compile_model(*W.hierarchical(W.ns_product(), G, N))
+    assert big.num_slices == 16
+    small = _trace.compile_model(*W.simple_normal(W.ns_product()))
+    assert small.num_slices == 1
+
+
+def test_unsliceable_program_is_rejected(gpu):
+    from mlx_mcmc_amd import _lib, _trace
+
+    def lp(p):
+        ns = W.ns_product()
+        return ns.sum(ns.Normal(0.0, p["s"]).log_prob(p["x"]))   # two per-element params
+
+    prog = _trace.compile_model(lp, {"x": np.zeros(10, np.float32),
+                                     "s": np.ones(10, np.float32)})
+    with pytest.raises(_lib.EngineError):
+        prog.set_slices(2)
+    assert prog.num_slices == 1
+
+
+@pytest.mark.parametrize("name", sorted(MODELS))
+@pytest.mark.parametrize("S", [2, 3])
+def test_sliced_matches_unsliced(gpu, name, S):
+    lp, init = MODELS[name](W.ns_product())
+    a, ia = _run(lp, init, 1)
+    b, ib = _run(lp, init, S)
+    np.testing.assert_array_equal(ia.trace["accepted"], ib.trace["accepted"])
+    np.testing.assert_array_equal(ia.trace["step_size"], ib.trace["step_size"])
+    for k in a:
+        np.testing.assert_allclose(b[k], a[k], rtol=1e-3, atol=1e-4)
+    np.testing.assert_allclose(ib.trace["energy"], ia.trace["energy"], rtol=1e-4, atol=1e-3)
+
+
+def test_sliced_determinism_chain_split_and_block_size(gpu):
+    lp, init = model_hier_small(W.ns_product())
+    full, _ = _run(lp, init, 4, C=24)          # 16-chain blocks
+    again, _ = _run(lp, init, 4, C=24)
+    for k in full:
+        np.testing.assert_array_equal(full[k], again[k])
+    part, _ = _run(lp, init, 4, C=4, chain_offset=10)   # 8-chain block, 4 used
+    for k in full:
+        np.testing.assert_array_equal(full[k][10:14], part[k])
+
+
+def test_sliced_golden_hmc_trace(gpu):
+    m = _m()
+    with open(os.path.join(os.path.dirname(__file__), "golden", "hmc_simple.json")) as f:
+        h = json.load(f)
+    lp, init = W.simple_normal(W.ns_product())
+    _, _, info = m.hmc(lp, init, num_samples=h["num_samples"], num_warmup=h["num_warmup"],
+                       step_size=h["step_size"], num_leapfrog_steps=h["num_leapfrog_steps"],
+                       key=m.random.key(h["seed"]), progress=False, return_info=True,
+                       return_trace=True, num_slices=2)
+    acc = info.trace["accepted"][0].astype(bool).tolist()
+    same = next((i for i, (x, y) in enumerate(zip(acc, h["accepted"])) if x != y), len(acc))
+    assert same >= 50
+    np.testing.assert_array_equal(info.trace["step_size"][0][:same], h["eps"][:same])
+
+
+def test_sliced_large_matches_unsliced(gpu):
+    """bench.py's workload: decisions and energies agree with k_hmc."""
+    G, N = W.SHAPES["large"]
+    lp, init = W.hierarchical(W.ns_product(), G, N)
+    a, ia = _run(lp, init, 1, C=16, warm=5, samp=5, L=20, eps=0.01)
+    b, ib = _run(lp, init, 0, C=16, warm=5, samp=5, L=20, eps=0.01)
+    np.testing.assert_array_equal(ia.trace["accepted"], ib.trace["accepted"])
+    np.testing.assert_allclose(ib.trace["energy"], ia.trace["energy"], rtol=1e-5)
+    for k in a:
+        np.testing.assert_allclose(b[k], a[k], rtol=1e-3, atol=1e-4)
+
+
+def test_sliced_posterior(gpu):
+    """Reference-style statistical check through the sliced path
+    (tests/test_hmc.py:13-40 posterior of the simple normal model)."""
+    m = _m()
+    lp, init = W.simple_normal(W.ns_product())
+    s, rate = m.hmc(lp, init, num_samples=1000, num_warmup=500, step_size=0.1,
+                    num_leapfrog_steps=10, key=m.random.key(0), num_chains=16, progress=False,
+                    num_slices=2)
+    assert abs(float(np.mean(s["mu"])) - 5.0) < 0.6
+    assert 1.4 < float(np.mean(s["sigma"])) < 2.6
+    assert 0.3 < float(np.mean(rate)) <= 1.0
