@@ -674,8 +674,11 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
     int rc = plan_slices(p, S, P);
     if (rc == MC_OK) {
         p->sl = P;  // host tables; geometry below needs them in place
-        p->sl.nb_max = sl_lds_bytes(p, 16) <= kSlLdsBudget ? 16
-                     : (sl_lds_bytes(p, 8) <= kSlLdsBudget ? 8 : 0);
+        auto fit = [&]() {
+            return sl_lds_bytes(p, 16) <= kSlLdsBudget ? 16
+                 : (sl_lds_bytes(p, 8) <= kSlLdsBudget ? 8 : 0);
+        };
+        p->sl.nb_max = fit();
         if (p->sl.nb_max == 0)
             rc = fail(MC_ERR_UNSUPPORTED, "slice state (%d bytes) exceeds the LDS budget",
                       sl_lds_bytes(p, 8));
@@ -1457,7 +1460,13 @@ extern "C" int mc_debug_stamps(unsigned long long* acc, unsigned long long* cnt,
         unsigned long long z[16 * 32] = {0};
         MC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mc_stamp_acc), z, sizeof(z)));
         MC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mc_stamp_cnt), z, sizeof(z)));
+        std::vector<unsigned long long> zw(1024 * 4, 0);
+        MC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mc_stamp_wg), zw.data(), zw.size() * 8));
     }
+    return MC_OK;
+}
+extern "C" int mc_debug_stamps_wg(unsigned long long* wg) {
+    MC_HIP_TRY(hipMemcpyFromSymbol(wg, HIP_SYMBOL(mc_stamp_wg), 1024 * 4 * 8));
     return MC_OK;
 }
 #endif

@@ -38,6 +38,7 @@ enum : int32_t { SK_NONE = 0, SK_CONST = 1, SK_SHARED = 2, SK_DATA = 3, SK_PP = 
 constexpr int kSlLanes = 64;  // run slots per chain pair (one wave serves two chains)
 constexpr int kSlItr = 8;     // run iterations per combine round
 constexpr int kSlVc = kSlLanes * kSlItr;  // staged run cotangents per chain and round
+constexpr int kSlShReg = 4;   // shared parameters whose cotangents stay in registers
 
 // One term restricted to one slice.  Its elements are grouped into runs of
 // equal per-element parameter ("pp", the PVEC/GATHER operand) — or plain
@@ -101,7 +102,8 @@ struct SlLayout {
         pm = o;    o += NB * P.Lp;
         vpart = o; o += P.combine ? NB * kSlVc : 0;
         sacc = o;  o += NB * (P.Dsh + 1);
-        xin = o;   o += P.S > 16 ? P.S * P.nitems * NB : 0;
+        xin = o;   o += (P.S > 16 || P.nitems * NB * 16 > 4 * (kSlLanes * NB / 2))
+                             ? P.S * P.nitems * NB : 0;
         ob = o;    o += P.nitems * NB;
         o = (o + 3) / 4 * 4;
         der = o;   o += 4 * NB * (P.Dsh > 0 ? P.Dsh : 1);
@@ -254,7 +256,7 @@ MC_DEV void sl_scalar_stage(const SlCtx& P, const float* q2, uint32_t pmask, flo
 template <int NB>
 MC_DEV void sl_term(const SlCtx& P, const SlTerm& T, const float* sd, const float* q2, float* g2,
                     uint32_t pmask, int b0, int j, float* vpart, float* sacc, const float4* der,
-                    int tid, float (&lp)[2]) {
+                    int tid, float (&lp)[2], float (&acc)[kSlShReg][2]) {
     constexpr int NT = kSlLanes * NB / 2;
     const int Lp = P.Lp;
     int qb[2];
@@ -309,17 +311,19 @@ MC_DEV void sl_term(const SlCtx& P, const SlTerm& T, const float* sd, const floa
                     float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, cnt[2];
                     bool neg[2] = {false, false};
                     if (T.dist == MC_DIST_NORMAL) {
-                        float vv[2], mm[2];
+                        {
+                            float vv[2], mm[2];
 #pragma unroll
-                        for (int c = 0; c < 2; ++c) {
-                            vv[c] = (k0 == SK_PP) ? th[c] : uv[c];
-                            mm[c] = (k1 == SK_PP) ? th[c] : um[c];
+                            for (int c = 0; c < 2; ++c) {
+                                vv[c] = (k0 == SK_PP) ? th[c] : uv[c];
+                                mm[c] = (k1 == SK_PP) ? th[c] : um[c];
+                            }
+                            const int dc = (k0 == SK_DATA ? 1 : 0) | (k1 == SK_DATA ? 2 : 0);
+                            if (dc == 1) run_moments2<1>(x0, x1, len, lmin4, vv, mm, s1, s2);
+                            else if (dc == 0) run_moments2<0>(x0, x1, len, lmin4, vv, mm, s1, s2);
+                            else if (dc == 2) run_moments2<2>(x0, x1, len, lmin4, vv, mm, s1, s2);
+                            else run_moments2<3>(x0, x1, len, lmin4, vv, mm, s1, s2);
                         }
-                        const int dc = (k0 == SK_DATA ? 1 : 0) | (k1 == SK_DATA ? 2 : 0);
-                        if (dc == 1) run_moments2<1>(x0, x1, len, lmin4, vv, mm, s1, s2);
-                        else if (dc == 0) run_moments2<0>(x0, x1, len, lmin4, vv, mm, s1, s2);
-                        else if (dc == 2) run_moments2<2>(x0, x1, len, lmin4, vv, mm, s1, s2);
-                        else run_moments2<3>(x0, x1, len, lmin4, vv, mm, s1, s2);
                         cnt[0] = cnt[1] = (float)len;
                         MC_STAMP(14);
                     } else {
@@ -408,21 +412,35 @@ MC_DEV void sl_term(const SlCtx& P, const SlTerm& T, const float* sd, const floa
         }
     }
     MC_STAMP(15);
-    // broadcast-operand cotangents: wave totals, one writer per chain
+    if (P.Dsh <= kSlShReg) {
+        // broadcast-operand cotangents stay per lane until the end of the
+        // evaluation (one reduction per shared parameter, not per term)
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        float* row = sacc + (b0 + c) * (P.Dsh + 1);
-        if (k0 == SK_SHARED) {
-            const float x = wave_sum(pv[c]);
-            if (j == 0) row[T.jsh[0]] += x;
+        for (int q = 0; q < kSlShReg; ++q) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (k0 == SK_SHARED && T.jsh[0] == q) acc[q][c] += pv[c];
+                if (k1 == SK_SHARED && T.jsh[1] == q) acc[q][c] += pm[c];
+                if (k2 == SK_SHARED && T.jsh[2] == q) acc[q][c] += ps[c];
+            }
         }
-        if (k1 == SK_SHARED) {
-            const float x = wave_sum(pm[c]);
-            if (j == 0) row[T.jsh[1]] += x;
-        }
-        if (k2 == SK_SHARED) {
-            const float x = wave_sum(ps[c]);
-            if (j == 0) row[T.jsh[2]] += x;
+    } else {
+        // wave totals per term, one writer per chain
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            float* row = sacc + (b0 + c) * (P.Dsh + 1);
+            if (k0 == SK_SHARED) {
+                const float x = wave_sum(pv[c]);
+                if (j == 0) row[T.jsh[0]] += x;
+            }
+            if (k1 == SK_SHARED) {
+                const float x = wave_sum(pm[c]);
+                if (j == 0) row[T.jsh[1]] += x;
+            }
+            if (k2 == SK_SHARED) {
+                const float x = wave_sum(ps[c]);
+                if (j == 0) row[T.jsh[2]] += x;
+            }
         }
     }
     MC_STAMP(16);
@@ -451,19 +469,34 @@ MC_DEV void sl_eval(const SlCtx& P, int slice, const float* sd, const float* q2,
     }
     __syncthreads();
     float lp[2] = {0.0f, 0.0f};
+    float acc[kSlShReg][2];
+#pragma unroll
+    for (int q = 0; q < kSlShReg; ++q) acc[q][0] = acc[q][1] = 0.0f;
     for (int t = 0; t < P.n_terms; ++t) {
         if (tt[t].niter == 0) continue;
         const SlTerm T = load_slterm(tt + t);
         // no barrier between terms: a parameter's direct runs are on the same
         // lane in every term (the planner's lane map), split runs are combined
         // between barriers of their own
-        sl_term<NB>(P, T, sd, q2, g2, pmask, b0, j, vpart, sacc, der, tid, lp);
+        sl_term<NB>(P, T, sd, q2, g2, pmask, b0, j, vpart, sacc, der, tid, lp, acc);
         MC_STAMP(4 + (t < 7 ? t : 7));
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         const float x = wave_sum(lp[c]);
         if (j == 0) ob[b0 + c] = x;  // record item 0: log p partial
+    }
+    if (P.Dsh <= kSlShReg) {
+#pragma unroll
+        for (int q = 0; q < kSlShReg; ++q) {
+            if (q < P.Dsh) {
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const float x = wave_sum(acc[q][c]);
+                    if (j == 0) sacc[(b0 + c) * Dc + q] = x;
+                }
+            }
+        }
     }
     // scalar terms need only this step's shared values: evaluate them in the
     // slack before the barrier (the exchange adds them to the totals)
@@ -496,36 +529,63 @@ MC_DEV unsigned long long granule_load(unsigned long long* p) {
 
 constexpr uint32_t kSpinLimit = 1u << 23;  // ~seconds: then status = 1, exit
 
-// Publish this slice's record for every chain (the outbox ob[item][b]), wait
-// for all S records of the block and sum them.  Items: 0 log p, 1..Dsh shared
+// Publish this slice's record for every chain (the outbox ob[item][b]);
+// collect: wait for all S records of the block and sum them.  Items: 0 log p, 1..Dsh shared
 // cotangents, Dsh+1 K0 partial, Dsh+2 K1 partial.  With S <= 16 thread x
 // polls the granule of (item x/16, slice x%16) and a 16-lane DPP row sums the
 // item straight from registers (a fixed tree, identical in every slice);
 // otherwise the records go through LDS and are summed in slice order.  The
 // scalar terms' staged rows are added in term order.  Returns false on timeout.
 template <int NB>
-MC_DEV bool sl_exchange(const SlCtx& P, int slice, unsigned long long* xg, uint32_t tag,
-                        float* g2, uint32_t pmask, const float* ob, float* xin,
-                        const float* sst, float* cs, int* flags, int* status, int tid) {
+MC_DEV void sl_publish(const SlCtx& P, int slice, unsigned long long* xg, uint32_t tag,
+                       const float* ob, int tid) {
+    constexpr int NT = kSlLanes * NB / 2;
+    const int n_items = P.nitems * NB;
+    for (int idx = tid; idx < n_items; idx += NT)
+        granule_store(xg + (int64_t)slice * n_items + idx, tag, ob[idx]);
+}
+
+constexpr int kMaxPass = 4;  // granules per thread on the fast (register) path
+
+// Polled granules of one exchange, held in registers between issue and
+// completion so that the memory round trip overlaps other work.
+struct SlPoll {
+    unsigned long long y[kMaxPass];
+};
+
+template <int NB>
+MC_DEV bool sl_fast_path(const SlCtx& P) {
+    constexpr int NT = kSlLanes * NB / 2;
+    return P.S <= 16 && (P.nitems * NB * 16 + NT - 1) / NT <= kMaxPass;
+}
+
+// Issue this thread's granule loads of the exchange (no wait).
+template <int NB>
+MC_DEV void sl_poll_issue(const SlCtx& P, unsigned long long* xg, SlPoll& R, int tid) {
+    constexpr int NT = kSlLanes * NB / 2;
+    if (!sl_fast_path<NB>(P)) return;
+    const int n_items = P.nitems * NB;
+    const int npass = (n_items * 16 + NT - 1) / NT;
+#pragma unroll
+    for (int p = 0; p < kMaxPass; ++p) {
+        const int x = p * NT + tid, idx = x >> 4, sl = x & 15;
+        R.y[p] = 0;
+        if (p < npass && idx < n_items && sl < P.S) R.y[p] = granule_load(xg + sl * n_items + idx);
+    }
+}
+
+// Complete the exchange: re-poll the granules whose tags were stale, sum
+// every item over the slices (a 16-lane DPP row per item: a fixed tree,
+// identical in every slice; or in slice order through LDS when S > 16) and
+// add the scalar terms' staged rows in term order.  Returns false on timeout.
+template <int NB>
+MC_DEV bool sl_collect(const SlCtx& P, unsigned long long* xg, uint32_t tag, float* g2,
+                       uint32_t pmask, float* xin, const float* sst, float* cs, int* flags,
+                       int* status, SlPoll& R, int tid) {
     constexpr int NT = kSlLanes * NB / 2;
     const int nI = P.nitems, Dsh = P.Dsh, Lp = P.Lp;
     const int n_items = nI * NB;
     MC_STAMP_DECL
-    for (int idx = tid; idx < n_items; idx += NT)
-        granule_store(xg + (int64_t)slice * n_items + idx, tag, ob[idx]);
-    MC_STAMP(17);
-    auto poll = [&](int g, float& v) -> bool {
-        uint32_t spins = 0;
-        for (;;) {
-            const unsigned long long x = granule_load(xg + g);
-            if ((uint32_t)(x >> 32) == tag) {
-                v = __uint_as_float((uint32_t)x);
-                return true;
-            }
-            if (++spins > kSpinLimit) return false;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    };
     auto finish_item = [&](int idx, float s) {
         const int i = idx / NB, b = idx - i * NB;
         if (i <= Dsh)
@@ -536,20 +596,69 @@ MC_DEV bool sl_exchange(const SlCtx& P, int slice, unsigned long long* xg, uint3
         else cs[CS_K1 * NB + b] = s;
     };
     bool ok = true;
-    if (P.S <= 16) {
-        for (int base = 0; base < n_items * 16; base += NT) {
-            const int x = base + tid;
-            const int idx = x >> 4, sl = x & 15;
-            float v = 0.0f;
-            if (idx < n_items && sl < P.S && ok) ok = poll(sl * n_items + idx, v);
-            v += dpp_row<0xB1>(v);
-            v += dpp_row<0x4E>(v);
-            v += dpp_row<0x141>(v);
-            v += dpp_row<0x140>(v);
-            if (idx < n_items && sl == 0) finish_item(idx, v);
+    const bool fast = sl_fast_path<NB>(P);
+    if (fast) {
+        const int npass = (n_items * 16 + NT - 1) / NT;
+        float v[kMaxPass];
+        uint32_t need = 0;
+#pragma unroll
+        for (int p = 0; p < kMaxPass; ++p) {
+            v[p] = 0.0f;
+            const int x = p * NT + tid, idx = x >> 4, sl = x & 15;
+            if (p < npass && idx < n_items && sl < P.S) {
+                if ((uint32_t)(R.y[p] >> 32) == tag) v[p] = __uint_as_float((uint32_t)R.y[p]);
+                else need |= 1u << p;
+            }
+        }
+        uint32_t spins = 0;
+        while (need) {
+            if (++spins > kSpinLimit) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            unsigned long long y[kMaxPass];
+#pragma unroll
+            for (int p = 0; p < kMaxPass; ++p) {
+                const int x = p * NT + tid, idx = x >> 4, sl = x & 15;
+                if ((need >> p) & 1u) y[p] = granule_load(xg + sl * n_items + idx);
+            }
+#pragma unroll
+            for (int p = 0; p < kMaxPass; ++p) {
+                if (((need >> p) & 1u) && (uint32_t)(y[p] >> 32) == tag) {
+                    v[p] = __uint_as_float((uint32_t)y[p]);
+                    need &= ~(1u << p);
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < kMaxPass; ++p) {
+            if (p < npass) {
+                const int x = p * NT + tid, idx = x >> 4, sl = x & 15;
+                float t = v[p];
+                t += dpp_row<0xB1>(t);
+                t += dpp_row<0x4E>(t);
+                t += dpp_row<0x141>(t);
+                t += dpp_row<0x140>(t);
+                if (idx < n_items && sl == 0) finish_item(idx, t);
+            }
         }
     } else {
-        for (int g = tid; g < P.S * n_items && ok; g += NT) ok = poll(g, xin[g]);
+        for (int g = tid; g < P.S * n_items && ok; g += NT) {
+            uint32_t spins = 0;
+            for (;;) {
+                const unsigned long long x = granule_load(xg + g);
+                if ((uint32_t)(x >> 32) == tag) {
+                    xin[g] = __uint_as_float((uint32_t)x);
+                    break;
+                }
+                if (++spins > kSpinLimit) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
     }
     if (!ok) {
         flags[1] = 1;
@@ -558,7 +667,7 @@ MC_DEV bool sl_exchange(const SlCtx& P, int slice, unsigned long long* xg, uint3
     __syncthreads();
     MC_STAMP(19);
     if (flags[1]) return false;
-    if (P.S > 16) {
+    if (!fast) {
         for (int idx = tid; idx < n_items; idx += NT) {
             float v = xin[idx];
             for (int sl = 1; sl < P.S; ++sl) v += xin[sl * n_items + idx];
@@ -724,32 +833,46 @@ k_hmc_sl(SlCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         __syncthreads();
 
         const uint32_t prop = ~cur;  // proposal buffer of every chain
-        if (L == 0) {
-            ++epoch;
-            if (tid < NB) ob[tid] = 0.0f;
-            __syncthreads();
-            unsigned long long* xg = xch + ((int64_t)(epoch & 1) * n_groups + grp) * S * nI * NB;
-            if (!sl_exchange<NB>(P, slice, xg, epoch, g2, prop, ob, xin, sst, cs, flags, status, tid))
-                return;
-        }
-        MC_STAMP_DECL
-        for (int l = 0; l < L; ++l) {
-            // step 0 starts from the current point, later steps update the
-            // proposal in place (each slot is read and written by one thread)
+        SlPoll poll;
+        auto xbuf = [&](uint32_t ep) {
+            return xch + ((int64_t)(ep & 1) * n_groups + grp) * S * nI * NB;
+        };
+        // position update of slots [k_lo, k_hi) of every chain: step 0 starts
+        // from the current point, later steps update the proposal in place
+        // (each slot is read and written by one thread)
+        auto advance = [&](int l, int k_lo, int k_hi) {
             const uint32_t from = (l == 0) ? cur : prop;
-            for (int idx = tid; idx < NB * Lp; idx += NT) {
-                const int b = idx / Lp, k = idx - b * Lp;
+            const int w = k_hi - k_lo;
+            for (int idx = tid; idx < NB * w; idx += NT) {
+                const int b = idx / w, k = k_lo + (idx - b * w);
                 const int src = slot_of(from, b, NB, Lp) + k;
                 const int dst = slot_of(prop, b, NB, Lp) + k;
                 const float h = cs[CS_H * NB + b], e = cs[CS_E * NB + b];
                 const float gj = g2[src];
-                float pj = pm[idx];
+                float pj = pm[b * Lp + k];
                 if (l > 0) pj = pj + h * gj;  // second half kick of step l-1
                 pj = pj + h * gj;             // first half kick of step l
-                pm[idx] = pj;
+                pm[b * Lp + k] = pj;
                 q2[dst] = q2[src] + e * pj;
                 g2[dst] = 0.0f;
             }
+        };
+        if (L == 0) {
+            ++epoch;
+            if (tid < NB) ob[tid] = 0.0f;
+            __syncthreads();
+            sl_publish<NB>(P, slice, xbuf(epoch), epoch, ob, tid);
+            sl_poll_issue<NB>(P, xbuf(epoch), poll, tid);
+            if (!sl_collect<NB>(P, xbuf(epoch), epoch, g2, prop, xin, sst, cs, flags, status,
+                                poll, tid))
+                return;
+        }
+        MC_STAMP_DECL
+        for (int l = 0; l < L; ++l) {
+            // private slots of step l > 0 were advanced while the previous
+            // exchange was in flight (their gradients were complete)
+            if (l == 0) advance(0, 0, Lp);
+            else advance(l, P.Pmax, P.Pmax + P.Dsh);
             __syncthreads();
             MC_STAMP(0);
             sl_eval<NB>(P, slice, sd, q2, g2, prop, vpart, sacc, der, sst, ob, tid);
@@ -759,8 +882,11 @@ k_hmc_sl(SlCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 __syncthreads();
             }
             ++epoch;
-            unsigned long long* xg = xch + ((int64_t)(epoch & 1) * n_groups + grp) * S * nI * NB;
-            if (!sl_exchange<NB>(P, slice, xg, epoch, g2, prop, ob, xin, sst, cs, flags, status, tid))
+            sl_publish<NB>(P, slice, xbuf(epoch), epoch, ob, tid);
+            if (l + 1 < L) advance(l + 1, 0, P.Pmax);  // overlaps the records' flight
+            sl_poll_issue<NB>(P, xbuf(epoch), poll, tid);
+            if (!sl_collect<NB>(P, xbuf(epoch), epoch, g2, prop, xin, sst, cs, flags, status,
+                                poll, tid))
                 return;
             MC_STAMP(2);
         }

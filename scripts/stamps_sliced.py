@@ -71,6 +71,14 @@ SECS += [(4 + t, f" term {t}") for t in range(5)] + [
     (11, " final sync"), (12, "  term setup"), (13, "  run tables+theta"), (14, "  moments"),
     (15, "  finish+rest of runs"), (16, "  deposits"), (17, " x publish"), (18, " x scalar stage"),
     (19, " x poll"), (20, " x barrier"), (21, " x totals+scalar")]
+wg = (ctypes.c_ulonglong * (1024 * 4))()
+lib.mc_debug_stamps_wg.argtypes = [ctypes.c_void_p]
+lib.mc_debug_stamps_wg(wg)
+wga = np.array(wg[:], dtype=np.float64).reshape(1024, 4)[: 16 * ((C + 15) // 16)] / steps
+for sec, name in ((0, "pos(+hoist)"), (1, "eval"), (2, "collect")):
+    v = wga[:, sec]
+    print(f"  per-WG {name:12s} min {v.min():7.0f} median {np.median(v):7.0f} max {v.max():7.0f}"
+          f"  argmax WG {int(v.argmax())}")
 for sec, name in SECS:
     vals = " ".join(f"{a[w, sec] / steps:7.0f}" for w in range(8))
     print(f"  {name:18s} {vals}")
