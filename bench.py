@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-oracle baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=15,
+                    help="processes of the aggregate CPU baseline (0: skip)")
     ap.add_argument("--no-ess", action="store_true")
     return ap.parse_args()
 
@@ -78,7 +80,7 @@ def ess_device(samples, max_lag=100):
     return torch.where(var == 0, torch.full_like(ess, float(n)), ess)   # [C, D]
 
 
-def cpu_baseline(G, N, L, step_size, budget_s):
+def cpu_baseline(G, N, L, step_size, budget_s, chain=0):
     """Time the CPU oracle (reference cost structure) on the same model, 1 chain, 1 thread."""
     import torch
 
@@ -95,14 +97,14 @@ def cpu_baseline(G, N, L, step_size, budget_s):
     t0 = time.perf_counter()
     # one HMC iteration = momentum, L two-gradient leapfrog steps, accept
     while time.perf_counter() - t0 < budget_s:
-        p = R.momentum(0, 0, iters, M.D)
+        p = R.momentum(0, chain, iters, M.D)
         H0 = M.hamiltonian(q, p)
         qp, pp = q, p
         for _ in range(L):
             qp, pp = M.leapfrog(qp, pp, step_size)
             steps += 1
         H1 = M.hamiltonian(qp, pp)
-        if R.logf_ref(R.uniform(0, 0, iters, R.TAG_ACCEPT)) < -(H1 - H0):
+        if R.logf_ref(R.uniform(0, chain, iters, R.TAG_ACCEPT)) < -(H1 - H0):
             q = qp
         iters += 1
     dt = time.perf_counter() - t0
@@ -110,6 +112,41 @@ def cpu_baseline(G, N, L, step_size, budget_s):
             "sample": (f"oracle/samplers.py HMC restatement (2 gradients per leapfrog step, "
                        f"torch-CPU autograd), 1 chain, 1 thread, {iters} iterations x L={L} "
                        f"on the same D={G + 3}, N={N} model, {dt:.1f} s")}
+
+
+def _cpu_worker(a):
+    """One process of the aggregate CPU baseline (spawned: no GPU state)."""
+    G, N, L, step_size, budget_s, seed = a
+    import torch
+
+    torch.set_num_threads(1)
+    r = cpu_baseline(G, N, L, step_size, budget_s, chain=seed)
+    return r["value"]
+
+
+def cpu_aggregate(G, N, L, step_size, budget_s, nproc):
+    """nproc independent single-thread oracle processes, one
+    chain each; aggregate chain-steps/s."""
+    import multiprocessing as mp
+
+    # the workers are CPU-only: hide the GPU from them (spawned children copy
+    # the environment when the pool starts)
+    hide = ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES")
+    saved = {k: os.environ.get(k) for k in hide}
+    for k in hide:
+        os.environ[k] = ""
+    try:
+        ctx = mp.get_context("spawn")
+        pool = ctx.Pool(nproc)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    with pool:
+        vals = pool.map(_cpu_worker, [(G, N, L, step_size, budget_s, i) for i in range(nproc)])
+    return float(sum(vals))
 
 
 def main():
@@ -225,10 +262,16 @@ def main():
                            if prog.num_slices > 1 else f"k_hmc<{prog.waves_per_chain}>"),
                 "kernel_ms": kern_ms,
                 "flops_per_launch": flops_per_launch,
-                "note": ("fp32 compute bound (vector FP32 peak = f32-MFMA peak 157.3 TF); "
-                         "F = 5N + 13D flops per chain-leapfrog-step, C*L per launch"),
+                "note": ("fp32 VALU bound (SURVEY 8d; vector FP32 peak = f32-MFMA peak 157.3 TF); "
+                         "F = 5N + 13D flops per chain-leapfrog-step, C*L per launch; kernel_ms = "
+                         "HIP events around each launch (the sampler kernel and, when sliced, "
+                         "its exchange-buffer memset); traffic = (2*FETCH_SIZE + WRITE_SIZE) per "
+                         "launch from profiles/pmc_traffic.json"),
             },
             "accept_rate": accept, "step_size": eps,
+            # the data every chain reads per step (8N bytes: y and the
+            # group index), times chain-steps/s; chains share it through LDS/L2
+            "per_chain_streamed_gbs": 8.0 * N * value / 1e9,
         }
         if gather_ms is not None:
             out["gather_ms"] = gather_ms
@@ -241,6 +284,13 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(G, N, L, max(eps, 1e-4), args.cpu_seconds)
             out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+            if args.cpu_procs > 0:
+                agg = cpu_aggregate(G, N, L, max(eps, 1e-4), args.cpu_seconds / 2, args.cpu_procs)
+                out["cpu_baseline"]["aggregate"] = {
+                    "value": agg, "processes": args.cpu_procs, "unit": "leapfrog-steps/s",
+                    "gpu_over_cpu": value / agg,
+                    "sample": f"{args.cpu_procs} spawned single-thread oracle processes, one "
+                              f"chain each, {args.cpu_seconds / 2:.1f} s each (SURVEY 8d (ii))"}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -348,7 +348,7 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P) {
     for (int s = 0; s < S; ++s)
         for (int j = 0; j < P.Dsh; ++j) P.gidx[(size_t)s * P.Lp + P.Pmax + j] = shl[j];
     P.terms.assign((size_t)S * nT, SlTerm());
-    P.blocks.assign(3 * (size_t)S, 0);
+    P.blocks.assign(4 * (size_t)S, 0);
     P.sdata_floats = 0;
 
     // operand kinds of a slice term (SK_*)
@@ -537,7 +537,9 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P) {
                 }
             }
         }
-        // ---- per-term tables and tiled data, in program order ----
+        // ---- per-term tables and tiled data, in program order; the slice's
+        // active terms are stored first, compacted ----
+        int nact = 0;
         for (int t = 0; t < nT; ++t) {
             const DevTerm& rt = raw[t];
             const std::vector<int64_t>& E = elems[s][t];
@@ -633,13 +635,14 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P) {
             st.comb_off = put(ents, false);
             st.pos_off = put(plist, false);
             if (st.pp >= 0 && !st.direct && st.niter > 0) P.combine = 1;
-            P.terms[(size_t)s * nT + t] = st;
+            if (st.niter > 0) P.terms[(size_t)s * nT + nact++] = st;
         }
         while (P.data.size() % 4) P.data.push_back(0.0f);
         const int64_t blen = (int64_t)P.data.size() - blk0;
-        P.blocks[3 * s] = blk0;
-        P.blocks[3 * s + 1] = blen;
-        P.blocks[3 * s + 2] = (int64_t)priv[s].size();
+        P.blocks[4 * s] = blk0;
+        P.blocks[4 * s + 1] = blen;
+        P.blocks[4 * s + 2] = (int64_t)priv[s].size();
+        P.blocks[4 * s + 3] = nact;
         if (blen > INT32_MAX / 8) return fail(MC_ERR_UNSUPPORTED, "slice data too large");
         P.sdata_floats = std::max<int>(P.sdata_floats, (int)blen);
     }

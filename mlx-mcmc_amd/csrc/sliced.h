@@ -73,7 +73,7 @@ struct SlCtx {
     const SlTerm* terms;    // [S][n_terms]
     const float* data;      // slice blocks
     const int32_t* index;   // (unused: the tables are in the blocks)
-    const int64_t* blocks;  // per slice {data offset, data floats, private count}
+    const int64_t* blocks;  // per slice {data offset, data floats, private count, active terms}
     const int32_t* gidx;    // [S][Lp] global parameter of each local slot, -1: padding
     int32_t n_terms;
     int32_t S;
@@ -257,6 +257,7 @@ template <int NB>
 MC_DEV void sl_term(const SlCtx& P, const SlTerm& T, const float* sd, const float* q2, float* g2,
                     uint32_t pmask, int b0, int j, float* vpart, float* sacc, const float4* der,
                     int tid, float (&lp)[2], float (&acc)[kSlShReg][2]) {
+    MC_STAMP_DECL
     constexpr int NT = kSlLanes * NB / 2;
     const int Lp = P.Lp;
     int qb[2];
@@ -289,10 +290,10 @@ MC_DEV void sl_term(const SlCtx& P, const SlTerm& T, const float* sd, const floa
         }
     }
     float pv[2] = {0.f, 0.f}, pm[2] = {0.f, 0.f}, ps[2] = {0.f, 0.f};
-    MC_STAMP_DECL
     MC_STAMP(12);
 
     for (int rd = 0; rd < nrounds; ++rd) {
+        MC_STAMP(23);
         const int it_end = min(T.niter, (rd + 1) * kSlItr);
         for (int it = rd * kSlItr; it < it_end; ++it) {
             const int toff = tiles[3 * it], lmin4 = tiles[3 * it + 2];
@@ -452,8 +453,8 @@ MC_DEV void sl_term(const SlCtx& P, const SlTerm& T, const float* sd, const floa
 // complete on return; shared ones hold this slice's partial; cs[LPP] = the
 // slice's log p partial.
 template <int NB>
-MC_DEV void sl_eval(const SlCtx& P, int slice, const float* sd, const float* q2, float* g2,
-                    uint32_t pmask, float* vpart, float* sacc, float4* der, float* sst,
+MC_DEV void sl_eval(const SlCtx& P, int slice, int nact, const float* sd, const float* q2,
+                    float* g2, uint32_t pmask, float* vpart, float* sacc, float4* der, float* sst,
                     float* ob, int tid) {
     constexpr int NT = kSlLanes * NB / 2;
     const int Lp = P.Lp, Dc = P.Dsh + 1;
@@ -472,9 +473,9 @@ MC_DEV void sl_eval(const SlCtx& P, int slice, const float* sd, const float* q2,
     float acc[kSlShReg][2];
 #pragma unroll
     for (int q = 0; q < kSlShReg; ++q) acc[q][0] = acc[q][1] = 0.0f;
-    for (int t = 0; t < P.n_terms; ++t) {
-        if (tt[t].niter == 0) continue;
+    for (int t = 0; t < nact; ++t) {  // the slice's active terms, compacted
         const SlTerm T = load_slterm(tt + t);
+        MC_STAMP(22);
         // no barrier between terms: a parameter's direct runs are on the same
         // lane in every term (the planner's lane map), split runs are combined
         // between barriers of their own
@@ -749,7 +750,8 @@ k_hmc_sl(SlCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     int* ci = (int*)cs;
     int* flags = (int*)(cs + CS_COUNT * NB);  // [0] current-buffer mask, [1] abort
 
-    const int64_t* blk = P.blocks + 3 * (int64_t)slice;
+    const int64_t* blk = P.blocks + 4 * (int64_t)slice;
+    const int nact = (int)blk[3];
     const int64_t doff = blk[0];
     const int dlen = (int)blk[1];
     const int Ps = (int)blk[2];
@@ -875,7 +877,7 @@ k_hmc_sl(SlCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             else advance(l, P.Pmax, P.Pmax + P.Dsh);
             __syncthreads();
             MC_STAMP(0);
-            sl_eval<NB>(P, slice, sd, q2, g2, prop, vpart, sacc, der, sst, ob, tid);
+            sl_eval<NB>(P, slice, nact, sd, q2, g2, prop, vpart, sacc, der, sst, ob, tid);
             MC_STAMP(1);
             if (l == L - 1) {
                 sl_kinetic<NB>(pm, g2, prop, cs, true, Ps, Lp, ob + (P.Dsh + 2) * NB, tid);

@@ -70,7 +70,8 @@ SECS = [(0, "position update"), (1, "evaluation"), (2, "kinetic+exchange")]
 SECS += [(4 + t, f" term {t}") for t in range(5)] + [
     (11, " final sync"), (12, "  term setup"), (13, "  run tables+theta"), (14, "  moments"),
     (15, "  finish+rest of runs"), (16, "  deposits"), (17, " x publish"), (18, " x scalar stage"),
-    (19, " x poll"), (20, " x barrier"), (21, " x totals+scalar")]
+    (19, " x poll"), (20, " x barrier"), (21, " x totals+scalar"), (22, "  load_slterm"),
+    (23, "  round start")]
 wg = (ctypes.c_ulonglong * (1024 * 4))()
 lib.mc_debug_stamps_wg.argtypes = [ctypes.c_void_p]
 lib.mc_debug_stamps_wg(wg)
