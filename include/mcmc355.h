@@ -16,6 +16,9 @@
  *   mlx_mcmc/kernels/nuts.py:119-135 no_u_turn         (inside mc_nuts_run)
  *   mlx_mcmc/distributions/normal.py:33-56 log_prob    MC_DIST_NORMAL term / mc_dist_log_prob
  *   mlx_mcmc/distributions/halfnormal.py:34-63         MC_DIST_HALFNORMAL term / mc_dist_log_prob
+ *   mlx_mcmc/distributions/exponential.py:48-71        MC_DIST_EXPONENTIAL term / mc_dist_log_prob
+ *   mlx_mcmc/distributions/gamma.py:40-88              MC_DIST_GAMMA term / mc_dist_log_prob
+ *   mlx_mcmc/distributions/beta.py:37-91               MC_DIST_BETA term / mc_dist_log_prob
  *   mlx.core.random (key/split/normal/uniform)         Philox4x32-10 counter RNG, mc_rng_fill
  *
  * The reference is pure Python on MLX and has no FFI of its own; the
@@ -59,9 +62,16 @@ extern "C" {
 /* A term is  weight * sum_i dist(loc_i, scale_i).log_prob(value_i)  over n
  * broadcast elements.  This is exactly the shape every reference model takes
  * (e.g. tests/test_hmc.py:187-198, examples/02_hmc_comparison.py:40-52).   */
+/* Operand slots of a term: value, then (loc | alpha), then (scale | rate |
+ * beta).  The gammaln normalisers of Gamma and Beta are evaluated at the
+ * current shape values but carry no gradient, exactly as the reference's
+ * host-side scipy gammaln (gamma.py:48-59, beta.py:45-57).                   */
 typedef enum {
-    MC_DIST_NORMAL     = 0,   /* normal.py:33-56      (value, loc, scale)   */
-    MC_DIST_HALFNORMAL = 1    /* halfnormal.py:34-63  (value, scale)        */
+    MC_DIST_NORMAL      = 0,  /* normal.py:33-56       (value, loc, scale)   */
+    MC_DIST_HALFNORMAL  = 1,  /* halfnormal.py:34-63   (value, -, scale)     */
+    MC_DIST_EXPONENTIAL = 2,  /* exponential.py:48-71  (value, -, rate)      */
+    MC_DIST_GAMMA       = 3,  /* gamma.py:40-88        (value, alpha, beta)  */
+    MC_DIST_BETA        = 4   /* beta.py:37-91         (value, alpha, beta)  */
 } mc_dist_kind;
 
 typedef enum {
@@ -129,9 +139,11 @@ int mc_logp_grad(const mc_program* prog, int64_t n_points,
                  const float* q_dev, float* logp_dev, float* grad_dev,
                  void* hip_stream);
 
-/* Elementwise Distribution.log_prob (normal.py:33-56, halfnormal.py:34-63):
- * out[i] = log_prob(value[i]; loc[i|0], scale[i|0]).  loc_dev may be NULL
- * for HalfNormal.  *_bcast = 1 means the operand is a single element.      */
+/* Elementwise Distribution.log_prob (normal.py:33-56, halfnormal.py:34-63,
+ * exponential.py:48-71, gamma.py:61-88, beta.py:59-91):
+ * out[i] = log_prob(value[i]; loc|alpha[i|0], scale|rate|beta[i|0]).  The
+ * middle operand may be NULL for HalfNormal and Exponential.  *_bcast = 1
+ * means the operand is a single element.                                    */
 int mc_dist_log_prob(int32_t dist, int64_t n,
                      const float* value_dev, int32_t value_bcast,
                      const float* loc_dev, int32_t loc_bcast,

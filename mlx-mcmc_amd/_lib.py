@@ -35,6 +35,9 @@ MC_ERR_NOMEM = -4
 
 MC_DIST_NORMAL = 0
 MC_DIST_HALFNORMAL = 1
+MC_DIST_EXPONENTIAL = 2
+MC_DIST_GAMMA = 3
+MC_DIST_BETA = 4
 
 MC_OP_NONE = 0
 MC_OP_CONST = 1

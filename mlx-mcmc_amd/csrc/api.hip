@@ -106,6 +106,11 @@ static float c_log_norm() {
     return -0.5f * l;
 }
 static float c_log2() { return (float)std::log(2.0); }
+static float dist_c0(int dist) {
+    if (dist == MC_DIST_NORMAL) return c_log_norm();
+    if (dist == MC_DIST_HALFNORMAL) return c_log2() + c_log_norm();
+    return 0.0f;
+}
 
 static int choose_wpc(int64_t max_n) {
     if (max_n <= 512) return 1;
@@ -381,7 +386,11 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P) {
                 default: st.kind[a] = SK_NONE; break;
             }
         }
-        st.mode = (st.kind[2] == SK_DATA || st.kind[2] == SK_PP) ? 1 : 0;
+        // moment sums for Normal / HalfNormal with a broadcast scale, else
+        // the per-element formula
+        st.mode = (st.kind[2] == SK_DATA || st.kind[2] == SK_PP ||
+                   (rt.dist != MC_DIST_NORMAL && rt.dist != MC_DIST_HALFNORMAL)) ? 1 : 0;
+        st.clg = rt.clg;
         return st;
     };
     // scalar terms (only constants and broadcast parameters): evaluated once
@@ -726,7 +735,7 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
 
     for (int32_t t = 0; t < n_terms; ++t) {
         const mc_term& src = terms[t];
-        if (src.dist != MC_DIST_NORMAL && src.dist != MC_DIST_HALFNORMAL)
+        if (src.dist < MC_DIST_NORMAL || src.dist > MC_DIST_BETA)
             return fail(MC_ERR_INVALID, "term %d: unknown distribution %d", t, src.dist);
         if (src.n < 1) return fail(MC_ERR_INVALID, "term %d: n must be >= 1", t);
         const int64_t n = src.n;
@@ -735,7 +744,7 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
         dt.dist = src.dist;
         dt.n = n;
         dt.weight = src.weight;
-        dt.c0 = (src.dist == MC_DIST_NORMAL) ? c_log_norm() : (c_log2() + c_log_norm());
+        dt.c0 = dist_c0(src.dist);
         const mc_operand* ops[3] = {&src.value, &src.loc, &src.scale};
         for (int a = 0; a < 3; ++a) {
             const mc_operand& o = *ops[a];
@@ -745,10 +754,12 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
             d.pool = o.pool_offset;
             d.cval = o.value;
             d.unique = 1;
-            const bool need = !(a == 1 && src.dist == MC_DIST_HALFNORMAL);
+            const bool need =
+                !(a == 1 && (src.dist == MC_DIST_HALFNORMAL || src.dist == MC_DIST_EXPONENTIAL));
             if (!need) {
                 if (o.kind != MC_OP_NONE && o.kind != MC_OP_CONST)
-                    return fail(MC_ERR_INVALID, "term %d: HalfNormal takes no loc operand", t);
+                    return fail(MC_ERR_INVALID, "term %d: %s takes no loc operand", t,
+                                src.dist == MC_DIST_HALFNORMAL ? "HalfNormal" : "Exponential");
                 d.kind = MC_OP_NONE;
                 continue;
             }
@@ -874,6 +885,11 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
         dt.pass_masks = masks[0] | (masks[1] << 4) | (masks[2] << 8);
         dt.wave_task = -1;
         dt.clogs = (dt.op[2].kind == MC_OP_CONST) ? (float)std::log((double)dt.op[2].cval) : 0.0f;
+        dt.clg = 0.0f;
+        if ((dt.dist == MC_DIST_GAMMA && dt.op[1].kind == MC_OP_CONST) ||
+            (dt.dist == MC_DIST_BETA && dt.op[1].kind == MC_OP_CONST &&
+             dt.op[2].kind == MC_OP_CONST))
+            dt.clg = lgamma_norm(dt.dist, dt.op[1].cval, dt.op[2].cval);
         dt.prim_poff = primary >= 0 ? dt.op[primary].poff : 0;
         if (primary >= 0) {
             const int rc = build_segments(dt, dpool, ipool, 64 * wpc);
@@ -1109,28 +1125,24 @@ __global__ void k_dist(int dist, float c0, int64_t n, const float* v, int vb, co
          i += (int64_t)gridDim.x * blockDim.x) {
         const float vv = v[vb ? 0 : i];
         const float ss = s[sb ? 0 : i];
+        const float mm = m[mb ? 0 : i];
         const float logs = logf(ss);
-        ElemOut e;
-        if (dist == MC_DIST_NORMAL) {
-            const float mm = m[mb ? 0 : i];
-            e = elem_normal(c0, vv, mm, ss, logs);
-        } else {
-            e = elem_halfnormal(c0, vv, ss, logs);
-        }
-        out[i] = e.lp;
+        const float lg = lgamma_norm(dist, mm, ss);
+        out[i] = elem_eval(dist, c0, vv, mm, ss, logs, lg).lp;
     }
 }
 
 extern "C" int mc_dist_log_prob(int32_t dist, int64_t n, const float* v, int32_t vb,
                                 const float* m, int32_t mb, const float* s, int32_t sb,
                                 float* out, void* stream) {
-    if (dist != MC_DIST_NORMAL && dist != MC_DIST_HALFNORMAL)
+    if (dist < MC_DIST_NORMAL || dist > MC_DIST_BETA)
         return fail(MC_ERR_INVALID, "unknown distribution %d", dist);
     if (n < 0) return fail(MC_ERR_INVALID, "n < 0");
     if (n == 0) return MC_OK;
-    if (!v || !s || !out || (dist == MC_DIST_NORMAL && !m))
-        return fail(MC_ERR_INVALID, "NULL operand");
-    const float c0 = (dist == MC_DIST_NORMAL) ? c_log_norm() : (c_log2() + c_log_norm());
+    const bool need_m = dist == MC_DIST_NORMAL || dist == MC_DIST_GAMMA || dist == MC_DIST_BETA;
+    if (!v || !s || !out || (need_m && !m)) return fail(MC_ERR_INVALID, "NULL operand");
+    if (!need_m) mb = 1;  // the unused middle operand is read as element 0 of value
+    const float c0 = dist_c0(dist);
     const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(k_dist, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, dist,
                        c0, n, v, vb, m ? m : v, mb, s, sb, out);

@@ -128,7 +128,7 @@ MC_DEV DevTerm load_term(const MC_CONST DevTerm* p) {
     t.prim_poff = p->prim_poff;
     t.wave_task = p->wave_task;
     t.clogs = p->clogs;
-    t.pad2 = 0.0f;
+    t.clg = p->clg;
     t.op[0] = load_op(&p->op[0]);
     t.op[1] = load_op(&p->op[1]);
     t.op[2] = load_op(&p->op[2]);
@@ -260,6 +260,91 @@ MC_DEV ElemOut elem_halfnormal(float c0, float v, float s, float logs) {
     return o;
 }
 
+// exponential.py:48-71: where(v >= 0, log(rate) - rate * v, -inf); operand
+// slot 2 is the rate.
+MC_DEV ElemOut elem_exponential(float v, float r, float logr) {
+    ElemOut o;
+    if (v >= 0.0f) {
+        o.lp = logr - r * v;
+        o.dv = -r;
+        o.ds = 1.0f / r - v;
+    } else {
+        o.lp = -__builtin_inff();
+        o.dv = 0.0f;
+        o.ds = 0.0f;
+    }
+    o.dm = 0.0f;
+    return o;
+}
+
+// gamma.py:48-59,61-88 (slots: value, alpha, beta):
+//   log_norm = alpha * log(beta) - f32(gammaln(alpha))
+//   where(v > 0, log_norm + (alpha - 1) * log(v) - beta * v, -inf)
+// gammaln is the reference's host scipy value: it carries no gradient.
+MC_DEV ElemOut elem_gamma(float v, float a, float b, float logb, float lga) {
+    ElemOut o;
+    if (v > 0.0f) {
+        const float lv = logf(v);
+        const float lnorm = a * logb - lga;
+        o.lp = (lnorm + (a - 1.0f) * lv) - b * v;
+        o.dv = (a - 1.0f) / v - b;
+        o.dm = logb + lv;
+        o.ds = a / b - v;
+    } else {
+        o.lp = -__builtin_inff();
+        o.dv = o.dm = o.ds = 0.0f;
+    }
+    return o;
+}
+
+// beta.py:45-57,59-91 (slots: value, alpha, beta):
+//   where(0 < v < 1, (alpha-1) log v + (beta-1) log(1-v) - logB(alpha, beta), -inf)
+// logB from host scipy gammaln in the reference: no gradient.
+MC_DEV ElemOut elem_beta(float v, float a, float b, float lbeta) {
+    ElemOut o;
+    if (v > 0.0f && v < 1.0f) {
+        const float lv = logf(v);
+        const float l1v = logf(1.0f - v);
+        o.lp = ((a - 1.0f) * lv + (b - 1.0f) * l1v) - lbeta;
+        o.dv = (a - 1.0f) / v - (b - 1.0f) / (1.0f - v);
+        o.dm = lv;
+        o.ds = l1v;
+    } else {
+        o.lp = -__builtin_inff();
+        o.dv = o.dm = o.ds = 0.0f;
+    }
+    return o;
+}
+
+// Every distribution: logs = f32 log of operand slot 2 (scale / rate / beta;
+// unused by Beta), lg = the gammaln normaliser (Gamma, Beta; see lgamma_norm).
+MC_DEV ElemOut elem_eval(int dist, float c0, float v, float m, float s, float logs, float lg) {
+    switch (dist) {
+        case MC_DIST_NORMAL: return elem_normal(c0, v, m, s, logs);
+        case MC_DIST_HALFNORMAL: return elem_halfnormal(c0, v, s, logs);
+        case MC_DIST_EXPONENTIAL: return elem_exponential(v, s, logs);
+        case MC_DIST_GAMMA: return elem_gamma(v, m, s, logs, lg);
+        default: return elem_beta(v, m, s, lg);
+    }
+}
+
+// The gammaln normaliser as the reference forms it (float64 scipy gammaln of
+// the float32 shapes, rounded once): Gamma lgamma(alpha); Beta
+// lgamma(alpha) + lgamma(beta) - lgamma(alpha + beta).
+__host__ __device__ inline float lgamma_norm(int dist, float a, float b) {
+    if (dist == MC_DIST_GAMMA) return (float)lgamma((double)a);
+    if (dist == MC_DIST_BETA)
+        return (float)(lgamma((double)a) + lgamma((double)b) - lgamma((double)a + (double)b));
+    return 0.0f;
+}
+
+// Does the normaliser vary per element (a vector shape operand)?
+MC_DEV bool lg_per_element(int dist, int k1, int k2) {
+    const bool v1 = k1 == MC_OP_DATA || k1 == MC_OP_PVEC || k1 == MC_OP_GATHER;
+    const bool v2 = k2 == MC_OP_DATA || k2 == MC_OP_PVEC || k2 == MC_OP_GATHER;
+    return (dist == MC_DIST_GAMMA && v1) || (dist == MC_DIST_BETA && (v1 || v2));
+}
+
 MC_DEV bool is_vec(int kind) {
     return kind == MC_OP_DATA || kind == MC_OP_PVEC || kind == MC_OP_GATHER;
 }
@@ -375,17 +460,17 @@ MC_DEV void accum(const DevOperand& o, int64_t i, float c, float& scalar_part, f
 // Generic per-element path (vector scale, injective gathers): full formulas.
 MC_DEV void strided_generic(const DevTerm& T, const DevCtx& P, const float* q, float* g, int tid,
                             int nthr, uint32_t mask, float uv, float um, float us, float ulogs,
-                            float& lp_acc, float& pv, float& pm, float& ps) {
+                            float ulg, float& lp_acc, float& pv, float& pm, float& ps) {
     const bool scale_vec = is_vec(T.op[2].kind);
-    const bool normal = (T.dist == MC_DIST_NORMAL);
+    const bool lgv = lg_per_element(T.dist, T.op[1].kind, T.op[2].kind);
     const float w = T.weight;
     for (int64_t i = tid; i < T.n; i += nthr) {
         const float v = fetch(T.op[0], i, uv, q, P);
         const float m = fetch(T.op[1], i, um, q, P);
         const float s = fetch(T.op[2], i, us, q, P);
         const float logs = scale_vec ? logf(s) : ulogs;
-        const ElemOut e = normal ? elem_normal(T.c0, v, m, s, logs)
-                                 : elem_halfnormal(T.c0, v, s, logs);
+        const float lg = lgv ? lgamma_norm(T.dist, m, s) : ulg;
+        const ElemOut e = elem_eval(T.dist, T.c0, v, m, s, logs, lg);
         if (mask & PASS_LP) lp_acc += w * e.lp;
         if (mask & PASS_VALUE) accum(T.op[0], i, w * e.dv, pv, g, P);
         if (mask & PASS_LOC) accum(T.op[1], i, w * e.dm, pm, g, P);
@@ -538,7 +623,7 @@ MC_DEV float seg_fetch(const DevOperand& o, int64_t e, float uni, float prim, bo
 template <int WPC>
 MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float* g,
                         const Group<WPC>& G, uint32_t mask, float uv, float um, float us,
-                        float ulogs, float& lp_acc, float& pv, float& pm, float& ps,
+                        float ulogs, float ulg, float& lp_acc, float& pv, float& pm, float& ps,
                         float* vpart) {
     const int wave = G.tid >> 6;
     const int lane = G.tid & 63;
@@ -549,7 +634,8 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
     const bool acc_prim = (mask & (1u << a)) != 0;
     const bool split = T.ncomb > 0;
     const bool scale_vec = is_vec(T.op[2].kind);
-    const bool normal = (T.dist == MC_DIST_NORMAL);
+    const bool lgv = lg_per_element(T.dist, a == 1 ? MC_OP_PVEC : T.op[1].kind,
+                                    a == 2 ? MC_OP_PVEC : T.op[2].kind);
     const float w = T.weight;
     for (int t = wave; t < T.ntiles; t += WPC) {
         const int off = tiles[3 * t];
@@ -567,8 +653,8 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
                 const float m = seg_fetch(T.op[1], e, um, th, a == 1, q, P);
                 const float s = seg_fetch(T.op[2], e, us, th, a == 2, q, P);
                 const float logs = (scale_vec || a == 2) ? logf(s) : ulogs;
-                const ElemOut o = normal ? elem_normal(T.c0, vv, m, s, logs)
-                                         : elem_halfnormal(T.c0, vv, s, logs);
+                const float lg = lgv ? lgamma_norm(T.dist, m, s) : ulg;
+                const ElemOut o = elem_eval(T.dist, T.c0, vv, m, s, logs, lg);
                 if (mask & PASS_LP) lp_acc += w * o.lp;
                 if (mask & PASS_VALUE) {
                     if (a == 0) cp += w * o.dv;
@@ -607,6 +693,13 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
         scale_vec ? 0.0f : (T.op[2].kind == MC_OP_CONST ? T.clogs : logf(us));
     const float var = us * us;
     const bool normal = (T.dist == MC_DIST_NORMAL);
+    const bool moment_dist = normal || T.dist == MC_DIST_HALFNORMAL;
+    // the gammaln normaliser when it is the same for every element
+    const float ulg = lg_per_element(T.dist, T.op[1].kind, T.op[2].kind)
+                          ? 0.0f
+                          : ((T.op[1].kind == MC_OP_PSCALAR || T.op[2].kind == MC_OP_PSCALAR)
+                                 ? lgamma_norm(T.dist, um, us)
+                                 : T.clg);
 
     for (int pass = 0; pass < T.npass; ++pass) {
         const uint32_t mask = (T.pass_masks >> (4 * pass)) & 0xFu;
@@ -617,7 +710,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
         if (T.primary < 0) {
             const int fv = fast_kind(T.op[0].kind);
             const int fl = normal ? fast_kind(T.op[1].kind) : 0;
-            if (!scale_vec && fv >= 0 && fl >= 0) {
+            if (moment_dist && !scale_vec && fv >= 0 && fl >= 0) {
                 moments = true;
                 const int code = normal ? (fv * 3 + fl) : (9 + fv);
                 switch (code) {
@@ -642,8 +735,8 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                         break;
                 }
             } else {
-                strided_generic(T, P, q, g, tid, nthr, mask, uv, um, us, ulogs, lp_acc, pv, pm,
-                                ps);
+                strided_generic(T, P, q, g, tid, nthr, mask, uv, um, us, ulogs, ulg, lp_acc, pv,
+                                pm, ps);
             }
         } else {
             float* vpart = S.vpart;
@@ -656,8 +749,8 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                 else
                     seg_normal_uscale<WPC, 0>(T, P, q, g, G, mask, var, M, vpart);
             } else {
-                seg_generic<WPC>(T, P, q, g, G, mask, uv, um, us, ulogs, lp_acc, pv, pm, ps,
-                                 vpart);
+                seg_generic<WPC>(T, P, q, g, G, mask, uv, um, us, ulogs, ulg, lp_acc, pv, pm,
+                                 ps, vpart);
             }
             if (T.ncomb > 0 && (mask & (1u << T.primary))) {
                 // split segments: add the virtual partials in order

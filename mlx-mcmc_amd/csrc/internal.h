@@ -45,7 +45,8 @@ struct DevTerm {
                           // cotangents, evaluated by this one wave while the
                           // other waves move on (-1: every wave)
     float clogs;          // CONST scale: f32 log(scale), precomputed
-    float pad2;
+    float clg;            // Gamma / Beta with constant shapes: the gammaln
+                          // normaliser (lgamma_norm), precomputed
     DevOperand op[3];  // value, loc, scale
     // ---- segment-tiled layout (primary >= 0) --------------------------------
     // Elements are grouped by the primary index into runs ("segments"), long

@@ -61,6 +61,7 @@ struct SlTerm {
     int32_t doff[3];   // SK_DATA: float offset in the slice's block
     float cval[3];     // SK_CONST
     float cinv, cinv2; // CONST scale: f32 1/scale, 1/scale^2
+    float clg;         // Gamma / Beta with constant shapes: gammaln normaliser
     // int32 tables at these word offsets in the slice block
     int32_t tile_off;   // per iteration: {data offset, len_max, len_min / 4}
     int32_t lane_off;   // per (iteration, lane): {local slot or -1, len} (len 0: none)
@@ -147,6 +148,7 @@ MC_DEV SlTerm load_slterm(const MC_CONST SlTerm* p) {
     }
     t.cinv = p->cinv;
     t.cinv2 = p->cinv2;
+    t.clg = p->clg;
     t.tile_off = p->tile_off;
     t.lane_off = p->lane_off;
     t.round_off = p->round_off;
@@ -235,8 +237,9 @@ MC_DEV void sl_scalar_stage(const SlCtx& P, const float* q2, uint32_t pmask, flo
         const SlTerm T = load_slterm(cptr(P.sterms) + t);
         const float v = sl_uni(T, 0, qc), m = sl_uni(T, 1, qc), sc = sl_uni(T, 2, qc);
         const float ls = (T.kind[2] == SK_CONST) ? T.clogs : logf(sc);
-        const ElemOut e = (T.dist == MC_DIST_NORMAL) ? elem_normal(T.c0, v, m, sc, ls)
-                                                     : elem_halfnormal(T.c0, v, sc, ls);
+        const float lg = (T.kind[1] == SK_SHARED || T.kind[2] == SK_SHARED)
+                             ? lgamma_norm(T.dist, m, sc) : T.clg;
+        const ElemOut e = elem_eval(T.dist, T.c0, v, m, sc, ls, lg);
         const float wn = T.weight * (float)T.niter;
         // row (t, b): column 0 log p, column 1 + j shared parameter j
         float* row = st + (t * NB + b) * Dc;
@@ -364,15 +367,20 @@ MC_DEV void sl_term(const SlCtx& P, const SlTerm& T, const float* sd, const floa
                                         float& lpc, float& rcc, float& pvc, float& pmc,
                                         float& psc) {
                         const float lsc = (k2 == SK_PP) ? logf(thc) : lgc;
+                        // gammaln normaliser: per element when a shape varies by
+                        // element, else once per chain
+                        const bool lgv = (k1 == SK_DATA || k1 == SK_PP || k2 == SK_DATA ||
+                                          k2 == SK_PP);
+                        const float lgu = (k1 == SK_SHARED || k2 == SK_SHARED)
+                                              ? lgamma_norm(T.dist, umc, usc) : T.clg;
                         for (int u = 0; u < len; ++u) {
                             const int o = (u >> 2) * 256 + (u & 3);
                             const float v = (k0 == SK_DATA) ? x0[o] : (k0 == SK_PP ? thc : uvc);
                             const float m = (k1 == SK_DATA) ? x1[o] : (k1 == SK_PP ? thc : umc);
                             const float sc = (k2 == SK_DATA) ? x2[o] : (k2 == SK_PP ? thc : usc);
                             const float ls = (k2 == SK_DATA) ? logf(sc) : lsc;
-                            const ElemOut e = (T.dist == MC_DIST_NORMAL)
-                                                  ? elem_normal(c0, v, m, sc, ls)
-                                                  : elem_halfnormal(c0, v, sc, ls);
+                            const float lg = lgv ? lgamma_norm(T.dist, m, sc) : lgu;
+                            const ElemOut e = elem_eval(T.dist, c0, v, m, sc, ls, lg);
                             lpc += w * e.lp;
                             rcc += w * (T.pp == 0 ? e.dv : (T.pp == 1 ? e.dm : e.ds));
                             pvc += w * e.dv;

@@ -7,6 +7,10 @@ by autograd exactly where the reference uses ``mx.grad``.
 
   Normal      restates mlx_mcmc/distributions/normal.py:27-56
   HalfNormal  restates mlx_mcmc/distributions/halfnormal.py:28-63
+  Exponential restates mlx_mcmc/distributions/exponential.py:40-71
+  Gamma       restates mlx_mcmc/distributions/gamma.py:40-88
+  Beta        restates mlx_mcmc/distributions/beta.py:37-91
+              (gammaln: host float64 value, no gradient, as the reference)
   sum/array/log/exp/where/pi/inf  the mx.* calls those models use
 
 Pinned by the reference's own known-answer tests (tests/test_oracle_pins.py
@@ -85,3 +89,52 @@ class HalfNormal:
         var = self.scale ** 2
         log_prob_pos = self._log2 + self._log_norm - self._log_scale - 0.5 * (value ** 2) / var
         return torch.where(value >= 0, log_prob_pos, _t(-inf))
+
+
+def _gammaln(x):
+    """scipy.special.gammaln on the host, as gamma.py:48-59 / beta.py:45-57 call it:
+    float64 of the current float32 value, a constant for autograd."""
+    return torch.lgamma(_t(x).detach().double())
+
+
+class Exponential:
+    """exponential.py:40-71."""
+
+    def __init__(self, rate):
+        self.rate = _t(rate)
+
+    def log_prob(self, value):
+        value = _t(value)
+        lp = torch.log(self.rate) - self.rate * value
+        return torch.where(value >= 0, lp, _t(-inf))
+
+
+class Gamma:
+    """gamma.py:40-88 (shape alpha, rate beta)."""
+
+    def __init__(self, alpha, beta=1.0):
+        self.alpha = _t(alpha)
+        self.beta = _t(beta)
+        self._log_norm = self.alpha * torch.log(self.beta) - _gammaln(self.alpha).float()
+
+    def log_prob(self, value):
+        value = _t(value)
+        lp = self._log_norm + (self.alpha - 1) * torch.log(value) - self.beta * value
+        return torch.where(value > 0, lp, _t(-inf))
+
+
+class Beta:
+    """beta.py:37-91."""
+
+    def __init__(self, alpha, beta):
+        self.alpha = _t(alpha)
+        self.beta = _t(beta)
+        a, b = _gammaln(self.alpha), _gammaln(self.beta)
+        ab = torch.lgamma(self.alpha.detach().double() + self.beta.detach().double())
+        self._log_beta_const = (a + b - ab).float()
+
+    def log_prob(self, value):
+        value = _t(value)
+        lp = ((self.alpha - 1) * torch.log(value) + (self.beta - 1) * torch.log(1 - value)
+              - self._log_beta_const)
+        return torch.where((value > 0) & (value < 1), lp, _t(-inf))

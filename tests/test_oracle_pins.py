@@ -90,6 +90,76 @@ def test_oracle_gradient_matches_finite_differences():
     np.testing.assert_allclose(g, fd, rtol=1e-4, atol=1e-3)
 
 
+# ---- reference tests/test_new_distributions.py KATs --------------
+def test_exponential_gamma_beta_kats():
+    """test_new_distributions.py:18-38,89-101,137-156: support and values."""
+    assert np.isclose(float(ns.Exponential(2.0).log_prob(0.0)), np.log(2.0))
+    lp = float(ns.Exponential(1.0).log_prob(0.5))
+    assert lp < 0 and np.isfinite(lp)
+    assert float(ns.Exponential(1.0).log_prob(-1.0)) == -np.inf
+    lp = float(ns.Gamma(2, 1).log_prob(1.5))
+    assert lp < 0 and np.isfinite(lp)
+    assert float(ns.Gamma(2, 1).log_prob(-1.0)) == -np.inf
+    lp = float(ns.Beta(2, 2).log_prob(0.5))
+    assert np.isfinite(lp)
+    for v in (-0.1, 1.5, 0.0, 1.0):
+        assert float(ns.Beta(2, 2).log_prob(v)) == -np.inf
+
+
+def test_exponential_gamma_beta_match_scipy():
+    """float32 restatements vs float64 closed forms (scipy.stats)."""
+    import scipy.stats as st
+
+    rng = np.random.default_rng(1)
+    x = rng.uniform(0.01, 5, 200)
+    r = rng.uniform(0.2, 4, 200)
+    np.testing.assert_allclose(ns.Exponential(r).log_prob(x).numpy(),
+                               st.expon.logpdf(x, scale=1 / r), rtol=3e-6, atol=3e-6)
+    a, b = rng.uniform(0.5, 8, 200), rng.uniform(0.3, 5, 200)
+    np.testing.assert_allclose(ns.Gamma(a, b).log_prob(x).numpy(),
+                               st.gamma.logpdf(x, a, scale=1 / b), rtol=3e-6, atol=3e-5)
+    u = rng.uniform(0.01, 0.99, 200)
+    np.testing.assert_allclose(ns.Beta(a, b).log_prob(u).numpy(),
+                               st.beta.logpdf(u, a, b), rtol=3e-6, atol=3e-5)
+
+
+def test_new_distribution_gradients_follow_reference_autodiff():
+    """The gammaln normalisers carry no gradient (host scipy in the reference):
+    d/dalpha Gamma = log(beta) + log(x); d/dalpha Beta = log(x)."""
+    import torch
+
+    a = torch.tensor(2.5, requires_grad=True)
+    b = torch.tensor(1.5, requires_grad=True)
+    x = torch.tensor(0.7, requires_grad=True)
+    ns.Gamma(a, b).log_prob(x).backward()
+    assert np.isclose(float(a.grad), np.log(1.5) + np.log(0.7), rtol=1e-6)
+    assert np.isclose(float(b.grad), 2.5 / 1.5 - 0.7, rtol=1e-6)
+    assert np.isclose(float(x.grad), 1.5 / 0.7 - 1.5, rtol=1e-6)
+    a.grad = b.grad = x.grad = None
+    ns.Beta(a, b).log_prob(x).backward()
+    assert np.isclose(float(a.grad), np.log(0.7), rtol=1e-6)
+    assert np.isclose(float(b.grad), np.log(0.3), rtol=1e-5)
+    assert np.isclose(float(x.grad), 1.5 / 0.7 - 0.5 / 0.3, rtol=1e-5)
+
+
+def test_example03_04_models_closed_form():
+    """The example 03/04 models in the oracle equal their float64 closed forms."""
+    import scipy.stats as st
+    import workloads as W
+
+    lp, _ = W.event_rates(W.ns_oracle())
+    t = W.event_rates_data()
+    assert np.isclose(float(lp({"rate": 2.0})),
+                      st.gamma.logpdf(2.0, 2, scale=1) + st.expon.logpdf(t, scale=0.5).sum(),
+                      rtol=1e-6)
+    lp, _ = W.ab_testing(W.ns_oracle())
+    n, ca, cb = W.ab_testing_data()
+    ref = st.beta.logpdf(0.1, ca + 1, n - ca + 1) + st.beta.logpdf(0.12, cb + 1, n - cb + 1)
+    got = float(lp({"p_A": 0.1, "p_B": 0.12}))
+    # float32 log B(k + 1, n - k + 1) ~ -370 carries ~3e-5 of absolute rounding
+    assert abs(got - ref) < 1e-3
+
+
 # ---- HMC: reference tests/test_hmc.py ----------------------------------------
 def _std_normal(p):
     return ns.Normal(0, 1).log_prob(p["x"])

@@ -17,15 +17,17 @@ def ns_product():
     import mlx_mcmc_amd as m
     import mlx_mcmc_amd.core as mx
 
-    return SimpleNamespace(Normal=m.Normal, HalfNormal=m.HalfNormal, sum=mx.sum,
-                           array=mx.array, name="product")
+    return SimpleNamespace(Normal=m.Normal, HalfNormal=m.HalfNormal, Exponential=m.Exponential,
+                           Gamma=m.Gamma, Beta=m.Beta, sum=mx.sum, array=mx.array,
+                           name="product")
 
 
 def ns_oracle():
     from oracle import ns
 
-    return SimpleNamespace(Normal=ns.Normal, HalfNormal=ns.HalfNormal, sum=ns.sum,
-                           array=ns.array, name="oracle")
+    return SimpleNamespace(Normal=ns.Normal, HalfNormal=ns.HalfNormal, Exponential=ns.Exponential,
+                           Gamma=ns.Gamma, Beta=ns.Beta, sum=ns.sum, array=ns.array,
+                           name="oracle")
 
 
 # ---- config 1: examples/01_simple_normal.py:26-50 (vectorised as in
@@ -104,3 +106,48 @@ def illcond_normal(ns, D=100):
         return ns.sum(ns.Normal(0, scales).log_prob(params["x"]))
 
     return log_prob, {"x": np.zeros(D, np.float32)}
+
+
+# ---- SURVEY 8f-1 models: examples/03_ab_testing.py:26-59 and
+#      examples/04_event_rates.py:26-55 (same data generation and log_prob) ------
+def ab_testing_data():
+    np.random.seed(42)
+    n = 1000
+    ca = int(np.random.binomial(n, 0.12))
+    cb = int(np.random.binomial(n, 0.15))
+    return n, ca, cb
+
+
+def ab_testing(ns):
+    """Beta(1, 1) priors and Beta(k + 1, n - k + 1) 'likelihoods' on p_A, p_B:
+    the posterior of p_X is Beta(k_X + 1, n - k_X + 1)."""
+    n, ca, cb = ab_testing_data()
+
+    def log_prob(params):
+        p_a, p_b = params["p_A"], params["p_B"]
+        return (ns.Beta(1, 1).log_prob(p_a) + ns.Beta(1, 1).log_prob(p_b)
+                + ns.Beta(ca + 1, n - ca + 1).log_prob(p_a)
+                + ns.Beta(cb + 1, n - cb + 1).log_prob(p_b))
+
+    return log_prob, {"p_A": 0.1, "p_B": 0.1}
+
+
+def event_rates_data():
+    np.random.seed(42)
+    return np.random.exponential(scale=1 / 3.0, size=50)
+
+
+def event_rates(ns):
+    """Gamma(2, 1) prior, Exponential likelihood written as the reference's loop:
+    the posterior of the rate is Gamma(2 + n, 1 + sum t)."""
+    t = event_rates_data()
+
+    def log_prob(params):
+        rate = params["rate"]
+        lp = ns.Gamma(alpha=2, beta=1).log_prob(rate)
+        ll = ns.array(0.0)
+        for ti in t:
+            ll = ll + ns.Exponential(rate).log_prob(ns.array(ti))
+        return lp + ll
+
+    return log_prob, {"rate": 2.0}
