@@ -3,7 +3,7 @@
 Workload (BASELINE.json configs[2], SURVEY §8d "Large"): hierarchical Normal,
 D = 1000 parameters (theta[997], mu, tau, sigma), N = 100,000 observations,
 HMC with L = 20 leapfrog steps, 256 chains per GPU (configs[3] at N = 8: 2048
-chains, 256/GPU, RCCL gather of the samples).  One *step* = one HMC iteration
+chains, 256/GPU; ESS and R-hat reduced over RCCL as [2, D] moment blocks).  One *step* = one HMC iteration
 of every chain on the GPU = one launch of the persistent kernel k_hmc
 (L leapfrog steps, fused gradient tape, accept, sample store).
 
@@ -54,30 +54,9 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=15,
                     help="processes of the aggregate CPU baseline (0: skip)")
     ap.add_argument("--no-ess", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="also gather every rank's samples to rank 0 over RCCL (untimed)")
     return ap.parse_args()
-
-
-def ess_device(samples, max_lag=100):
-    """Reference compute_ess (examples/06_nuts_comparison.py:22-41) for every
-    (chain, param) series at once, on the device.  samples: [C, S, D]."""
-    import torch
-
-    x = samples.double()
-    n = x.shape[1]
-    mean = x.mean(dim=1, keepdim=True)
-    var = x.var(dim=1, unbiased=False)
-    xc = x - mean
-    acf_sum = torch.zeros_like(var)
-    active = var != 0
-    safe = torch.where(active, var, torch.ones_like(var))
-    for lag in range(1, min(n // 2, max_lag)):
-        if not bool(active.any()):
-            break
-        c = (xc[:, :-lag] * xc[:, lag:]).mean(dim=1) / safe
-        acf_sum = torch.where(active, acf_sum + c, acf_sum)
-        active = active & ~(c < 0.05)
-    ess = n / (1.0 + 2.0 * acf_sum)
-    return torch.where(var == 0, torch.full_like(ess, float(n)), ess)   # [C, D]
 
 
 def cpu_baseline(G, N, L, step_size, budget_s, chain=0):
@@ -213,12 +192,21 @@ def main():
     accept = float(np.mean(sc["n_accept"] / np.maximum(sc["n_total"], 1)))
     eps = float(np.mean(sc["step_size"]))
 
-    # ---- final sample gather over RCCL (not timed) -----------------------------
+    # ---- diagnostics on the device (not timed) ----------------------------------
+    # ESS per (chain, element) with the reference rule and split R-hat; across
+    # ranks only [2, D] f64 moment blocks are all-reduced (RCCL), no samples move
+    diag = None
+    diag_ms = None
+    if not args.no_ess and K >= 10:
+        from mlx_mcmc_amd.diagnostics import chain_diagnostics
+
+        td = time.perf_counter()
+        diag = chain_diagnostics(samples[:, :K, :])
+        diag_ms = (time.perf_counter() - td) * 1e3
     gather_ms = None
-    all_samples = samples
-    if world > 1:
+    if world > 1 and args.gather:
         tg = time.perf_counter()
-        all_samples = gather_to_root(samples)   # RCCL, the only collective
+        gather_to_root(samples)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
 
@@ -275,12 +263,15 @@ def main():
         }
         if gather_ms is not None:
             out["gather_ms"] = gather_ms
-        if not args.no_ess and K >= 10:
-            ess = ess_device(all_samples[:, :K, :])           # [C_total, D]
-            ess_sum = ess.sum(dim=0)                          # per param
+        if diag is not None:
+            ess_sum = diag["ess_sum"]                         # per element, all chains
             out["ess_per_sec"] = {"min": float(ess_sum.min()) / elapsed,
-                                  "median": float(ess_sum.median()) / elapsed,
-                                  "unit": "effective samples/s (sum over chains)"}
+                                  "median": float(np.median(ess_sum)) / elapsed,
+                                  "unit": "effective samples/s (sum over chains)",
+                                  "draws": K}
+            out["rhat"] = {"max": float(np.nanmax(diag["rhat"])),
+                           "median": float(np.nanmedian(diag["rhat"])), "split": True}
+            out["diagnostics_ms"] = diag_ms
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(G, N, L, max(eps, 1e-4), args.cpu_seconds)
             out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]

@@ -20,6 +20,9 @@
  *   mlx_mcmc/distributions/gamma.py:40-88              MC_DIST_GAMMA term / mc_dist_log_prob
  *   mlx_mcmc/distributions/beta.py:37-91               MC_DIST_BETA term / mc_dist_log_prob
  *   mlx.core.random (key/split/normal/uniform)         Philox4x32-10 counter RNG, mc_rng_fill
+ *   examples/06_nuts_comparison.py:22-41 compute_ess   mc_series_stats (MC_ST_ESS)
+ *   README.md:214 roadmap "R-hat" (no reference code)  mc_stats_reduce + mc_rhat
+ *   mlx_mcmc/inference/mcmc.py:191-227 summary         mc_pool_moments, mc_select
  *
  * The reference is pure Python on MLX and has no FFI of its own; the
  * Python host layer of this repository (mlx_mcmc_amd/_lib.py) binds these
@@ -256,6 +259,48 @@ int mc_nuts_run(const mc_program* prog, const mc_run_config* cfg,
 int mc_rng_fill(uint64_t seed, uint32_t chain, uint32_t iteration,
                 uint32_t tag, uint32_t sub, uint32_t index0, int64_t n,
                 int32_t mode, void* out_dev, void* hip_stream);
+
+/* ---- diagnostics over a sample buffer [C, S, D] (device, f32) ---------- */
+/* A series is samples[c, :, d].  mc_series_stats writes stats[f * C*D + c*D + d]
+ * (f64, device) for each field f:                                            */
+#define MC_ST_ESS     0   /* compute_ess (examples/06_nuts_comparison.py:22-41):
+                             n / (1 + 2 sum rho_k), lags 1 .. min(S/2, max_lag)-1,
+                             stopping at (and including) the first rho < 0.05;
+                             S when the variance is 0.  max_lag = 100 there.  */
+#define MC_ST_MEAN    1   /* series mean                                      */
+#define MC_ST_M2      2   /* sum of squared deviations from the mean          */
+#define MC_ST_HMEAN0  3   /* mean of draws [0, S/2)                           */
+#define MC_ST_HMEAN1  4   /* mean of draws [S - S/2, S)                       */
+#define MC_ST_HM2_0   5   /* sum of squared deviations, first half            */
+#define MC_ST_HM2_1   6   /* sum of squared deviations, second half           */
+#define MC_ST_COUNT   7
+int mc_series_stats(int64_t C, int64_t S, int64_t D, const float* samples_dev,
+                    int32_t max_lag, double* stats_dev, void* hip_stream);
+/* Chain-order reduction to out_dev[2, D] (f64).  center_dev == NULL:
+ *   out[0][d] = sum of the 2C half-chain means, out[1][d] = sum_c ESS.
+ * center_dev = that out[0] summed over every rank (m_total = all half chains):
+ *   out[0][d] = sum (half mean - center[d]/m_total)^2,
+ *   out[1][d] = sum of half-chain variances (ddof 1).
+ * Multi-GPU: all-reduce (sum) out between the two calls and after the second. */
+int mc_stats_reduce(int64_t C, int64_t S, int64_t D, const double* stats_dev,
+                    const double* center_dev, int64_t m_total, double* out_dev,
+                    void* hip_stream);
+/* Split R-hat (Gelman et al., BDA3 eq. 11.4) over m_total half chains of
+ * S/2 draws from the second reduction: rhat_dev[D] (f64).  S >= 4.          */
+int mc_rhat(int64_t D, int64_t m_total, int64_t S, const double* spread_dev,
+            double* rhat_dev, void* hip_stream);
+/* Pooled mean and std (ddof 0) of every value of elements [off, off+len)
+ * over all chains and draws (mcmc.py:205-206): out_dev[2] f64.             */
+int mc_pool_moments(int64_t C, int64_t S, int64_t D, const double* stats_dev,
+                    int64_t off, int64_t len, double* out_dev, void* hip_stream);
+/* Exact order statistics (0-based ranks k[0..nk), host array, nk <= 8) of the
+ * pooled values of elements [off, off+len): out_dev[nk] f32; NaN if any
+ * pooled value is NaN (np.percentile / np.median, mcmc.py:207-209).          */
+int64_t mc_select_workspace_bytes(int32_t nk);
+int mc_select(int64_t C, int64_t S, int64_t D, const float* samples_dev,
+              int64_t off, int64_t len, int32_t nk, const int64_t* k,
+              float* out_dev, void* workspace_dev, int64_t workspace_bytes,
+              void* hip_stream);
 
 const char* mc_last_error(void);
 int32_t mc_abi_version(void);

@@ -39,6 +39,10 @@ MC_DIST_EXPONENTIAL = 2
 MC_DIST_GAMMA = 3
 MC_DIST_BETA = 4
 
+# mc_series_stats fields (include/mcmc355.h)
+MC_ST_ESS, MC_ST_MEAN, MC_ST_M2, MC_ST_HMEAN0, MC_ST_HMEAN1, MC_ST_HM2_0, MC_ST_HM2_1 = range(7)
+MC_ST_COUNT = 7
+
 MC_OP_NONE = 0
 MC_OP_CONST = 1
 MC_OP_PSCALAR = 2
@@ -161,6 +165,18 @@ SIGNATURES = [
     ("mc_rng_fill", ctypes.c_int,
      [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_uint32, ctypes.c_int64, ctypes.c_int32, _VP, _VP]),
+    ("mc_series_stats", ctypes.c_int,
+     [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _VP, ctypes.c_int32, _VP, _VP]),
+    ("mc_stats_reduce", ctypes.c_int,
+     [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _VP, _VP, ctypes.c_int64, _VP, _VP]),
+    ("mc_rhat", ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _VP, _VP, _VP]),
+    ("mc_pool_moments", ctypes.c_int,
+     [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _VP, ctypes.c_int64, ctypes.c_int64, _VP,
+      _VP]),
+    ("mc_select_workspace_bytes", ctypes.c_int64, [ctypes.c_int32]),
+    ("mc_select", ctypes.c_int,
+     [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _VP, ctypes.c_int64, ctypes.c_int64,
+      ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), _VP, _VP, ctypes.c_int64, _VP]),
     ("mc_last_error", ctypes.c_char_p, []),
     ("mc_abi_version", ctypes.c_int32, []),
 ]

@@ -12,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#include "diag.h"
 #include "eval.h"
 #include "hmc.h"
 #include "internal.h"
@@ -1485,6 +1486,103 @@ extern "C" int mc_debug_stamps_wg(unsigned long long* wg) {
     return MC_OK;
 }
 #endif
+
+// ---------------------------------------------------------------------------
+// diagnostics (diag.h)
+// ---------------------------------------------------------------------------
+static int check_csd(int64_t C, int64_t S, int64_t D, const void* x) {
+    if (C < 1 || S < 1 || D < 1) return fail(MC_ERR_INVALID, "C, S and D must be >= 1");
+    if (!x) return fail(MC_ERR_INVALID, "samples is NULL");
+    return MC_OK;
+}
+
+extern "C" int mc_series_stats(int64_t C, int64_t S, int64_t D, const float* samples,
+                               int32_t max_lag, double* stats, void* stream) {
+    if (int rc = check_csd(C, S, D, samples)) return rc;
+    if (!stats) return fail(MC_ERR_INVALID, "stats is NULL");
+    if (max_lag < 1) return fail(MC_ERR_INVALID, "max_lag must be >= 1");
+    const int32_t lmax = (int32_t)std::min<int64_t>(S / 2, max_lag);
+    const int64_t blocks = (C * D + 255) / 256;
+    hipLaunchKernelGGL(k_series_stats, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       samples, C, S, D, lmax, stats);
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+extern "C" int mc_stats_reduce(int64_t C, int64_t S, int64_t D, const double* stats,
+                               const double* center, int64_t m_total, double* out, void* stream) {
+    if (int rc = check_csd(C, S, D, stats)) return rc;
+    if (!out) return fail(MC_ERR_INVALID, "out is NULL");
+    if (center && (S < 4 || m_total < 2))
+        return fail(MC_ERR_INVALID, "split R-hat needs S >= 4 draws and >= 2 half chains");
+    hipLaunchKernelGGL(k_stats_reduce, dim3((unsigned)((D + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, stats, C, S, D, center ? 1 : 0, center, m_total, out);
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+extern "C" int mc_rhat(int64_t D, int64_t m_total, int64_t S, const double* spread, double* rhat,
+                       void* stream) {
+    if (D < 1 || !spread || !rhat) return fail(MC_ERR_INVALID, "bad mc_rhat arguments");
+    if (S < 4 || m_total < 2)
+        return fail(MC_ERR_INVALID, "split R-hat needs S >= 4 draws and >= 2 half chains");
+    hipLaunchKernelGGL(k_rhat, dim3((unsigned)((D + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, spread, D, m_total, S / 2, rhat);
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+extern "C" int mc_pool_moments(int64_t C, int64_t S, int64_t D, const double* stats, int64_t off,
+                               int64_t len, double* out, void* stream) {
+    if (int rc = check_csd(C, S, D, stats)) return rc;
+    if (off < 0 || len < 1 || off + len > D || !out)
+        return fail(MC_ERR_INVALID, "element range [%lld, %lld) outside [0, %lld)", (long long)off,
+                    (long long)(off + len), (long long)D);
+    hipLaunchKernelGGL(k_pool_moments, dim3(1), dim3(256), 0, (hipStream_t)stream, stats, C, S, D,
+                       off, len, out);
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
+extern "C" int64_t mc_select_workspace_bytes(int32_t nk) {
+    if (nk < 1 || nk > kSelMaxTargets) return -1;
+    return (int64_t)nk * (int64_t)(sizeof(SelState) + 256 * sizeof(unsigned long long)) + 16;
+}
+
+extern "C" int mc_select(int64_t C, int64_t S, int64_t D, const float* samples, int64_t off,
+                         int64_t len, int32_t nk, const int64_t* k, float* out, void* ws,
+                         int64_t ws_bytes, void* stream) {
+    if (int rc = check_csd(C, S, D, samples)) return rc;
+    if (off < 0 || len < 1 || off + len > D)
+        return fail(MC_ERR_INVALID, "element range outside [0, D)");
+    if (nk < 1 || nk > kSelMaxTargets || !k || !out)
+        return fail(MC_ERR_INVALID, "nk must be in [1, %d] with k and out set", kSelMaxTargets);
+    if (!ws || ws_bytes < mc_select_workspace_bytes(nk))
+        return fail(MC_ERR_INVALID, "workspace too small (need %lld bytes)",
+                    (long long)mc_select_workspace_bytes(nk));
+    const int64_t rows = C * S, n = rows * len;
+    SelTargets tg{};
+    tg.nk = nk;
+    for (int i = 0; i < nk; ++i) {
+        if (k[i] < 0 || k[i] >= n)
+            return fail(MC_ERR_INVALID, "rank %lld outside [0, %lld)", (long long)k[i], (long long)n);
+        tg.k[i] = k[i];
+    }
+    hipStream_t st = (hipStream_t)stream;
+    SelState* stt = (SelState*)ws;
+    unsigned long long* hist = (unsigned long long*)(stt + nk);
+    uint32_t* nanf = (uint32_t*)(hist + nk * 256);
+    hipLaunchKernelGGL(k_sel_init, dim3(1), dim3(256), 0, st, tg, stt, hist, nanf);
+    const unsigned blocks = (unsigned)std::min<int64_t>((n + 1023) / 1024, 2048);
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        hipLaunchKernelGGL(k_sel_hist, dim3(blocks), dim3(256), 0, st, samples, rows, D, off, len,
+                           nk, shift, stt, hist, nanf);
+        hipLaunchKernelGGL(k_sel_pick, dim3(1), dim3(64), 0, st, nk, shift, stt, hist, nanf,
+                           shift == 0 ? out : nullptr);
+    }
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
 
 extern "C" const char* mc_last_error(void) { return g_last_error.c_str(); }
 extern "C" int32_t mc_abi_version(void) { return MC_ABI_VERSION; }

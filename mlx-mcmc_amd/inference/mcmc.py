@@ -4,7 +4,10 @@
 the MI355X kernels exactly as the reference's branches do (mcmc.py:83-133):
 ``key`` is built from ``random_seed``, extra kwargs go to the sampler,
 samples are stored as NumPy arrays in ``.samples`` and the rate in
-``.acceptance_rate``.  ``summary`` / ``print_summary`` follow mcmc.py:191-246.
+``.acceptance_rate``.  ``summary`` / ``print_summary`` follow mcmc.py:191-246,
+computed on the device from the kept [C, S, D] sample buffer
+(diagnostics.summarize: per-series moments and exact order statistics);
+``diagnostics()`` adds per-element ESS and split R-hat.
 
 ``method='metropolis'`` (the reference default, mcmc.py:43,135-189) is not on
 the GPU hot path this engine covers and raises
@@ -14,6 +17,7 @@ from __future__ import annotations
 
 import numpy as np
 
+from .. import diagnostics as _diag
 from .. import random as _random
 from ..kernels.hmc import hmc
 from ..kernels.nuts import nuts
@@ -38,6 +42,7 @@ class MCMC:
             sampler = hmc if method == 'hmc' else nuts
             kwargs = dict(kwargs)
             kwargs['return_info'] = True
+            kwargs.setdefault('keep_on_device', True)
             samples, accept_rate, info = sampler(
                 self.log_prob_fn, initial_params, num_samples=num_samples,
                 num_warmup=num_warmup, key=_random.key(random_seed), **kwargs)
@@ -56,21 +61,34 @@ class MCMC:
         raise ValueError(f"Unknown sampling method: {method}")
 
     def summary(self, credible_interval=0.95):
+        """Per parameter: mean, std, median and the central credible interval
+        over every chain, draw and element (mcmc.py:191-227)."""
         if self.samples is None:
             raise ValueError("Must run sampling first. Call run() method.")
-        alpha = 1 - credible_interval
-        lower_pct = 100 * alpha / 2
-        upper_pct = 100 * (1 - alpha / 2)
-        summary = {}
-        for name, s in self.samples.items():
-            summary[name] = {
-                'mean': float(np.mean(s)),
-                'std': float(np.std(s)),
-                'median': float(np.median(s)),
-                f'{lower_pct:.1f}%': float(np.percentile(s, lower_pct)),
-                f'{upper_pct:.1f}%': float(np.percentile(s, upper_pct)),
-            }
-        return summary
+        dev = getattr(self.info, "device_samples", None)
+        if dev is not None:
+            return _diag.summarize(dev, self.info.layout, credible_interval)
+        return _diag.summarize(self.samples, None, credible_interval)
+
+    def diagnostics(self, max_lag=100):
+        """Per parameter: ESS per chain (examples/06_nuts_comparison.py:22-41
+        rule), ESS summed over chains and split R-hat, shaped like the
+        parameter (chain axis first for the per-chain ESS)."""
+        if self.samples is None:
+            raise ValueError("Must run sampling first. Call run() method.")
+        dev = getattr(self.info, "device_samples", None)
+        if dev is None:
+            raise ValueError("diagnostics need the device samples (keep_on_device=True)")
+        d = _diag.chain_diagnostics(dev, max_lag=max_lag, group=False)
+        lay = self.info.layout
+        out = {}
+        C = d["ess"].shape[0]
+        for name, shape, off in zip(lay.names, lay.shapes, lay.offsets):
+            n = int(np.prod(shape)) if shape else 1
+            out[name] = {"ess": d["ess"][:, off:off + n].reshape((C,) + tuple(shape)),
+                         "ess_sum": d["ess_sum"][off:off + n].reshape(shape),
+                         "r_hat": d["rhat"][off:off + n].reshape(shape)}
+        return out
 
     def print_summary(self, credible_interval=0.95):
         summary = self.summary(credible_interval)

@@ -311,7 +311,7 @@ def test_nuts_freezes_like_the_reference_on_example06():
 
 # ---- ESS (examples/06_nuts_comparison.py:22-41) ---------------------------------
 def test_ess_batch_matches_reference_loop():
-    from mlx_mcmc_amd.diagnostics import ess_batch
+    from oracle.diag import ess_batch
 
     rng = np.random.default_rng(1)
     x = np.zeros((2000, 5))
@@ -323,3 +323,38 @@ def test_ess_batch_matches_reference_loop():
     x[:, 4] = 3.0  # zero variance -> n
     ref = np.array([S.compute_ess(x[:, j]) for j in range(5)])
     np.testing.assert_allclose(ess_batch(x), ref, rtol=1e-12)
+
+
+# ---- split R-hat (BDA3 11.4; the reference has none: README.md:214) ---------------
+def test_split_rhat_known_answers():
+    from oracle.diag import split_rhat
+
+    # halves [0,1] [4,5] [2,3] [6,7]: W = 0.5, B/n = 20/3, var+ = 0.25 + 20/3
+    x = np.array([[0, 1, 2, 3], [4, 5, 6, 7]], np.float64)
+    assert abs(split_rhat(x) - np.sqrt((0.25 + 20 / 3) / 0.5)) < 1e-12
+    rng = np.random.default_rng(0)
+    assert abs(split_rhat(rng.normal(size=(8, 4000))) - 1.0) < 0.01
+    drift = rng.normal(size=(4, 1000)) + np.linspace(0, 5, 1000)
+    assert split_rhat(drift) > 1.3          # a trend is caught by the split
+
+
+# ---- MCMC.summary quantiles (mcmc.py:207-209) --------------------------------------
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 40, 999, 1000, 40001, 3_000_017])
+@pytest.mark.parametrize("ci", [0.95, 0.9, 0.5, 0.99])
+def test_quantiles_from_order_stats_match_numpy(n, ci):
+    """The device summary assembles median / percentiles from exact order
+    statistics; the assembly must reproduce np.median / np.percentile bit for
+    bit on float32 pools (here the order statistics come from np.sort)."""
+    from mlx_mcmc_amd.diagnostics import quantiles_from_order_stats
+
+    rng = np.random.default_rng(n)
+    x = rng.normal(3.0, 2.0, n).astype(np.float32)
+    if n > 10:
+        x[: n // 10] = x[n // 10]                     # ties
+    xs = np.sort(x)
+    alpha = 1 - ci
+    lo_p, hi_p = 100 * alpha / 2, 100 * (1 - alpha / 2)
+    med, lo, hi = quantiles_from_order_stats(n, lo_p, hi_p, lambda r: xs[np.array(r)])
+    assert float(med) == float(np.median(x))
+    assert float(lo) == float(np.percentile(x, lo_p))
+    assert float(hi) == float(np.percentile(x, hi_p))
