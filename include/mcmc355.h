@@ -12,6 +12,8 @@
  *   mlx_mcmc/kernels/hmc.py:102-111 hamiltonian        (fused inside mc_hmc_run)
  *   mlx_mcmc/kernels/hmc.py:113-153 hmc_step           (fused inside mc_hmc_run)
  *   mlx_mcmc/kernels/nuts.py:16-358 nuts()             mc_nuts_run (+ mc_state_init)
+ *   mlx_mcmc/kernels/metropolis.py:6-101               mc_mh_run (+ mc_state_init)
+ *     metropolis_hastings()
  *   mlx_mcmc/kernels/nuts.py:137-218 build_tree        (iterative, inside mc_nuts_run)
  *   mlx_mcmc/kernels/nuts.py:119-135 no_u_turn         (inside mc_nuts_run)
  *   mlx_mcmc/distributions/normal.py:33-56 log_prob    MC_DIST_NORMAL term / mc_dist_log_prob
@@ -244,6 +246,22 @@ int mc_nuts_run(const mc_program* prog, const mc_run_config* cfg,
                 void* state_dev, float* samples_dev, const mc_trace* trace,
                 void* workspace_dev, int64_t workspace_bytes, void* hip_stream);
 
+/* Random-walk Metropolis-Hastings (metropolis.py:6-101): per iteration
+ * q' = q + f32(z * f32(proposal_scale)), z ~ N(0, I) (Philox, tag
+ * MC_RNG_TAG_PROPOSAL), accept iff f32 log U < f32(lp(q') - lp(q)) (NaN
+ * rejects), the current point is stored after every iteration.  The forward
+ * tape only: one log density evaluation per iteration.  Every iteration of
+ * the launch is a sampling iteration (set num_warmup = 0; MCMC.run's warmup
+ * is a separate sampler run with its own seed, mcmc.py:145-178).  Uses
+ * num_chains, chain_offset, iter_begin/iter_count, sample_begin/capacity and
+ * seed of cfg; the state's logp (mc_state_init) is the current log density.
+ * The gradient section of the state is not updated.  Trace: accepted,
+ * accept_stat = log ratio, step_size = proposal scale, energy = log p.      */
+int64_t mc_mh_workspace_bytes(const mc_program* prog, int64_t num_chains);
+int mc_mh_run(const mc_program* prog, const mc_run_config* cfg, double proposal_scale,
+              void* state_dev, float* samples_dev, const mc_trace* trace,
+              void* workspace_dev, int64_t workspace_bytes, void* hip_stream);
+
 /* ---- RNG (replaces mx.random for the sampler draws) --------------------- */
 /* Philox4x32-10 (Salmon et al., SC'11).  key = (seed lo, seed hi); counter =
  * (chain, iteration, tag << 24 | sub, index).  mode 0: raw u32 words
@@ -255,6 +273,7 @@ int mc_nuts_run(const mc_program* prog, const mc_run_config* cfg,
 #define MC_RNG_TAG_SLICE    3
 #define MC_RNG_TAG_DEPTH    4
 #define MC_RNG_TAG_MERGE    5
+#define MC_RNG_TAG_PROPOSAL 6   /* Metropolis-Hastings random-walk noise      */
 #define MC_RNG_TAG_USER     16
 int mc_rng_fill(uint64_t seed, uint32_t chain, uint32_t iteration,
                 uint32_t tag, uint32_t sub, uint32_t index0, int64_t n,

@@ -3,7 +3,7 @@
 A ``ChainSet`` owns, for C chains of one program, the state blob of
 include/mcmc355.h (per-chain scalars + position + gradient), the sampler
 workspace and the optional trace buffers, all as torch tensors on the current
-ROCm device.  ``run_hmc`` / ``run_nuts`` launch iterations
+ROCm device.  ``run_hmc`` / ``run_nuts`` / ``run_mh`` launch iterations
 [iter_begin, iter_begin + iter_count) on torch's current stream; splitting a
 run into several launches does not change any draw or result.
 """
@@ -142,6 +142,20 @@ class ChainSet:
         _lib.check(self.lib.mc_hmc_run(
             self.program.handle, ctypes.byref(c), _lib.ptr(self.state), _lib.ptr(samples),
             ctypes.byref(tr) if tr is not None else None, _lib.ptr(ws),
+            ws.numel() if ws is not None else 0, _lib.stream_handle()))
+
+    def run_mh(self, *, proposal_scale: float, samples=None, trace: Optional[Trace] = None,
+               **cfg):
+        """Random-walk Metropolis-Hastings iterations (csrc/mh.h)."""
+        cfg.setdefault("step_size", self.step_size0)
+        cfg.setdefault("target_accept", 0.0)
+        c = self._config(**cfg)
+        need = self.lib.mc_mh_workspace_bytes(self.program.handle, self.C)
+        ws = self._workspace(need)
+        tr = trace.c_struct() if trace is not None else None
+        _lib.check(self.lib.mc_mh_run(
+            self.program.handle, ctypes.byref(c), float(proposal_scale), _lib.ptr(self.state),
+            _lib.ptr(samples), ctypes.byref(tr) if tr is not None else None, _lib.ptr(ws),
             ws.numel() if ws is not None else 0, _lib.stream_handle()))
 
     def check_status(self) -> None:

@@ -55,6 +55,7 @@ MC_RNG_TAG_ACCEPT = 2
 MC_RNG_TAG_SLICE = 3
 MC_RNG_TAG_DEPTH = 4
 MC_RNG_TAG_MERGE = 5
+MC_RNG_TAG_PROPOSAL = 6
 MC_RNG_TAG_USER = 16
 
 
@@ -161,6 +162,10 @@ SIGNATURES = [
     ("mc_nuts_workspace_bytes", ctypes.c_int64, [_VP, ctypes.c_int64, ctypes.c_int32]),
     ("mc_nuts_run", ctypes.c_int,
      [_VP, ctypes.POINTER(McRunConfig), _VP, _VP, ctypes.POINTER(McTrace), _VP,
+      ctypes.c_int64, _VP]),
+    ("mc_mh_workspace_bytes", ctypes.c_int64, [_VP, ctypes.c_int64]),
+    ("mc_mh_run", ctypes.c_int,
+     [_VP, ctypes.POINTER(McRunConfig), ctypes.c_double, _VP, _VP, ctypes.POINTER(McTrace), _VP,
       ctypes.c_int64, _VP]),
     ("mc_rng_fill", ctypes.c_int,
      [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,

@@ -678,7 +678,9 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
 }
 
 // ---------------------------------------------------------------------------
-template <int WPC>
+// VALUE_ONLY: the forward tape alone (Metropolis-Hastings, mh.h) — every
+// sweep keeps only its PASS_LP work and nothing is written to g.
+template <int WPC, bool VALUE_ONLY = false>
 MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* g,
                       const Group<WPC>& G, float& lp_acc, const SegScratch& S) {
     const bool task = T.wave_task >= 0;
@@ -702,7 +704,9 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                                  : T.clg);
 
     for (int pass = 0; pass < T.npass; ++pass) {
-        const uint32_t mask = (T.pass_masks >> (4 * pass)) & 0xFu;
+        const uint32_t mask =
+            ((T.pass_masks >> (4 * pass)) & 0xFu) & (VALUE_ONLY ? PASS_LP : 0xFu);
+        if (VALUE_ONLY && mask == 0) continue;  // uniform: no writes, no barrier needed
         float pv = 0.0f, pm = 0.0f, ps = 0.0f;
         Moments M = {0.0f, 0.0f, 0.0f, false};
         bool moments = false;
@@ -775,20 +779,21 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
         if ((mask & PASS_VALUE) && T.op[0].kind == MC_OP_PSCALAR) flush(T.op[0].slot, pv);
         if ((mask & PASS_LOC) && T.op[1].kind == MC_OP_PSCALAR) flush(T.op[1].slot, pm);
         if ((mask & PASS_SCALE) && T.op[2].kind == MC_OP_PSCALAR) flush(T.op[2].slot, ps);
-        if (pass + 1 < T.npass) G.sync();  // passes exist because their writes overlap
+        if (!VALUE_ONLY && pass + 1 < T.npass) G.sync();  // passes exist because their writes overlap
     }
 }
 
-// Log density at q and its gradient into g (g may not alias q).  Every thread
+// Log density at q and its gradient into g (g may not alias q; unused and may
+// be NULL with VALUE_ONLY).  Every thread
 // of the group returns the same value.  Barriers: one after zeroing g (skipped
 // when the caller zeroed it in its own sweep), one before a term whose vector
 // writes overlap an earlier term's since the last barrier (host-computed
 // sync_before), one before and one after the fixed-order slot reduction.
-template <int WPC>
+template <int WPC, bool VALUE_ONLY = false>
 MC_DEV float eval_lp_grad(const DevCtx& P, const float* q, float* g, const Group<WPC>& G,
                           const SegScratch& S, bool g_zeroed = false) {
     MC_STAMP_DECL
-    if (!g_zeroed) {
+    if (!VALUE_ONLY && !g_zeroed) {
         for (int j = G.tid; j < P.D; j += G.T) g[j] = 0.0f;
         G.sync();
     }
@@ -796,9 +801,9 @@ MC_DEV float eval_lp_grad(const DevCtx& P, const float* q, float* g, const Group
     const MC_CONST DevTerm* terms = cptr(P.terms);
     for (int t = 0; t < P.n_terms; ++t) {
         const DevTerm T = load_term(terms + t);
-        if (T.sync_before) G.sync();
+        if (!VALUE_ONLY && T.sync_before) G.sync();
         MC_STAMP(2 + 2 * (t < 7 ? t : 7));
-        eval_term<WPC>(T, P, q, g, G, lp_acc, S);
+        eval_term<WPC, VALUE_ONLY>(T, P, q, g, G, lp_acc, S);
         MC_STAMP(3 + 2 * (t < 7 ? t : 7));
     }
     const int lp_slot = P.nslots - 1;
@@ -809,7 +814,7 @@ MC_DEV float eval_lp_grad(const DevCtx& P, const float* q, float* g, const Group
     const MC_CONST int* fin = cptr(P.index) + P.sfin_base;
     const int nsp = fin[0];
     const MC_CONST int* ids = fin + 1 + 3 * nsp;
-    for (int i = G.tid; i < nsp; i += G.T) {
+    for (int i = G.tid; i < (VALUE_ONLY ? 0 : nsp); i += G.T) {
         const int poff = fin[1 + 3 * i], first = fin[2 + 3 * i], cnt = fin[3 + 3 * i];
         float t = 0.0f;
         for (int c = 0; c < cnt; ++c) {

@@ -9,9 +9,10 @@ computed on the device from the kept [C, S, D] sample buffer
 (diagnostics.summarize: per-series moments and exact order statistics);
 ``diagnostics()`` adds per-element ESS and split R-hat.
 
-``method='metropolis'`` (the reference default, mcmc.py:43,135-189) is not on
-the GPU hot path this engine covers and raises
-``NotImplementedError``; unknown methods raise ``ValueError`` (mcmc.py:138).
+``method='metropolis'`` (the reference default) follows mcmc.py:135-189: a
+warmup run of ``metropolis_hastings`` with ``random_seed``, then a sampling
+run from its last draw with ``random_seed + 1`` (both on the GPU, k_mh in
+csrc/mh.h).  Unknown methods raise ``ValueError`` (mcmc.py:138).
 """
 from __future__ import annotations
 
@@ -20,6 +21,7 @@ import numpy as np
 from .. import diagnostics as _diag
 from .. import random as _random
 from ..kernels.hmc import hmc
+from ..kernels.metropolis import metropolis_hastings
 from ..kernels.nuts import nuts
 
 
@@ -54,11 +56,52 @@ class MCMC:
                 print("Sampling complete!")
                 print(f"{'=' * 70}\n")
             return self.samples
-        if method == 'metropolis':
-            raise NotImplementedError(
-                "method='metropolis' is not implemented on the MI355X engine (its hot path is "
-                "gradient-based HMC/NUTS); use method='hmc' or method='nuts'")
-        raise ValueError(f"Unknown sampling method: {method}")
+        if method != 'metropolis':
+            raise ValueError(f"Unknown sampling method: {method}")
+        sampler = metropolis_hastings
+        if verbose:
+            print(f"\n{'=' * 70}")
+            print(f"MLX-MCMC: {method.upper()} Sampling")
+            print(f"{'=' * 70}\n")
+        kwargs = dict(kwargs)
+        kwargs['return_info'] = True
+        kwargs.setdefault('keep_on_device', True)
+        # warmup phase (mcmc.py:145-165): a sampler run whose last draw starts sampling
+        if num_warmup > 0:
+            if verbose:
+                print(f"Warmup phase: {num_warmup} samples")
+            wkw = dict(kwargs)
+            wkw['keep_on_device'] = False
+            warmup_samples, warmup_accept, winfo = sampler(
+                self.log_prob_fn, initial_params, num_samples=num_warmup,
+                proposal_scale=proposal_scale, random_seed=random_seed, verbose=verbose, **wkw)
+            if verbose:
+                print(f"Warmup acceptance rate: {float(np.mean(warmup_accept)):.2%}\n")
+            if np.ndim(warmup_accept) == 0:
+                final_warmup = {k: v[-1] for k, v in warmup_samples.items()}
+            else:  # several chains: each continues from its own last draw
+                C = len(warmup_accept)
+                final_warmup = initial_params
+                kwargs['initial_positions'] = np.concatenate(
+                    [np.asarray(warmup_samples[n])[:, -1].reshape(C, -1)
+                     for n in winfo.layout.names], axis=1)
+        else:
+            final_warmup = initial_params
+        # sampling phase (mcmc.py:167-178)
+        if verbose:
+            print(f"Sampling phase: {num_samples} samples")
+        samples, self.acceptance_rate, self.info = sampler(
+            self.log_prob_fn, final_warmup, num_samples=num_samples,
+            proposal_scale=proposal_scale,
+            random_seed=random_seed + 1 if num_warmup > 0 else random_seed,
+            verbose=verbose, **kwargs)
+        if verbose:
+            print(f"Sampling acceptance rate: {float(np.mean(self.acceptance_rate)):.2%}")
+            print(f"\n{'=' * 70}")
+            print("Sampling complete!")
+            print(f"{'=' * 70}\n")
+        self.samples = {k: np.array(v) for k, v in samples.items()}
+        return self.samples
 
     def summary(self, credible_interval=0.95):
         """Per parameter: mean, std, median and the central credible interval

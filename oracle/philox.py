@@ -27,6 +27,7 @@ TAG_ACCEPT = 2
 TAG_SLICE = 3
 TAG_DEPTH = 4
 TAG_MERGE = 5
+TAG_PROPOSAL = 6
 TAG_USER = 16
 
 
@@ -93,6 +94,13 @@ def momentum(seed, chain, it, D):
     """float32 [D]: element j from block j // 4, word j % 4."""
     blocks = (D + 3) // 4
     w = draw(seed, chain, it, TAG_MOMENTUM, 0, np.arange(blocks))
+    return normals4(w).reshape(-1)[:D]
+
+
+def proposal_noise(seed, chain, it, D):
+    """float32 [D] Metropolis-Hastings random-walk normals (same mapping as momentum)."""
+    blocks = (D + 3) // 4
+    w = draw(seed, chain, it, TAG_PROPOSAL, 0, np.arange(blocks))
     return normals4(w).reshape(-1)[:D]
 
 

@@ -8,6 +8,11 @@ CPU restatement of the reference samplers, float32 throughout as MLX is:
           H_init) (hmc.py:139-153), cumulative-rate x0.95 / x1.05 warmup rule
           for i > 10 (hmc.py:159-170), counters reset after warmup
           (hmc.py:178-180), ZeroDivisionError at num_warmup = 0 (hmc.py:175).
+  metropolis_hastings()  restates mlx_mcmc/kernels/metropolis.py:6-101 —
+          q' = q + f32(z * f32(scale)) (:73-74), ratio = f32(lp' - lp)
+          (:77-78), accept iff f32 log U < ratio (:81-88, NaN rejects), the
+          current point stored every iteration (:90-92), rate over all
+          iterations (:99, ZeroDivisionError at num_samples = 0).
   nuts()  restates mlx_mcmc/kernels/nuts.py:16-358 — the recursive
           build_tree (nuts.py:137-218) verbatim, Python min/max semantics
           (NaN alpha counts as 1, nuts.py:173), f32 slice variable
@@ -172,6 +177,39 @@ def hmc(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_siz
     accept_rate = n_accept / n_total
     return OracleRun(np.array(samples, np.float32).reshape(num_samples, M.D), accept_rate,
                      warmup_accept_rate, epsilon, trace, n_grad)
+
+
+# ---------------------------------------------------------------------------
+# Metropolis-Hastings
+# ---------------------------------------------------------------------------
+def metropolis_hastings(log_prob_fn, initial_params, num_samples=1000, proposal_scale=0.1,
+                        random_seed=0, chain=0, record=True) -> OracleRun:
+    M = EagerModel(log_prob_fn, initial_params)
+    q = M.flatten(initial_params)
+    lp = M.logp(q)
+    scale = F32(proposal_scale)
+    trace = {"accepted": [], "ratio": [], "logp": []}
+    samples = []
+    n_accepted = 0
+    for i in range(num_samples):
+        z = R.proposal_noise(random_seed, chain, i, M.D)
+        qp = (q + (z * scale).astype(np.float32)).astype(np.float32)
+        lpp = M.logp(qp)
+        with np.errstate(invalid="ignore", over="ignore"):
+            ratio = F32(lpp - lp)
+        log_u = R.logf_ref(R.uniform(random_seed, chain, i, R.TAG_ACCEPT))
+        accepted = bool(log_u < ratio)
+        if accepted:
+            q, lp = qp, lpp
+            n_accepted += 1
+        samples.append(q.copy())
+        if record:
+            trace["accepted"].append(accepted)
+            trace["ratio"].append(float(ratio))
+            trace["logp"].append(float(lp))
+    rate = n_accepted / num_samples  # ZeroDivisionError at num_samples = 0 (:99)
+    return OracleRun(np.array(samples, np.float32).reshape(num_samples, M.D), rate, float("nan"),
+                     float(proposal_scale), trace, 0)
 
 
 # ---------------------------------------------------------------------------

@@ -358,3 +358,33 @@ def test_quantiles_from_order_stats_match_numpy(n, ci):
     assert float(med) == float(np.median(x))
     assert float(lo) == float(np.percentile(x, lo_p))
     assert float(hi) == float(np.percentile(x, hi_p))
+
+
+# ---- Metropolis-Hastings (metropolis.py:6-101) -------------------
+def test_mh_oracle_example01_posterior():
+    """examples/01_simple_normal.py's model and MH settings (proposal 0.3):
+    the posterior concentrates on the sample mean / std of the data."""
+    import workloads as W
+
+    lp, init = W.simple_normal(W.ns_oracle())
+    data = W.simple_normal_data()
+    r = S.metropolis_hastings(lp, init, num_samples=4000, proposal_scale=0.3, random_seed=42)
+    mu, sigma = r.samples[1000:, 0], r.samples[1000:, 1]
+    assert abs(mu.mean() - data.mean()) < 0.15 and abs(sigma.mean() - data.std()) < 0.15
+    assert 0.1 < r.accept_rate < 0.9
+    assert r.samples.dtype == np.float32
+    # the stored point changes exactly on the accepted iterations
+    moved = np.any(np.diff(r.samples, axis=0) != 0, axis=1)
+    assert list(moved) == r.trace["accepted"][1:]
+
+
+def test_mh_oracle_rules():
+    # NaN / -inf ratios reject (metropolis.py:84: float(log_u) < float(nan) is False)
+    r = S.metropolis_hastings(lambda p: _std_normal(p) * float("nan"), {"x": 0.0},
+                              num_samples=20, random_seed=0)
+    assert r.accept_rate == 0.0 and np.all(r.samples == 0)
+    r = S.metropolis_hastings(lambda p: ns.HalfNormal(1.0).log_prob(p["s"]), {"s": 0.01},
+                              num_samples=500, proposal_scale=1.0, random_seed=2)
+    assert np.all(r.samples > 0) and 0 < r.accept_rate < 1
+    with pytest.raises(ZeroDivisionError):
+        S.metropolis_hastings(_std_normal, {"x": 0.0}, num_samples=0)

@@ -107,7 +107,13 @@ def test_mcmc_method_errors():
     mc = m.MCMC(lambda p: m.Normal(0, 1).log_prob(p["x"]))
     with pytest.raises(ValueError):
         mc.run({"x": 0.0}, method="gibbs")
-    with pytest.raises(NotImplementedError):
-        mc.run({"x": 0.0}, method="metropolis")
+    import torch
+
+    if not torch.cuda.is_available():
+        # no CPU fallback: the GPU sampler fails loudly without a device
+        from mlx_mcmc_amd import _lib
+
+        with pytest.raises(_lib.EngineUnavailable):
+            mc.run({"x": 0.0}, method="metropolis", verbose=False)
     with pytest.raises(ValueError):
         mc.summary()
