@@ -41,8 +41,8 @@ def _ensure_pkg():
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=1000)   # S = 1000
+    ap.add_argument("--warmup", type=int, default=500)   #   and W = 500
     ap.add_argument("--shape", default="large", choices=["small", "medium", "large"])
     ap.add_argument("--chains", type=int, default=256, help="chains per GPU")
     ap.add_argument("--leapfrog", type=int, default=20)
@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=15,
                     help="processes of the aggregate CPU baseline (0: skip)")
     ap.add_argument("--no-ess", action="store_true")
+    ap.add_argument("--slice-kernel", default="auto", choices=["auto", "interpreter", "lanes"],
+                    help="kernel of the sliced program (csrc/lanes.h or csrc/sliced.h)")
     ap.add_argument("--gather", action="store_true",
                     help="also gather every rank's samples to rank 0 over RCCL (untimed)")
     return ap.parse_args()
@@ -128,6 +130,16 @@ def cpu_aggregate(G, N, L, step_size, budget_s, nproc):
     return float(sum(vals))
 
 
+def kernel_label(prog, C):
+    """The sampler kernel a launch runs (rocprof names it the same way)."""
+    kind = prog.slice_kernel
+    if kind == "lanes":
+        return f"k_hmc_lr (S={prog.num_slices} slices, lane-resident)"
+    if kind == "interpreter":
+        return f"k_hmc_sl<{16 if C > 8 else 8}> (S={prog.num_slices} slices)"
+    return f"k_hmc<{prog.waves_per_chain}>"
+
+
 def main():
     args = parse()
     import numpy as np
@@ -154,7 +166,7 @@ def main():
     K = args.steps
     Wm = args.warmup
     lp_fn, init = W.hierarchical(W.ns_product(), G, N)
-    prog = _trace.compile_model(lp_fn, init)
+    prog = _trace.compile_model(lp_fn, init, slice_kernel=args.slice_kernel)
     chains = _engine.ChainSet(prog, C, prog.layout.flatten(init), args.step_size, device=dev)
     samples = torch.empty((C, max(K, 1), D), dtype=torch.float32, device=dev)
     chain_offset, _ = shard(C * world, world, rank)   # weak scaling: C chains per GPU
@@ -246,8 +258,7 @@ def main():
             "roofline": {
                 "bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
-                "kernel": (f"k_hmc_sl<{16 if C > 8 else 8}> (S={prog.num_slices} slices)"
-                           if prog.num_slices > 1 else f"k_hmc<{prog.waves_per_chain}>"),
+                "kernel": kernel_label(prog, C),
                 "kernel_ms": kern_ms,
                 "flops_per_launch": flops_per_launch,
                 "note": ("fp32 VALU bound (SURVEY 8d; vector FP32 peak = f32-MFMA peak 157.3 TF); "

@@ -137,6 +137,17 @@ int32_t mc_program_waves_per_chain(const mc_program* prog);
  * chain-per-workgroup kernels.                                              */
 int mc_program_set_slices(mc_program* prog, int32_t num_slices);
 int32_t mc_program_num_slices(const mc_program* prog);
+/* Which kernel runs a sliced HMC program.  kernel: 0 = automatic (the
+ * lane-resident kernel when the layout qualifies: <= 16 slices, <= 4
+ * broadcast parameters, <= 256 private parameters per slice, every
+ * per-element parameter operand private; else the term interpreter),
+ * 1 = term interpreter, 2 = lane-resident (MC_ERR_UNSUPPORTED if the layout
+ * does not qualify; mc_last_error says why).  mc_program_slice_kernel returns
+ * the kernel a launch with L > 0 will use: 0 unsliced, 1 interpreter, 2
+ * lane-resident.  Both compute the same sampler; they differ in fp32
+ * summation order only.  mc_program_set_slices resets the choice's layout. */
+int mc_program_set_slice_kernel(mc_program* prog, int32_t kernel);
+int32_t mc_program_slice_kernel(const mc_program* prog);
 
 /* Batched tape evaluation: for every point p, logp[p] = log density at
  * q[p, :] and grad[p, :] = its gradient (replaces hmc.py:53-67 mx.grad).   */

@@ -485,6 +485,22 @@ class Program:
         _lib.check(lib.mc_program_set_slices(self.handle, int(num_slices)))
         self.num_slices = lib.mc_program_num_slices(self.handle)
 
+    SLICE_KERNELS = {"auto": 0, "interpreter": 1, "lanes": 2}
+
+    def set_slice_kernel(self, kernel: str) -> None:
+        """Kernel of a sliced HMC program (mc_program_set_slice_kernel):
+        "auto" (lane-resident when the layout qualifies), "interpreter"
+        (k_hmc_sl, csrc/sliced.h) or "lanes" (k_hmc_lr, csrc/lanes.h; raises
+        EngineError when the layout does not qualify)."""
+        _lib.check(_lib.load().mc_program_set_slice_kernel(self.handle,
+                                                           self.SLICE_KERNELS[kernel]))
+
+    @property
+    def slice_kernel(self) -> str:
+        """"unsliced", "interpreter" or "lanes": what an HMC launch will run."""
+        k = _lib.load().mc_program_slice_kernel(self.handle)
+        return {0: "unsliced", 1: "interpreter", 2: "lanes"}[k]
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and h.value:
@@ -495,9 +511,12 @@ class Program:
             self.handle = None
 
 
-def compile_model(log_prob_fn, initial_params: dict, slices: int = 0) -> Program:
+def compile_model(log_prob_fn, initial_params: dict, slices: int = 0,
+                  slice_kernel: str = "auto") -> Program:
     _lib.require_device()
     prog = Program(trace(log_prob_fn, initial_params))
     if slices:
         prog.set_slices(slices)
+    if slice_kernel != "auto":
+        prog.set_slice_kernel(slice_kernel)
     return prog

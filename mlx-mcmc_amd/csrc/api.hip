@@ -16,6 +16,7 @@
 #include "eval.h"
 #include "hmc.h"
 #include "internal.h"
+#include "lanes.h"
 #include "mh.h"
 #include "nuts.h"
 #include "philox.h"
@@ -65,6 +66,23 @@ struct SlicePlan {
     int32_t* d_gidx = nullptr;
 };
 
+// Host copy of the lane-resident layout (lanes.h) and its device tables.
+struct LanePlan {
+    int ok = 0;          // the sliced program qualifies
+    int rs = 1;          // register slots per lane (1, 2 or 4)
+    int sdata_floats = 0;
+    int32_t shl[kLrMaxShared] = {0, 0, 0, 0};  // shared parameters by ordinal
+    std::string why;     // why it does not qualify
+    std::vector<LrTerm> terms;
+    std::vector<float> data;
+    std::vector<int64_t> blocks;
+    std::vector<int32_t> gidx;
+    LrTerm* d_terms = nullptr;
+    float* d_data = nullptr;
+    int64_t* d_blocks = nullptr;
+    int32_t* d_gidx = nullptr;
+};
+
 struct mc_program {
     int32_t D = 0;
     float lp_const = 0.0f;
@@ -82,6 +100,8 @@ struct mc_program {
     std::vector<float> h_data;
     std::vector<int32_t> h_index;
     SlicePlan sl;
+    LanePlan lr;
+    int32_t slice_kernel = 0;  // 0 automatic, 1 term interpreter, 2 lane-resident
 };
 
 static DevCtx ctx_of(const mc_program* p) {
@@ -294,7 +314,18 @@ static int64_t pp_index(const DevTerm& t, int a, int64_t i, const std::vector<in
     return o.kind == MC_OP_PVEC ? (int64_t)o.poff + i : (int64_t)o.poff + ip[o.pool + i];
 }
 
-static int plan_slices(mc_program* p, int S, SlicePlan& P) {
+// The parameter / element partition plan_slices computes, kept for the
+// lane-resident planner (plan_lanes).
+struct SlPartition {
+    std::vector<int> ppr;                 // per term: slot of its per-element parameter, or -1
+    std::vector<char> shared, scalar;     // per parameter / per term
+    std::vector<int> jsh;                 // per parameter: shared ordinal, or -1
+    std::vector<std::vector<int>> priv;   // per slice: its private parameters
+    std::vector<int> shl;                 // shared parameters by ordinal
+    std::vector<std::vector<std::vector<int64_t>>> elems;  // [slice][term] element ids
+};
+
+static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = nullptr) {
     const std::vector<DevTerm>& raw = p->raw;
     const std::vector<float>& dp = p->h_data;
     const std::vector<int32_t>& ip = p->h_index;
@@ -431,6 +462,15 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P) {
             }
             elems[s][t].push_back(i);
         }
+    }
+    if (part) {
+        part->ppr = ppr;
+        part->shared = shared;
+        part->scalar = scalar;
+        part->jsh = jsh;
+        part->priv = priv;
+        part->shl = shl;
+        part->elems = elems;
     }
 
     struct Run {
@@ -662,6 +702,224 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P) {
     return MC_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// lane-resident layout planner (lanes.h)
+// ---------------------------------------------------------------------------
+static void free_lanes(LanePlan& L) {
+    if (L.d_terms) (void)hipFree(L.d_terms);
+    if (L.d_data) (void)hipFree(L.d_data);
+    if (L.d_blocks) (void)hipFree(L.d_blocks);
+    if (L.d_gidx) (void)hipFree(L.d_gidx);
+    L = LanePlan();
+}
+
+static LrCtx lrctx_of(const mc_program* p) {
+    LrCtx c;
+    std::memset(&c, 0, sizeof(c));
+    const LanePlan& L = p->lr;
+    const SlicePlan& P = p->sl;
+    c.terms = L.d_terms;
+    c.data = L.d_data;
+    c.blocks = L.d_blocks;
+    c.gidx = L.d_gidx;
+    c.sterms = P.d_sterms;
+    c.n_terms = (int32_t)p->raw.size();
+    c.n_sterms = (int32_t)P.sterms.size();
+    c.S = P.S;
+    c.Dsh = P.Dsh;
+    c.D = p->D;
+    c.nitems = P.nitems;
+    c.sdata_floats = L.sdata_floats;
+    c.lp_const = p->lp_const;
+    for (int k = 0; k < kLrMaxShared; ++k) c.shl[k] = L.shl[k];
+    return c;
+}
+
+// Deal every slice's private parameters to (lane, slot), longest first onto
+// the least loaded lane with a free slot, and tile each term's elements per
+// (slot, lane).  Returns MC_ERR_UNSUPPORTED (with L.why) when the program does
+// not qualify; the term interpreter (k_hmc_sl) then runs it.
+static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartition& part,
+                      LanePlan& L) {
+    const std::vector<DevTerm>& raw = p->raw;
+    const std::vector<float>& dp = p->h_data;
+    const std::vector<int32_t>& ip = p->h_index;
+    const int nT = (int)raw.size();
+    const int S = SP.S;
+    auto no = [&](const char* why) {
+        L.why = why;
+        return MC_ERR_UNSUPPORTED;
+    };
+    if (S > kLrSlices) return no("more than 16 slices");
+    if (SP.Dsh > kLrMaxShared) return no("more than 4 broadcast parameters");
+    int rs = 1;
+    for (int s = 0; s < S; ++s) {
+        const int need = ((int)part.priv[s].size() + 63) / 64;
+        if (need > kLrMaxSlots) return no("more than 256 private parameters in a slice");
+        rs = std::max(rs, need);
+    }
+    if (rs == 3) rs = 4;
+    for (int t = 0; t < nT; ++t) {
+        if (part.scalar[t] || part.ppr[t] < 0) continue;
+        for (int64_t i = 0; i < raw[t].n; ++i)
+            if (part.shared[pp_index(raw[t], part.ppr[t], i, ip)])
+                return no("a per-element operand reads a broadcast parameter");
+    }
+    L.rs = rs;
+    for (int k = 0; k < SP.Dsh; ++k) L.shl[k] = part.shl[k];
+    L.terms.assign((size_t)S * nT, LrTerm());
+    L.blocks.assign(4 * (size_t)S, 0);
+    L.gidx.assign((size_t)S * kLrMaxSlots * 64, -1);
+    L.sdata_floats = 0;
+    std::vector<int> lane_of(p->D, -1), slot_of_p(p->D, -1);
+    for (int s = 0; s < S; ++s) {
+        // ---- parameters -> (lane, slot) ----
+        const std::vector<int>& pv = part.priv[s];
+        std::vector<int64_t> cost(pv.size(), 0);
+        std::vector<int> lpos(p->D, -1);
+        for (size_t k = 0; k < pv.size(); ++k) lpos[pv[k]] = (int)k;
+        for (int t = 0; t < nT; ++t) {
+            if (part.scalar[t] || part.ppr[t] < 0) continue;
+            for (int64_t i : part.elems[s][t]) cost[lpos[pp_index(raw[t], part.ppr[t], i, ip)]]++;
+        }
+        std::vector<int> ord(pv.size());
+        std::iota(ord.begin(), ord.end(), 0);
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+        std::vector<int64_t> load(64, 0);
+        std::vector<int> used(64, 0);
+        for (int k : ord) {
+            int best = -1;
+            for (int l = 0; l < 64; ++l)
+                if (used[l] < rs && (best < 0 || load[l] < load[best])) best = l;
+            lane_of[pv[k]] = best;
+            slot_of_p[pv[k]] = used[best]++;
+            load[best] += cost[k];
+            L.gidx[((size_t)s * kLrMaxSlots + slot_of_p[pv[k]]) * 64 + best] = pv[k];
+        }
+        // ---- terms: the swept ones (lanes.h kLrSweep) first ----
+        while (L.data.size() % 4) L.data.push_back(0.0f);
+        const int64_t blk0 = (int64_t)L.data.size();
+        int nact = 0;
+        std::vector<LrTerm> swept, rest;
+        for (int t = 0; t < nT; ++t) {
+            if (part.scalar[t]) continue;
+            const DevTerm& rt = raw[t];
+            const std::vector<int64_t>& E = part.elems[s][t];
+            if (E.empty()) continue;
+            LrTerm lt;
+            std::memset(&lt, 0, sizeof(lt));
+            lt.dist = rt.dist;
+            lt.pp = part.ppr[t];
+            lt.weight = rt.weight;
+            lt.c0 = rt.c0;
+            lt.clg = rt.clg;
+            if (rt.op[2].kind == MC_OP_CONST) {
+                const float c = rt.op[2].cval;
+                lt.clogs = (float)std::log((double)c);
+                lt.cinv = 1.0f / c;
+                lt.cinv2 = 1.0f / (c * c);
+            }
+            for (int a = 0; a < 3; ++a) {
+                const DevOperand& o = rt.op[a];
+                lt.jsh[a] = 0;
+                switch (o.kind) {
+                    case MC_OP_CONST: lt.kind[a] = SK_CONST; lt.cval[a] = o.cval; break;
+                    case MC_OP_PSCALAR: lt.kind[a] = SK_SHARED; lt.jsh[a] = part.jsh[o.poff]; break;
+                    case MC_OP_DATA: lt.kind[a] = SK_DATA; break;
+                    case MC_OP_PVEC:
+                    case MC_OP_GATHER: lt.kind[a] = SK_PP; break;
+                    default: lt.kind[a] = SK_NONE; break;
+                }
+            }
+            lt.mode = (lt.kind[2] == SK_DATA || lt.kind[2] == SK_PP ||
+                       (rt.dist != MC_DIST_NORMAL && rt.dist != MC_DIST_HALFNORMAL)) ? 1 : 0;
+            lt.sig = LS_GENERIC;
+            if (rt.dist == MC_DIST_NORMAL && lt.mode == 0) {
+                const int a = lt.kind[0], b = lt.kind[1], c = lt.kind[2];
+                if (a == SK_DATA && b == SK_PP) lt.sig = c == SK_SHARED ? LS_DATA_PP_SH : LS_DATA_PP_C;
+                else if (a == SK_PP && b == SK_SHARED && c == SK_SHARED) lt.sig = LS_PP_SH_SH;
+                else if (a == SK_PP && b == SK_CONST && c == SK_CONST) lt.sig = LS_PP_C_C;
+                else if (a == SK_PP && b == SK_DATA && c == SK_SHARED) lt.sig = LS_PP_DATA_SH;
+                else if (a == SK_DATA && b == SK_SHARED && c == SK_SHARED) lt.sig = LS_DATA_SH_SH;
+            }
+            // element lists per (slot, lane), in element order
+            std::vector<std::vector<int64_t>> lists((size_t)kLrMaxSlots * 64);
+            int nslot = 1;
+            if (lt.pp >= 0) {
+                for (int64_t i : E) {
+                    const int64_t g = pp_index(rt, lt.pp, i, ip);
+                    const int r = slot_of_p[g];
+                    lists[(size_t)r * 64 + lane_of[g]].push_back(i);
+                    nslot = std::max(nslot, r + 1);
+                }
+            } else {  // chunk term: contiguous near-equal chunks over the lanes (slot 0)
+                const int64_t nE = (int64_t)E.size(), nch = std::min<int64_t>(64, nE);
+                int64_t f = 0;
+                for (int64_t c = 0; c < nch; ++c) {
+                    const int64_t len = nE / nch + (c < nE % nch ? 1 : 0);
+                    for (int64_t u = 0; u < len; ++u) lists[(size_t)c].push_back(E[f + u]);
+                    f += len;
+                }
+            }
+            lt.nslot = nslot;
+            int64_t tot = 0;
+            std::vector<int32_t> lens((size_t)nslot * 64, 0);
+            for (int r = 0; r < nslot; ++r) {
+                int64_t lmax = 0, lmin = INT64_MAX;
+                for (int l = 0; l < 64; ++l) {
+                    const int64_t n = (int64_t)lists[(size_t)r * 64 + l].size();
+                    if (n > INT32_MAX / 256) return no("a lane run is too long");
+                    lens[(size_t)r * 64 + l] = (int32_t)n;
+                    lmax = std::max(lmax, n);
+                    if (n > 0) lmin = std::min(lmin, n);
+                }
+                if (tot > INT32_MAX / 4) return no("slice data too large");
+                lt.toff[r] = (int32_t)tot;
+                lt.lmin4[r] = lmax > 0 ? (int32_t)(lmin / 4) : 0;
+                tot += 64 * ((lmax + 3) / 4 * 4);
+            }
+            for (int a = 0; a < 3; ++a) {
+                if (lt.kind[a] != SK_DATA) continue;
+                while (L.data.size() % 4) L.data.push_back(0.0f);
+                const int64_t base = (int64_t)L.data.size();
+                L.data.resize(base + tot, 0.0f);
+                const int64_t src = rt.op[a].pool;
+                for (int r = 0; r < nslot; ++r)
+                    for (int l = 0; l < 64; ++l) {
+                        const std::vector<int64_t>& li = lists[(size_t)r * 64 + l];
+                        for (size_t u = 0; u < li.size(); ++u)
+                            L.data[base + lt.toff[r] + (u >> 2) * 256 + 4 * l + (u & 3)] =
+                                dp[src + li[u]];
+                    }
+                lt.doff[a] = (int32_t)(base - blk0);
+            }
+            const int64_t lo = (int64_t)L.data.size();
+            L.data.resize(lo + lens.size());
+            std::memcpy(&L.data[lo], lens.data(), lens.size() * 4);
+            lt.len_off = (int32_t)(lo - blk0);
+            const bool sw = lt.sig == LS_DATA_PP_SH || lt.sig == LS_DATA_PP_C ||
+                            lt.sig == LS_PP_C_C || lt.sig == LS_PP_DATA_SH;
+            if (sw && (int)swept.size() < kLrSweep) swept.push_back(lt);
+            else rest.push_back(lt);
+        }
+        for (const LrTerm& lt : swept) L.terms[(size_t)s * nT + nact++] = lt;
+        for (const LrTerm& lt : rest) L.terms[(size_t)s * nT + nact++] = lt;
+        while (L.data.size() % 4) L.data.push_back(0.0f);
+        const int64_t blen = (int64_t)L.data.size() - blk0;
+        if (blen > INT32_MAX / 8) return no("slice data too large");
+        L.blocks[4 * s] = blk0;
+        L.blocks[4 * s + 1] = blen;
+        L.blocks[4 * s + 2] = nact;
+        L.blocks[4 * s + 3] = (int64_t)swept.size();
+        L.sdata_floats = std::max<int>(L.sdata_floats, (int)blen);
+    }
+    if ((int64_t)L.sdata_floats * 4 > kSlLdsBudget) return no("slice data exceed the LDS budget");
+    if (L.data.empty()) L.data.assign(4, 0.0f);
+    L.ok = 1;
+    return MC_OK;
+}
+
 template <typename T>
 static hipError_t upload(T** dst, const std::vector<T>& v) {
     hipError_t e = hipMalloc(dst, v.size() * sizeof(T));
@@ -683,9 +941,11 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
     const bool automatic = (S == 0);
     if (automatic) S = auto_slices(p);
     free_slices(p->sl);
+    free_lanes(p->lr);
     if (S <= 1) return MC_OK;
     SlicePlan P;
-    int rc = plan_slices(p, S, P);
+    SlPartition part;
+    int rc = plan_slices(p, S, P, &part);
     if (rc == MC_OK) {
         p->sl = P;  // host tables; geometry below needs them in place
         auto fit = [&]() {
@@ -713,7 +973,42 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
         return fail(e == hipErrorOutOfMemory ? MC_ERR_NOMEM : MC_ERR_HIP,
                     "slice upload failed: %s", hipGetErrorString(e));
     }
+    // the lane-resident layout of the same slices, when the program qualifies
+    LanePlan& LP = p->lr;
+    if (plan_lanes(p, Q, part, LP) == MC_OK) {
+        e = upload(&LP.d_terms, LP.terms);
+        if (e == hipSuccess) e = upload(&LP.d_data, LP.data);
+        if (e == hipSuccess) e = upload(&LP.d_blocks, LP.blocks);
+        if (e == hipSuccess) e = upload(&LP.d_gidx, LP.gidx);
+        if (e != hipSuccess) {
+            free_lanes(LP);
+            free_slices(p->sl);
+            return fail(e == hipErrorOutOfMemory ? MC_ERR_NOMEM : MC_ERR_HIP,
+                        "slice upload failed: %s", hipGetErrorString(e));
+        }
+    } else {
+        const std::string why = LP.why;
+        free_lanes(LP);
+        LP.why = why;
+    }
     return MC_OK;
+}
+
+extern "C" int mc_program_set_slice_kernel(mc_program* p, int32_t kernel) {
+    if (!p) return fail(MC_ERR_INVALID, "program is NULL");
+    if (kernel < 0 || kernel > 2) return fail(MC_ERR_INVALID, "slice kernel must be 0, 1 or 2");
+    if (kernel == 2 && !p->lr.ok)
+        return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: %s",
+                    p->sl.S < 2 ? "program is not sliced" : p->lr.why.c_str());
+    p->slice_kernel = kernel;
+    return MC_OK;
+}
+
+extern "C" int32_t mc_program_slice_kernel(const mc_program* p) {
+    if (!p) return -1;
+    if (p->sl.S < 2) return 0;
+    if (p->slice_kernel == 1 || !p->lr.ok) return 1;
+    return 2;
 }
 
 extern "C" int32_t mc_program_num_slices(const mc_program* p) { return p ? p->sl.S : -1; }
@@ -1017,6 +1312,7 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
 extern "C" int mc_program_destroy(mc_program* p) {
     if (!p) return MC_OK;
     free_slices(p->sl);
+    free_lanes(p->lr);
     if (p->d_terms) (void)hipFree(p->d_terms);
     if (p->d_data) (void)hipFree(p->d_data);
     if (p->d_index) (void)hipFree(p->d_index);
@@ -1271,10 +1567,51 @@ static int64_t sl_groups_per_launch(const mc_program* p, int64_t C) {
     return std::min(groups, cap);
 }
 static constexpr int64_t kSlStatusBytes = 256;
+static int64_t lr_groups_per_launch(const mc_program* p, int64_t C) {
+    const int64_t groups = (C + kLrNB - 1) / kLrNB;
+    const int64_t cap = std::max<int64_t>(1, device_cus() / p->sl.S);
+    return std::min(groups, cap);
+}
 static int64_t sl_workspace_bytes(const mc_program* p, int64_t C) {
     const int nb = sl_nb_for(p, C);
-    return kSlStatusBytes +
-           2 * sl_groups_per_launch(p, C) * p->sl.S * (int64_t)p->sl.nitems * nb * 8;
+    int64_t x = 2 * sl_groups_per_launch(p, C) * p->sl.S * (int64_t)p->sl.nitems * nb * 8;
+    if (p->lr.ok)  // either kernel may run on the same workspace (lanes.h: one
+                   // 128-byte line per (wave, slice) record)
+        x = std::max(x, 2 * lr_groups_per_launch(p, C) * (kLrNB / 2) * p->sl.S * 128);
+    return kSlStatusBytes + x;
+}
+static bool use_lanes(const mc_program* p, const mc_run_config* cfg) {
+    return p->lr.ok && p->slice_kernel != 1 && cfg->num_leapfrog_steps > 0;
+}
+
+template <int RS, int NSH>
+static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* state,
+                         float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
+    int64_t qo, go;
+    mc_state_offsets(p, cfg->num_chains, &qo, &go);
+    char* b = (char*)state;
+    RunArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.cfg = *cfg;
+    const LrCtx ctx = lrctx_of(p);
+    const size_t lds = (size_t)p->lr.sdata_floats * 4;
+    MC_HIP_TRY(allow_lds(k_hmc_lr<RS, NSH>, lds));
+    const int64_t C = cfg->num_chains;
+    const int64_t groups = (C + kLrNB - 1) / kLrNB;
+    const int64_t gpl = lr_groups_per_launch(p, C);
+    const int64_t used = sl_workspace_bytes(p, C);
+    int* status = (int*)ws;
+    unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
+    for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
+        const int64_t ng = std::min(gpl, groups - g0);
+        MC_HIP_TRY(hipMemsetAsync(g0 == 0 ? ws : (void*)xch, 0,
+                                  g0 == 0 ? used : used - kSlStatusBytes, st));
+        hipLaunchKernelGGL((k_hmc_lr<RS, NSH>), dim3((unsigned)(ng * p->sl.S)), dim3(512), lds, st, ctx,
+                           A, g0 * kLrNB, ng, (mc_chain_scalars*)b, (float*)(b + qo),
+                           (float*)(b + go), samples, trace_of(tr), xch, status);
+        MC_HIP_TRY(hipGetLastError());
+    }
+    return MC_OK;
 }
 
 template <int NB>
@@ -1361,6 +1698,18 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
         if (ws == nullptr || ws_bytes < need)
             return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
         if (device_cus() <= 0) return fail(MC_ERR_HIP, "no HIP device");
+        if (use_lanes(p, cfg)) {
+            hipStream_t st = (hipStream_t)stream;
+            const bool n4 = p->sl.Dsh > 3;
+            switch (p->lr.rs) {
+                case 1: return n4 ? launch_hmc_lr<1, 4>(p, cfg, state, samples, tr, ws, st)
+                                  : launch_hmc_lr<1, 3>(p, cfg, state, samples, tr, ws, st);
+                case 2: return n4 ? launch_hmc_lr<2, 4>(p, cfg, state, samples, tr, ws, st)
+                                  : launch_hmc_lr<2, 3>(p, cfg, state, samples, tr, ws, st);
+                default: return n4 ? launch_hmc_lr<4, 4>(p, cfg, state, samples, tr, ws, st)
+                                   : launch_hmc_lr<4, 3>(p, cfg, state, samples, tr, ws, st);
+            }
+        }
         return sl_nb_for(p, cfg->num_chains) == 16
                    ? launch_hmc_sl<16>(p, cfg, state, samples, tr, ws, (hipStream_t)stream)
                    : launch_hmc_sl<8>(p, cfg, state, samples, tr, ws, (hipStream_t)stream);

@@ -1,0 +1,1000 @@
+// lanes.h — lane-resident sliced HMC: the work split of k_hmc_sl (sliced.h;
+// reference hmc.py:7-206 per chain), with every chain's state in registers.
+//
+//   * A workgroup evaluates one data slice for a block of 16 chains; wave w
+//     owns chains 2w and 2w+1 and runs their whole trajectory on its own: no
+//     workgroup barrier inside the iteration loop.
+//   * Each private parameter of the slice (theta_g with its groups'
+//     observations) is dealt to one (lane, slot): lane j keeps q, p, grad of
+//     its <= RS private parameters for both chains in VGPRs, and every term's
+//     elements of that parameter are tiled so that lane j streams them
+//     (element u of (slot r, lane j) at toff[r] + (u/4)*256 + 4j + u%4 of the
+//     operand's region of the slice block, in LDS).  The gradient of a private
+//     parameter is complete inside the lane.
+//   * The broadcast ("shared") parameters (mu, tau, sigma) are replicated in
+//     every lane of every slice: q, p, grad and their derived scale values
+//     (1/x, 1/x^2, log x) are registers too.
+//   * Per element both chains are advanced with packed FP32 (v_pk_add_f32 /
+//     v_pk_fma_f32): d = x - theta, s1 += d, s2 = fma(d, d, s2) — three
+//     instructions per element for two chains.
+//   * Once per leapfrog step each wave publishes its two chains' records (log
+//     p partial, shared-cotangent partials, kinetic partials) as tagged 8-byte
+//     granules and polls the 16 slices' records of the same two chains; a
+//     16-lane DPP row sums each item in a fixed tree (identical in every
+//     slice), so all replicas of a shared parameter stay bit-identical and
+//     every slice takes the same accept decision.  The scalar terms (priors of
+//     the shared parameters) are then added in term order.
+// Eligibility (host planner, api.hip plan_lanes): S <= 16, <= kLrMaxShared
+// shared parameters, <= 64 * kLrMaxSlots private parameters per slice, and
+// every per-element parameter operand private.  Results equal k_hmc_sl's up
+// to fp32 summation order; runs are bit-reproducible and independent of how
+// chains are split over launches or GPUs.
+#pragma once
+#include "sliced.h"
+
+namespace mc {
+
+constexpr int kLrMaxSlots = 4;   // private parameters per lane
+constexpr int kLrMaxShared = 4;  // broadcast parameters
+constexpr int kLrNB = 16;        // chains per block: 8 waves x 2 chains
+constexpr int kLrSlices = 16;    // max slices (one 16-lane DPP row per item)
+
+// One term restricted to one slice.
+struct LrTerm {
+    int32_t dist;
+    int32_t mode;     // 0: broadcast scale (moment sums), 1: per-element formula
+    int32_t pp;       // operand slot of the per-element parameter, or -1 (chunk term)
+    int32_t nslot;    // slots with elements (chunk term: 1)
+    float weight, c0;
+    float clogs, cinv, cinv2;  // CONST scale: f32 log(scale), 1/scale, 1/scale^2
+    float clg;                 // Gamma / Beta with constant shapes: gammaln normaliser
+    int32_t kind[3];  // SK_* of value, loc, scale
+    int32_t jsh[3];   // SK_SHARED: shared ordinal
+    int32_t doff[3];  // SK_DATA: float offset of the operand's tiled region (slice block)
+    float cval[3];    // SK_CONST
+    int32_t toff[kLrMaxSlots];   // per slot: tile offset inside an operand region
+    int32_t lmin4[kLrMaxSlots];  // per slot: min (over lanes with elements) length / 4
+    int32_t len_off;             // int32 [nslot][64] run lengths (slice block)
+    int32_t sig;                 // LS_*: a specialised form, or LS_GENERIC
+};
+
+// Specialised term forms (Normal, broadcast scale, moment sums) with their
+// operand kinds fixed at compile time: (value, loc, scale).
+enum : int32_t {
+    LS_GENERIC = 0,
+    LS_DATA_PP_SH = 1,   // y ~ Normal(theta[g], sigma)        grouped likelihood
+    LS_DATA_PP_C = 2,    // y ~ Normal(theta[g], const)
+    LS_PP_SH_SH = 3,     // theta ~ Normal(mu, tau)            hierarchical prior
+    LS_PP_C_C = 4,       // theta ~ Normal(const, const)
+    LS_PP_DATA_SH = 5,   // theta ~ Normal(m_data, tau)
+    LS_DATA_SH_SH = 6,   // y ~ Normal(mu, sigma)              chunked likelihood
+};
+
+struct LrCtx {
+    const LrTerm* terms;    // [S][n_terms], the slice's active terms first
+    const float* data;      // slice blocks
+    const int64_t* blocks;  // per slice {data offset, floats, active terms, swept terms}
+    const int32_t* gidx;    // [S][kLrMaxSlots][64]: global parameter of (slot, lane), -1
+    const SlTerm* sterms;   // scalar terms (constants / shared parameters only)
+    int32_t n_terms;
+    int32_t n_sterms;
+    int32_t S;
+    int32_t Dsh;
+    int32_t D;
+    int32_t nitems;         // record per chain: lp, Dsh cotangents, K0, K1
+    int32_t sdata_floats;
+    float lp_const;
+    int32_t shl[kLrMaxShared];  // global index of shared parameter k
+};
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+MC_DEV f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// Wave-uniform read of lane `lane`'s value (lane is uniform).
+MC_DEV float rl(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+// A [kLrMaxShared] register array indexed by a per-lane or uniform ordinal.
+MC_DEV float pick4(const float (&a)[kLrMaxShared], int k) {
+    float v = a[0];
+#pragma unroll
+    for (int kk = 1; kk < kLrMaxShared; ++kk) v = (k == kk) ? a[kk] : v;
+    return v;
+}
+MC_DEV void add4(float (&a)[kLrMaxShared][2], int k, int c, float x) {
+#pragma unroll
+    for (int kk = 0; kk < kLrMaxShared; ++kk)
+        if (k == kk) a[kk][c] += x;
+}
+
+// Moment sums of one lane's run for both chains (packed): DC bit 0 value is
+// data, bit 1 loc is data; vv / mm the chains' non-data operand values.
+template <int DC>
+MC_DEV void lr_moments(const float* xv, const float* xm, int len, int lmin4, f2 vv, f2 mm,
+                       f2& s1, f2& s2) {
+    f2 a1 = {0.0f, 0.0f}, a2 = {0.0f, 0.0f};
+    auto elem = [&](float x, float y) {
+        f2 d;
+        if (DC == 0) d = vv - mm;
+        else if (DC == 1) d = (f2){x, x} - mm;
+        else if (DC == 2) d = vv - (f2){y, y};
+        else { const float t = x - y; d = (f2){t, t}; }
+        a1 += d;
+        a2 = pk_fma(d, d, a2);
+    };
+    int u4 = 0;
+    for (; u4 + 4 <= lmin4; u4 += 4) {
+        float4 a[4], c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            a[q] = c[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (DC & 1) a[q] = *(const float4*)(xv + (u4 + q) * 256);
+            if (DC & 2) c[q] = *(const float4*)(xm + (u4 + q) * 256);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            elem(a[q].x, c[q].x);
+            elem(a[q].y, c[q].y);
+            elem(a[q].z, c[q].z);
+            elem(a[q].w, c[q].w);
+        }
+    }
+    for (; u4 < lmin4; ++u4) {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
+        if (DC & 1) a = *(const float4*)(xv + u4 * 256);
+        if (DC & 2) c = *(const float4*)(xm + u4 * 256);
+        elem(a.x, c.x);
+        elem(a.y, c.y);
+        elem(a.z, c.z);
+        elem(a.w, c.w);
+    }
+    for (int u = 4 * u4; u < len; ++u) {
+        const int o = (u >> 2) * 256 + (u & 3);
+        elem((DC & 1) ? xv[o] : 0.0f, (DC & 2) ? xm[o] : 0.0f);
+    }
+    s1 += a1;
+    s2 += a2;
+}
+
+// Private parameters of the lane's slots, both chains.
+template <int RS>
+struct LrPriv {
+    float q[RS][2], p[RS][2], g[RS][2];
+};
+
+// Shared parameters, distributed over the lanes: lane x < 2 Dsh holds
+// parameter k = x / 2 of chain c = x % 2 (the other lanes hold inert values:
+// q = 1, p = g = 0).  Uniform reads go through readlane.
+struct LrShared {
+    float q, p, g;
+    float is, iv, lg;  // 1/q, 1/q^2, f32 log q: the derived scale values
+};
+
+// One Normal term with a broadcast scale and compile-time operand kinds
+// (value, loc, scale) = (K0, K1, K2): moment sums per lane, no per-term kind
+// branches.  Same arithmetic as the generic path's moment branch.
+template <int RS, int K0, int K1, int K2>
+MC_DEV void lr_normal_term(const MC_CONST LrTerm* T, const float* sd, int j, LrPriv<RS>& R,
+                           const LrShared& sh, float (&lpp)[2],
+                           float (&gshp)[kLrMaxShared][2]) {
+    constexpr int DC = (K0 == SK_DATA ? 1 : 0) | (K1 == SK_DATA ? 2 : 0);
+    constexpr int PPS = (K0 == SK_PP) ? 0 : ((K1 == SK_PP) ? 1 : -1);
+    const int nslot = T->nslot;
+    const float w = T->weight, c0 = T->c0;
+    const int j0 = T->jsh[0], j1 = T->jsh[1], j2 = T->jsh[2];
+    const int32_t* lens = (const int32_t*)sd + T->len_off;
+    float uv[2], um[2], is[2], iv[2], lg[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        uv[c] = (K0 == SK_SHARED) ? rl(sh.q, 2 * j0 + c) : (K0 == SK_CONST ? T->cval[0] : 0.0f);
+        um[c] = (K1 == SK_SHARED) ? rl(sh.q, 2 * j1 + c) : (K1 == SK_CONST ? T->cval[1] : 0.0f);
+        is[c] = (K2 == SK_SHARED) ? rl(sh.is, 2 * j2 + c) : T->cinv;
+        iv[c] = (K2 == SK_SHARED) ? rl(sh.iv, 2 * j2 + c) : T->cinv2;
+        lg[c] = (K2 == SK_SHARED) ? rl(sh.lg, 2 * j2 + c) : T->clogs;
+    }
+    float pv[2] = {0.f, 0.f}, pm[2] = {0.f, 0.f}, ps[2] = {0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+        if (r >= nslot) break;
+        const int len = lens[r * 64 + j];
+        if (len <= 0) continue;
+        const int toff = T->toff[r] + 4 * j;
+        const float* x0 = sd + T->doff[0] + toff;
+        const float* x1 = sd + T->doff[1] + toff;
+        const f2 vv = (K0 == SK_PP) ? (f2){R.q[r][0], R.q[r][1]} : (f2){uv[0], uv[1]};
+        const f2 mm = (K1 == SK_PP) ? (f2){R.q[r][0], R.q[r][1]} : (f2){um[0], um[1]};
+        f2 s1 = {0.f, 0.f}, s2 = {0.f, 0.f};
+        lr_moments<DC>(x0, x1, len, T->lmin4[r], vv, mm, s1, s2);
+        const float cnt = (float)len;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const float lpt = cnt * (c0 - lg[c]) - (0.5f * s2[c]) * iv[c];
+            lpp[c] += w * lpt;
+            const float t = w * (s1[c] * iv[c]);
+            if (PPS == 0) R.g[r][c] += -t;
+            if (PPS == 1) R.g[r][c] += t;
+            pv[c] += -t;
+            pm[c] += t;
+            ps[c] += w * ((s2[c] * iv[c] - cnt) * is[c]);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        if (K0 == SK_SHARED) add4(gshp, j0, c, pv[c]);
+        if (K1 == SK_SHARED) add4(gshp, j1, c, pm[c]);
+        if (K2 == SK_SHARED) add4(gshp, j2, c, ps[c]);
+    }
+}
+
+// ---- sweep-ahead terms ------------------------------------------------------
+// A "swept" term (Normal, broadcast scale, neither value nor loc a shared
+// parameter: y ~ N(theta_g, sigma), theta ~ N(m, sigma) ...) needs only the
+// private parameters for its moment sums; the shared scale enters only when
+// they are finished.  So the sums of step l + 1 are taken while the records
+// of step l travel, and finished once the shared parameters of step l + 1
+// are known.  Same arithmetic as lr_normal_term.
+constexpr int kLrSweep = 2;  // swept terms per slice (the planner puts them first)
+
+template <int RS>
+struct LrMoments {
+    f2 s1[kLrSweep][RS], s2[kLrSweep][RS];
+};
+
+template <int RS, int K0, int K1>
+MC_DEV void lr_sweep_term(const MC_CONST LrTerm* T, const float* sd, int j, const LrPriv<RS>& R,
+                          f2 (&s1)[RS], f2 (&s2)[RS]) {
+    constexpr int DC = (K0 == SK_DATA ? 1 : 0) | (K1 == SK_DATA ? 2 : 0);
+    const int nslot = T->nslot;
+    const int32_t* lens = (const int32_t*)sd + T->len_off;
+    const f2 cv = {K0 == SK_CONST ? T->cval[0] : T->cval[1], K0 == SK_CONST ? T->cval[0] : T->cval[1]};
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+        s1[r] = (f2){0.f, 0.f};
+        s2[r] = (f2){0.f, 0.f};
+        if (r >= nslot) continue;
+        const int len = lens[r * 64 + j];
+        if (len <= 0) continue;
+        const int toff = T->toff[r] + 4 * j;
+        const f2 th = {R.q[r][0], R.q[r][1]};
+        const f2 vv = (K0 == SK_PP) ? th : cv;
+        const f2 mm = (K1 == SK_PP) ? th : cv;
+        lr_moments<DC>(sd + T->doff[0] + toff, sd + T->doff[1] + toff, len, T->lmin4[r], vv, mm,
+                       s1[r], s2[r]);
+    }
+}
+
+template <int RS>
+MC_DEV void lr_sweep(const MC_CONST LrTerm* tt, int nsweep, const float* sd, int j,
+                     const LrPriv<RS>& R, LrMoments<RS>& M) {
+#pragma unroll
+    for (int t = 0; t < kLrSweep; ++t) {
+        if (t >= nsweep) break;
+        const MC_CONST LrTerm* T = tt + t;
+        switch (T->sig) {
+            case LS_DATA_PP_SH:
+            case LS_DATA_PP_C: lr_sweep_term<RS, SK_DATA, SK_PP>(T, sd, j, R, M.s1[t], M.s2[t]); break;
+            case LS_PP_DATA_SH: lr_sweep_term<RS, SK_PP, SK_DATA>(T, sd, j, R, M.s1[t], M.s2[t]); break;
+            default: lr_sweep_term<RS, SK_PP, SK_CONST>(T, sd, j, R, M.s1[t], M.s2[t]); break;
+        }
+    }
+}
+
+// Finish the swept terms from their moment sums at the current shared values.
+template <int RS>
+MC_DEV void lr_finish_swept(const MC_CONST LrTerm* tt, int nsweep, const float* sd, int j,
+                            LrPriv<RS>& R, const LrShared& sh, const LrMoments<RS>& M,
+                            float (&lpp)[2], float (&gshp)[kLrMaxShared][2]) {
+#pragma unroll
+    for (int t = 0; t < kLrSweep; ++t) {
+        if (t >= nsweep) break;
+        const MC_CONST LrTerm* T = tt + t;
+        const int nslot = T->nslot, pp = T->pp, j2 = T->jsh[2];
+        const bool shs = T->kind[2] == SK_SHARED;
+        const float w = T->weight, c0 = T->c0;
+        const int32_t* lens = (const int32_t*)sd + T->len_off;
+        float is[2], iv[2], lg[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            is[c] = shs ? rl(sh.is, 2 * j2 + c) : T->cinv;
+            iv[c] = shs ? rl(sh.iv, 2 * j2 + c) : T->cinv2;
+            lg[c] = shs ? rl(sh.lg, 2 * j2 + c) : T->clogs;
+        }
+        float ps[2] = {0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            if (r >= nslot) break;
+            const int len = lens[r * 64 + j];
+            if (len <= 0) continue;
+            const float cnt = (float)len;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const float s1 = M.s1[t][r][c], s2 = M.s2[t][r][c];
+                const float lpt = cnt * (c0 - lg[c]) - (0.5f * s2) * iv[c];
+                lpp[c] += w * lpt;
+                const float u = w * (s1 * iv[c]);
+                R.g[r][c] += (pp == 0) ? -u : u;
+                ps[c] += w * ((s2 * iv[c] - cnt) * is[c]);
+            }
+        }
+        if (shs) {
+            add4(gshp, j2, 0, ps[0]);
+            add4(gshp, j2, 1, ps[1]);
+        }
+    }
+}
+
+// Log p partial of this slice at the current point; private gradients
+// (complete) into R.g, this lane's shared-cotangent partials into gshp.
+template <int RS>
+MC_DEV void lr_eval(const MC_CONST LrTerm* tt, int t0, int nact, const float* sd, int j,
+                    LrPriv<RS>& R, const LrShared& sh, float (&lpp)[2],
+                    float (&gshp)[kLrMaxShared][2]) {
+    for (int t = t0; t < nact; ++t) {
+        const MC_CONST LrTerm* T = tt + t;
+        switch (T->sig) {
+            case LS_DATA_PP_SH:
+                lr_normal_term<RS, SK_DATA, SK_PP, SK_SHARED>(T, sd, j, R, sh, lpp, gshp);
+                continue;
+            case LS_DATA_PP_C:
+                lr_normal_term<RS, SK_DATA, SK_PP, SK_CONST>(T, sd, j, R, sh, lpp, gshp);
+                continue;
+            case LS_PP_SH_SH:
+                lr_normal_term<RS, SK_PP, SK_SHARED, SK_SHARED>(T, sd, j, R, sh, lpp, gshp);
+                continue;
+            case LS_PP_C_C:
+                lr_normal_term<RS, SK_PP, SK_CONST, SK_CONST>(T, sd, j, R, sh, lpp, gshp);
+                continue;
+            case LS_PP_DATA_SH:
+                lr_normal_term<RS, SK_PP, SK_DATA, SK_SHARED>(T, sd, j, R, sh, lpp, gshp);
+                continue;
+            case LS_DATA_SH_SH:
+                lr_normal_term<RS, SK_DATA, SK_SHARED, SK_SHARED>(T, sd, j, R, sh, lpp, gshp);
+                continue;
+            default:
+                break;
+        }
+        const int dist = T->dist, mode = T->mode, pp = T->pp, nslot = T->nslot;
+        const int k0 = T->kind[0], k1 = T->kind[1], k2 = T->kind[2];
+        const int j0 = T->jsh[0], j1 = T->jsh[1], j2 = T->jsh[2];
+        const float w = T->weight, c0 = T->c0;
+        const int32_t* lens = (const int32_t*)sd + T->len_off;
+        // the chains' broadcast operand values and derived scale values
+        float uv[2], um[2], us[2], is[2], iv[2], lg[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            uv[c] = k0 == SK_SHARED ? rl(sh.q, 2 * j0 + c) : (k0 == SK_CONST ? T->cval[0] : 0.f);
+            um[c] = k1 == SK_SHARED ? rl(sh.q, 2 * j1 + c) : (k1 == SK_CONST ? T->cval[1] : 0.f);
+            us[c] = k2 == SK_SHARED ? rl(sh.q, 2 * j2 + c) : (k2 == SK_CONST ? T->cval[2] : 0.f);
+            is[c] = k2 == SK_SHARED ? rl(sh.is, 2 * j2 + c) : T->cinv;
+            iv[c] = k2 == SK_SHARED ? rl(sh.iv, 2 * j2 + c) : T->cinv2;
+            lg[c] = k2 == SK_SHARED ? rl(sh.lg, 2 * j2 + c) : T->clogs;
+        }
+        float pv[2] = {0.f, 0.f}, pm[2] = {0.f, 0.f}, ps[2] = {0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            if (r >= nslot) break;
+            const int len = lens[r * 64 + j];
+            if (len <= 0) continue;
+            const int toff = T->toff[r] + 4 * j;
+            const float* x0 = sd + T->doff[0] + toff;
+            const float* x1 = sd + T->doff[1] + toff;
+            const float* x2 = sd + T->doff[2] + toff;
+            const float th[2] = {R.q[r][0], R.q[r][1]};
+            float rc[2] = {0.f, 0.f};
+            if (mode == 0) {
+                f2 s1 = {0.f, 0.f}, s2 = {0.f, 0.f};
+                float cnt[2];
+                bool neg[2] = {false, false};
+                if (dist == MC_DIST_NORMAL) {
+                    const f2 vv = {k0 == SK_PP ? th[0] : uv[0], k0 == SK_PP ? th[1] : uv[1]};
+                    const f2 mm = {k1 == SK_PP ? th[0] : um[0], k1 == SK_PP ? th[1] : um[1]};
+                    const int dc = (k0 == SK_DATA ? 1 : 0) | (k1 == SK_DATA ? 2 : 0);
+                    const int lmin4 = T->lmin4[r];
+                    if (dc == 1) lr_moments<1>(x0, x1, len, lmin4, vv, mm, s1, s2);
+                    else if (dc == 0) lr_moments<0>(x0, x1, len, lmin4, vv, mm, s1, s2);
+                    else if (dc == 2) lr_moments<2>(x0, x1, len, lmin4, vv, mm, s1, s2);
+                    else lr_moments<3>(x0, x1, len, lmin4, vv, mm, s1, s2);
+                    cnt[0] = cnt[1] = (float)len;
+                } else {
+                    // HalfNormal: moments of the value over value >= 0
+                    cnt[0] = cnt[1] = 0.0f;
+                    float a1[2] = {0.f, 0.f}, a2[2] = {0.f, 0.f};
+                    for (int u = 0; u < len; ++u) {
+                        const float x = (k0 == SK_DATA) ? x0[(u >> 2) * 256 + (u & 3)] : 0.0f;
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            const float d = (k0 == SK_DATA) ? x : (k0 == SK_PP ? th[c] : uv[c]);
+                            if (d >= 0.0f) {
+                                a1[c] += d;
+                                a2[c] = fmaf(d, d, a2[c]);
+                                cnt[c] += 1.0f;
+                            } else {
+                                neg[c] = true;
+                            }
+                        }
+                    }
+                    s1 = (f2){a1[0], a1[1]};
+                    s2 = (f2){a2[0], a2[1]};
+                }
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const float lpt = neg[c] ? -__builtin_inff()
+                                             : cnt[c] * (c0 - lg[c]) - (0.5f * s2[c]) * iv[c];
+                    lpp[c] += w * lpt;
+                    const float t = w * (s1[c] * iv[c]);
+                    rc[c] = (pp == 0) ? -t : t;
+                    pv[c] += -t;
+                    pm[c] += t;
+                    ps[c] += w * ((s2[c] * iv[c] - cnt[c]) * is[c]);
+                }
+            } else {
+                // per-element formula, one chain at a time
+                const bool lgv = (k1 == SK_DATA || k1 == SK_PP || k2 == SK_DATA || k2 == SK_PP);
+                for (int c = 0; c < 2; ++c) {
+                    const float thc = c ? th[1] : th[0];
+                    const float uvc = c ? uv[1] : uv[0], umc = c ? um[1] : um[0];
+                    const float usc = c ? us[1] : us[0];
+                    const float lsc = (k2 == SK_PP) ? logf(thc) : (c ? lg[1] : lg[0]);
+                    const float lgu = (k1 == SK_SHARED || k2 == SK_SHARED)
+                                          ? lgamma_norm(dist, umc, usc) : T->clg;
+                    float lpc = 0.f, rcc = 0.f, pvc = 0.f, pmc = 0.f, psc = 0.f;
+                    for (int u = 0; u < len; ++u) {
+                        const int o = (u >> 2) * 256 + (u & 3);
+                        const float v = (k0 == SK_DATA) ? x0[o] : (k0 == SK_PP ? thc : uvc);
+                        const float m = (k1 == SK_DATA) ? x1[o] : (k1 == SK_PP ? thc : umc);
+                        const float sc = (k2 == SK_DATA) ? x2[o] : (k2 == SK_PP ? thc : usc);
+                        const float ls = (k2 == SK_DATA) ? logf(sc) : lsc;
+                        const float lgx = lgv ? lgamma_norm(dist, m, sc) : lgu;
+                        const ElemOut e = elem_eval(dist, c0, v, m, sc, ls, lgx);
+                        lpc += w * e.lp;
+                        rcc += w * (pp == 0 ? e.dv : (pp == 1 ? e.dm : e.ds));
+                        pvc += w * e.dv;
+                        pmc += w * e.dm;
+                        psc += w * e.ds;
+                    }
+                    if (c) {
+                        lpp[1] += lpc; rc[1] = rcc; pv[1] += pvc; pm[1] += pmc; ps[1] += psc;
+                    } else {
+                        lpp[0] += lpc; rc[0] = rcc; pv[0] += pvc; pm[0] += pmc; ps[0] += psc;
+                    }
+                }
+            }
+            if (pp >= 0) {
+                R.g[r][0] += rc[0];
+                R.g[r][1] += rc[1];
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (k0 == SK_SHARED) add4(gshp, j0, c, pv[c]);
+            if (k1 == SK_SHARED) add4(gshp, j1, c, pm[c]);
+            if (k2 == SK_SHARED) add4(gshp, j2, c, ps[c]);
+        }
+    }
+}
+
+// The scalar terms (constants and shared parameters only), lane-parallel:
+// lane x evaluates term t0 + x / 2 for chain x % 2; the rows are then summed
+// over the terms in term order for each chain (uniform results in lp[c],
+// gs[k][c]).  Every slice computes the same sums and adds them to the
+// exchanged totals, so they run while the records travel.
+MC_DEV void lr_scalar_terms(const LrCtx& P, const LrShared& sh, int j, float (&lp)[2],
+                            float (&gs)[kLrMaxShared][2]) {
+    for (int t0 = 0; t0 < P.n_sterms; t0 += 32) {
+        const int t = t0 + (j >> 1), c = j & 1;
+        const bool on = t < P.n_sterms;
+        const SlTerm* T = P.sterms + (on ? t : 0);  // per-lane term: vector loads
+        const int k0 = T->kind[0], k1 = T->kind[1], k2 = T->kind[2];
+        // chain c's shared values live in lane 2 jsh + c (all lanes active here)
+        const float q0 = __shfl(sh.q, 2 * T->jsh[0] + c);
+        const float q1 = __shfl(sh.q, 2 * T->jsh[1] + c);
+        const float q2 = __shfl(sh.q, 2 * T->jsh[2] + c);
+        float lpx = 0.0f, gx[kLrMaxShared] = {0.f, 0.f, 0.f, 0.f};
+        if (on) {
+            const float v = k0 == SK_SHARED ? q0 : (k0 == SK_CONST ? T->cval[0] : 0.f);
+            const float m = k1 == SK_SHARED ? q1 : (k1 == SK_CONST ? T->cval[1] : 0.f);
+            const float sc = k2 == SK_SHARED ? q2 : (k2 == SK_CONST ? T->cval[2] : 0.f);
+            const float ls = (k2 == SK_CONST) ? T->clogs : logf(sc);
+            const float lgx =
+                (k1 == SK_SHARED || k2 == SK_SHARED) ? lgamma_norm(T->dist, m, sc) : T->clg;
+            const ElemOut e = elem_eval(T->dist, T->c0, v, m, sc, ls, lgx);
+            const float wn = T->weight * (float)T->niter;
+            lpx = wn * e.lp;
+#pragma unroll
+            for (int k = 0; k < kLrMaxShared; ++k) {
+                float y = 0.0f;
+                if (k0 == SK_SHARED && T->jsh[0] == k) y += wn * e.dv;
+                if (k1 == SK_SHARED && T->jsh[1] == k) y += wn * e.dm;
+                if (k2 == SK_SHARED && T->jsh[2] == k) y += wn * e.ds;
+                gx[k] = y;
+            }
+        }
+        const int nt = min(32, P.n_sterms - t0);
+        for (int u = 0; u < nt; ++u) {
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                lp[cc] += rl(lpx, 2 * u + cc);
+#pragma unroll
+                for (int k = 0; k < kLrMaxShared; ++k) gs[k][cc] += rl(gx[k], 2 * u + cc);
+            }
+        }
+    }
+}
+
+// Wave totals of 8 values at once (a fixed tree, the same in every wave):
+// v32/v16 swaps pair the values across lane halves / quarters, then one
+// 16-lane DPP row sum per register; the total of value i is read from the row
+// that holds it.
+MC_DEV void wave_sum8(const float (&v)[8], float (&out)[8]) {
+    float w[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {  // lanes 0-31: v[2m], lanes 32-63: v[2m+1]
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[2 * m]),
+                                                        __float_as_uint(v[2 * m + 1]), false, false);
+        w[m] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    float x[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {  // per 32-lane half: lanes 0-15 w[2n], 16-31 w[2n+1]
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[2 * n]),
+                                                        __float_as_uint(w[2 * n + 1]), false, false);
+        x[n] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        float t = x[n];
+        t += dpp_row<0xB1>(t);
+        t += dpp_row<0x4E>(t);
+        t += dpp_row<0x141>(t);
+        t += dpp_row<0x140>(t);
+        // rows: 0 -> v[4n], 1 -> v[4n+2], 2 -> v[4n+1], 3 -> v[4n+3]
+        out[4 * n + 0] = rl(t, 0);
+        out[4 * n + 2] = rl(t, 16);
+        out[4 * n + 1] = rl(t, 32);
+        out[4 * n + 3] = rl(t, 48);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the sampler
+// ---------------------------------------------------------------------------
+template <int RS, int NSH>
+__global__ void __launch_bounds__(512)
+k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scalars* scal,
+         float* st_q, float* st_g, float* samples, TraceDev tr, unsigned long long* xch,
+         int* status) {
+    constexpr int NB = kLrNB;
+    // record items: 0 lp, 1..NSH shared cotangents, NSH+1 K0, NSH+2 K1; pair
+    // 2 item + c (chain c) is granule `pair` of the wave's line
+    constexpr int NPAIR = 2 * (NSH + 3), NPASS = (NPAIR + 3) / 4;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const mc_run_config& cfg = A.cfg;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, j = tid & 63;
+    const int S = P.S, D = P.D, Dsh = P.Dsh;
+    int64_t grp;
+    int slice;
+    {
+        const int64_t w = blockIdx.x, nwg = gridDim.x;
+        if (nwg % 8 == 0 && (nwg / 8) % S == 0) {  // a block's slices share an XCD (speed only)
+            const int64_t x = w & 7, r = w >> 3;
+            grp = x * ((nwg / 8) / S) + r / S;
+            slice = (int)(r % S);
+        } else {
+            grp = w / S;
+            slice = (int)(w % S);
+        }
+    }
+    const int64_t C = cfg.num_chains;
+    const int64_t cbase = chain_base + grp * NB;
+    const int b0 = 2 * wave;
+    int64_t cc[2];  // this wave's chains (clamped for reads and draws)
+    bool live[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        live[c] = cbase + b0 + c < C;
+        cc[c] = min(cbase + b0 + c, C - 1);
+    }
+    // this lane's shared parameter (lanes < 2 Dsh): k = j / 2 of chain c = j % 2
+    const int xk = j >> 1, xc = j & 1;
+    const bool xon = j < 2 * Dsh;
+    int xg = P.shl[0];
+#pragma unroll
+    for (int k = 1; k < kLrMaxShared; ++k) xg = (xk == k) ? P.shl[k] : xg;
+    const int64_t xch_id = xc ? cc[1] : cc[0];
+    const bool xlive = xon && (xc ? live[1] : live[0]);
+
+    float* sd = smem;
+    const int64_t* blk = P.blocks + 4 * (int64_t)slice;
+    const int64_t doff = blk[0];
+    const int dlen = (int)blk[1];
+    const int nact = (int)blk[2];
+    const int nsweep = (int)blk[3];  // the first nsweep active terms are swept
+    for (int i = tid; 4 * i < dlen; i += 512)
+        *(float4*)(sd + 4 * i) = *(const float4*)(P.data + doff + 4 * i);
+
+    // ---- registers: private slots and the lane's shared parameter ----------------
+    LrPriv<RS> R;
+    int gk[RS];
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+        gk[r] = P.gidx[((int64_t)slice * kLrMaxSlots + r) * 64 + j];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            R.q[r][c] = gk[r] >= 0 ? st_q[cc[c] * D + gk[r]] : 0.0f;
+            R.g[r][c] = gk[r] >= 0 ? st_g[cc[c] * D + gk[r]] : 0.0f;
+            R.p[r][c] = 0.0f;
+        }
+    }
+    LrShared sh;
+    sh.q = xon ? st_q[xch_id * D + xg] : 1.0f;
+    sh.g = xon ? st_g[xch_id * D + xg] : 0.0f;
+    sh.p = 0.0f;
+    double eps[2];
+    float lp[2];
+    int nacc[2], ntot[2], wacc[2], wtot[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        eps[c] = scal[cc[c]].step_size;
+        lp[c] = scal[cc[c]].logp;
+        nacc[c] = scal[cc[c]].n_accept;
+        ntot[c] = scal[cc[c]].n_total;
+        wacc[c] = scal[cc[c]].warmup_accept;
+        wtot[c] = scal[cc[c]].warmup_total;
+    }
+    MC_STAMP_INIT
+    __syncthreads();  // the slice block is in LDS
+
+    const MC_CONST LrTerm* tt = cptr(P.terms) + (int64_t)slice * P.n_terms;
+    const int L = cfg.num_leapfrog_steps;
+    uint32_t epoch = 0;
+    bool ok = true;
+    // granules: one 128-byte line per (wave, slice) record, written by one
+    // store instruction of one wave (lane = pair), so a polled line is never
+    // rewritten by another wave while it is read.  Per lane: its own line
+    // (publish) and line j % 16 (poll), for both epoch parities.
+    unsigned long long* gpub[2];
+    unsigned long long* gpoll[2];
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+        unsigned long long* b = xch + (((int64_t)par * n_groups + grp) * (NB / 2) + wave) * S * 16;
+        gpub[par] = b + slice * 16 + j;
+        gpoll[par] = b + (j & 15) * 16 + (j >> 4);
+    }
+    const bool poll_lane = (j & 15) < S;
+    const int64_t it_end = cfg.iter_begin + cfg.iter_count;
+    for (int64_t it = cfg.iter_begin; it < it_end && ok; ++it) {
+        MC_STAMP_DECL
+        const bool warm = it < cfg.num_warmup;
+        float h[2], e[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (it == cfg.num_warmup) {  // hmc.py:175-180
+                wacc[c] = nacc[c];
+                wtot[c] = ntot[c];
+                nacc[c] = 0;
+                ntot[c] = 0;
+            }
+            h[c] = (float)(0.5 * eps[c]);
+            e[c] = (float)eps[c];
+        }
+        const float xh = xc ? h[1] : h[0], xe = xc ? e[1] : e[0];
+        // momentum: parameter g takes normal g % 4 of Philox block g / 4
+        auto normal_of = [&](int g, int64_t chain) {
+            const mc_u32x4 rr = mc_draw(cfg.seed, (uint32_t)(cfg.chain_offset + chain),
+                                        (uint32_t)it, MC_RNG_TAG_MOMENTUM, 0, (uint32_t)(g >> 2));
+            float z0, z1;
+            if ((g & 3) < 2) mc_box_muller(rr.x, rr.y, &z0, &z1);
+            else mc_box_muller(rr.z, rr.w, &z0, &z1);
+            return (g & 1) ? z1 : z0;
+        };
+        float k0p[2] = {0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            if (gk[r] < 0) continue;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const float z = normal_of(gk[r], cc[c]);
+                R.p[r][c] = z;
+                k0p[c] += z * z;
+            }
+        }
+        sh.p = xon ? normal_of(xg, xch_id) : 0.0f;
+        const float K0w[2] = {wave_sum(k0p[0]), wave_sum(k0p[1])};
+        float k0s[2] = {0.f, 0.f};  // the shared parameters' part, in parameter order
+        {
+            const float p2 = sh.p * sh.p;
+            for (int k = 0; k < Dsh; ++k) {
+                k0s[0] += rl(p2, 2 * k);
+                k0s[1] += rl(p2, 2 * k + 1);
+            }
+        }
+        // the start point, restored on rejection
+        float q0[RS][2], g0[RS][2];
+#pragma unroll
+        for (int r = 0; r < RS; ++r)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                q0[r][c] = R.q[r][c];
+                g0[r][c] = R.g[r][c];
+            }
+        const float q0s = sh.q, g0s = sh.g;
+        float lpn[2] = {lp[0], lp[1]}, K0[2] = {0.f, 0.f}, K1[2] = {0.f, 0.f};
+        MC_STAMP(5);
+        // kick + drift of step 0 (private and shared), then the swept terms'
+        // moment sums at the new point
+        auto drift_private = [&](bool second_half) {
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+#pragma unroll
+                for (int r = 0; r < RS; ++r) {
+                    float pj = R.p[r][c];
+                    if (second_half) pj = pj + h[c] * R.g[r][c];  // end of the previous step
+                    pj = pj + h[c] * R.g[r][c];
+                    R.p[r][c] = pj;
+                    R.q[r][c] = R.q[r][c] + e[c] * pj;
+                }
+            }
+        };
+        auto drift_shared = [&](bool second_half) {
+            float pj = sh.p;
+            if (second_half) pj = pj + xh * sh.g;
+            pj = pj + xh * sh.g;
+            sh.p = pj;
+            sh.q = sh.q + xe * pj;
+            sh.is = 1.0f / sh.q;
+            sh.iv = 1.0f / (sh.q * sh.q);
+            sh.lg = logf(sh.q);
+        };
+        LrMoments<RS> M;
+        drift_private(false);
+        drift_shared(false);
+        lr_sweep<RS>(tt, nsweep, sd, j, R, M);
+        for (int l = 0; l < L; ++l) {
+            MC_STAMP(0);
+            // step l at the point q(l+1): finish the swept terms (shared values
+            // of this step are known), evaluate the others
+            float lpp[2] = {0.f, 0.f};
+            float gshp[kLrMaxShared][2];
+#pragma unroll
+            for (int k = 0; k < kLrMaxShared; ++k) gshp[k][0] = gshp[k][1] = 0.0f;
+#pragma unroll
+            for (int r = 0; r < RS; ++r) R.g[r][0] = R.g[r][1] = 0.0f;
+            lr_finish_swept<RS>(tt, nsweep, sd, j, R, sh, M, lpp, gshp);
+            lr_eval<RS>(tt, nsweep, nact, sd, j, R, sh, lpp, gshp);
+            MC_STAMP(1);
+            // the wave totals of the record, pair-indexed (2 item + chain)
+            float rec[NPAIR];
+            {
+                float v8[8], t8[8];
+                v8[0] = lpp[0];
+                v8[1] = lpp[1];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    v8[2 + 2 * k] = gshp[k][0];
+                    v8[3 + 2 * k] = gshp[k][1];
+                }
+                wave_sum8(v8, t8);
+#pragma unroll
+                for (int x = 0; x < 8; ++x) rec[x] = t8[x];
+                // the 4th shared parameter and the final kinetic partial
+                float k1p[2] = {0.f, 0.f};
+                if (l == L - 1) {
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+#pragma unroll
+                        for (int r = 0; r < RS; ++r) {
+                            const float pj = R.p[r][c] + h[c] * R.g[r][c];
+                            k1p[c] += pj * pj;
+                        }
+                }
+                if (NSH > 3 || l == L - 1) {
+                    v8[0] = gshp[3][0];
+                    v8[1] = gshp[3][1];
+                    v8[2] = k1p[0];
+                    v8[3] = k1p[1];
+#pragma unroll
+                    for (int x = 4; x < 8; ++x) v8[x] = 0.0f;
+                    wave_sum8(v8, t8);
+                }
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    if (NSH > 3) rec[8 + c] = t8[c];
+                    rec[2 * (NSH + 1) + c] = (l == 0) ? K0w[c] : 0.0f;
+                    rec[2 * (NSH + 2) + c] = (l == L - 1) ? t8[2 + c] : 0.0f;
+                }
+            }
+            ++epoch;
+            const int par = epoch & 1;
+            // publish: lane x < NPAIR stores pair x
+            if (j < NPAIR) {
+                float v = rec[0];
+#pragma unroll
+                for (int x = 1; x < NPAIR; ++x) v = (j == x) ? rec[x] : v;
+                granule_store(par ? gpub[1] : gpub[0], epoch, v);
+            }
+            MC_STAMP(2);
+            // while the records travel: the private parameters' next position
+            // (their gradients are complete) and the swept terms' sums there,
+            // and the scalar terms of this step
+            if (l + 1 < L) {
+                drift_private(true);
+                lr_sweep<RS>(tt, nsweep, sd, j, R, M);
+            }
+            float slp[2] = {0.f, 0.f};
+            float sgs[kLrMaxShared][2];
+#pragma unroll
+            for (int k = 0; k < kLrMaxShared; ++k) sgs[k][0] = sgs[k][1] = 0.0f;
+            lr_scalar_terms(P, sh, j, slp, sgs);
+            MC_STAMP(7);
+            // poll: pass ps, lane x -> pair 4 ps + x / 16, slice x % 16
+            unsigned long long* gp = par ? gpoll[1] : gpoll[0];
+            float vals[NPASS];
+            uint32_t need = 0;
+#pragma unroll
+            for (int ps = 0; ps < NPASS; ++ps) {
+                vals[ps] = 0.0f;
+                if (poll_lane && 4 * ps + (j >> 4) < NPAIR) {
+                    const unsigned long long y = granule_load(gp + 4 * ps);
+                    if ((uint32_t)(y >> 32) == epoch) vals[ps] = __uint_as_float((uint32_t)y);
+                    else need |= 1u << ps;
+                }
+            }
+            uint32_t spins = 0;
+            while (__ballot(need != 0)) {
+                if (++spins > kSpinLimit) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                for (int ps = 0; ps < NPASS; ++ps) {
+                    if ((need >> ps) & 1u) {
+                        const unsigned long long y = granule_load(gp + 4 * ps);
+                        if ((uint32_t)(y >> 32) == epoch) {
+                            vals[ps] = __uint_as_float((uint32_t)y);
+                            need &= ~(1u << ps);
+                        }
+                    }
+                }
+            }
+            if (!ok) {
+                __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            MC_STAMP(3);
+            // slice sums: a fixed 16-lane DPP tree per pair, read from the row's lane 0
+            float tot[4 * NPASS];
+#pragma unroll
+            for (int ps = 0; ps < NPASS; ++ps) {
+                float t = vals[ps];
+                t += dpp_row<0xB1>(t);
+                t += dpp_row<0x4E>(t);
+                t += dpp_row<0x141>(t);
+                t += dpp_row<0x140>(t);
+#pragma unroll
+                for (int row = 0; row < 4; ++row) tot[4 * ps + row] = rl(t, 16 * row);
+            }
+            // totals: the slice sum plus the scalar terms' sum
+            lpn[0] = (tot[0] + slp[0]) + P.lp_const;
+            lpn[1] = (tot[1] + slp[1]) + P.lp_const;
+            {
+                float gx = 0.0f;
+#pragma unroll
+                for (int k = 0; k < NSH; ++k)
+                    if (xk == k) gx = xc ? tot[2 + 2 * k + 1] + sgs[k][1] : tot[2 + 2 * k] + sgs[k][0];
+                sh.g = xon ? gx : 0.0f;
+            }
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (l == 0) K0[c] = tot[2 * (NSH + 1) + c];
+                if (l == L - 1) K1[c] = tot[2 * (NSH + 2) + c];
+            }
+            if (l + 1 < L) drift_shared(true);  // the shared parameters' next position
+            MC_STAMP(4);
+        }
+        if (!ok) break;
+        // ---- accept / adapt (identical in every slice of the block) ------------
+        float k1s[2] = {0.f, 0.f};
+        {
+            const float p1 = sh.p + xh * sh.g;
+            const float p2 = p1 * p1;
+            for (int k = 0; k < Dsh; ++k) {
+                k1s[0] += rl(p2, 2 * k);
+                k1s[1] += rl(p2, 2 * k + 1);
+            }
+        }
+        bool acc[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const float H0 = -lp[c] + 0.5f * (K0[c] + k0s[c]);
+            const float H1 = -lpn[c] + 0.5f * (K1[c] + k1s[c]);
+            const float ratio = -(H1 - H0);
+            const mc_u32x4 ru = mc_draw(cfg.seed, (uint32_t)(cfg.chain_offset + cc[c]),
+                                        (uint32_t)it, MC_RNG_TAG_ACCEPT, 0, 0);
+            const float logu = mc_logf_ref(mc_u01_f32(ru.x));
+            const bool accepted = logu < ratio;
+            acc[c] = accepted;
+            nacc[c] += accepted ? 1 : 0;
+            ntot[c] += 1;
+            const double eps_used = eps[c];
+            if (warm && cfg.adapt_step_size && it > 10) {
+                const double rate = (double)nacc[c] / (double)ntot[c];
+                eps[c] = (rate < cfg.target_accept) ? eps_used * 0.95 : eps_used * 1.05;
+            }
+            if (accepted) {
+                lp[c] = lpn[c];
+            } else {
+#pragma unroll
+                for (int r = 0; r < RS; ++r) {
+                    R.q[r][c] = q0[r][c];
+                    R.g[r][c] = g0[r][c];
+                }
+            }
+            if (slice == 0 && j == 0 && live[c]) {
+                const int64_t ti = it - tr.iter_begin;
+                if (ti >= 0 && ti < tr.capacity) {
+                    const int64_t o = cc[c] * tr.capacity + ti;
+                    if (tr.accepted) tr.accepted[o] = accepted ? 1 : 0;
+                    if (tr.accept_stat) tr.accept_stat[o] = ratio;
+                    if (tr.step_size) tr.step_size[o] = eps_used;
+                    if (tr.energy) tr.energy[o] = H0;
+                    if (tr.tree_depth) tr.tree_depth[o] = L;
+                    if (tr.n_leapfrog) tr.n_leapfrog[o] = L;
+                }
+            }
+        }
+        if (!(xc ? acc[1] : acc[0])) {
+            sh.q = q0s;
+            sh.g = g0s;
+        }
+        if (!warm && samples != nullptr) {
+            const int64_t s = it - cfg.num_warmup - cfg.sample_begin;
+            if (s >= 0 && s < cfg.sample_capacity) {
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    if (!live[c]) continue;
+                    float* out = samples + (cc[c] * cfg.sample_capacity + s) * (int64_t)D;
+#pragma unroll
+                    for (int r = 0; r < RS; ++r)
+                        if (gk[r] >= 0) out[gk[r]] = R.q[r][c];
+                }
+                if (slice == 0 && xlive)
+                    samples[(xch_id * cfg.sample_capacity + s) * (int64_t)D + xg] = sh.q;
+            }
+        }
+        MC_STAMP(6);
+    }
+
+    // ---- launch epilogue: state back to HBM ---------------------------------------
+    MC_STAMP_FLUSH
+    if (!ok) return;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        if (!live[c]) continue;
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            if (gk[r] >= 0) {
+                st_q[cc[c] * D + gk[r]] = R.q[r][c];
+                st_g[cc[c] * D + gk[r]] = R.g[r][c];
+            }
+        }
+        if (slice == 0 && j == 0) {
+            mc_chain_scalars& sc = scal[cc[c]];
+            sc.logp = lp[c];
+            sc.step_size = eps[c];
+            sc.n_accept = nacc[c];
+            sc.n_total = ntot[c];
+            sc.warmup_accept = wacc[c];
+            sc.warmup_total = wtot[c];
+            sc.n_grad += cfg.iter_count * (int64_t)L;
+        }
+    }
+    if (slice == 0 && xlive) {
+        st_q[xch_id * D + xg] = sh.q;
+        st_g[xch_id * D + xg] = sh.g;
+    }
+}
+
+}  // namespace mc

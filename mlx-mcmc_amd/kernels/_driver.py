@@ -54,7 +54,8 @@ def run_sampler(algorithm: str, log_prob_fn, initial_params, *, num_samples: int
                 max_tree_depth: int = 10, num_chains: int = 1, chain_offset: int = 0,
                 slice_mode: str = "reference", progress: bool = True,
                 progress_every: Optional[int] = None, return_trace: bool = False,
-                keep_on_device: bool = False, initial_positions=None, num_slices: int = 0):
+                keep_on_device: bool = False, initial_positions=None, num_slices: int = 0,
+                slice_kernel: str = "auto"):
     import torch
 
     if algorithm not in ("hmc", "nuts"):
@@ -62,7 +63,8 @@ def run_sampler(algorithm: str, log_prob_fn, initial_params, *, num_samples: int
     if num_samples < 0 or num_warmup < 0:
         raise ValueError("num_samples and num_warmup must be non-negative")
     k = _as_key(key)
-    program = _trace.compile_model(log_prob_fn, initial_params, slices=num_slices)
+    program = _trace.compile_model(log_prob_fn, initial_params, slices=num_slices,
+                                   slice_kernel=slice_kernel)
     layout = program.layout
     C = int(num_chains)
     if C < 1:

@@ -10,7 +10,10 @@ launch (samples gain a leading chain axis), ``chain_offset`` selects the RNG
 streams (for sharding chains over GPUs), ``return_info`` also returns a
 ``RunInfo`` with per-chain step sizes, timings and an optional trace.
 ``num_slices`` picks the work split of large models (0 automatic, 1 one
-chain per workgroup, >= 2 data slices per chain: csrc/sliced.h).
+chain per workgroup, >= 2 data slices per chain: csrc/sliced.h), and
+``slice_kernel`` the kernel of a sliced program ("auto": the lane-resident
+csrc/lanes.h when the layout qualifies, "interpreter": csrc/sliced.h,
+"lanes").
 Vector-valued parameters are supported (the reference's ``float()`` store,
 hmc.py:192, rejects them — SURVEY Q6).
 """
@@ -22,7 +25,7 @@ from ._driver import run_sampler
 def hmc(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_size=0.1,
         num_leapfrog_steps=10, adapt_step_size=True, target_accept=0.8, key=None, *,
         num_chains=1, chain_offset=0, progress=True, return_info=False, return_trace=False,
-        keep_on_device=False, initial_positions=None, num_slices=0):
+        keep_on_device=False, initial_positions=None, num_slices=0, slice_kernel="auto"):
     """Hamiltonian Monte Carlo sampler using gradient information.
 
     Returns ``(samples, acceptance_rate)`` like the reference: ``samples`` maps
@@ -37,7 +40,7 @@ def hmc(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_siz
         key=key, num_leapfrog_steps=num_leapfrog_steps, num_chains=num_chains,
         chain_offset=chain_offset, progress=progress, return_trace=return_trace,
         keep_on_device=keep_on_device, initial_positions=initial_positions,
-        num_slices=num_slices)
+        num_slices=num_slices, slice_kernel=slice_kernel)
     if return_info:
         return samples, rate, info
     return samples, rate

@@ -1,8 +1,10 @@
-"""Sliced HMC (csrc/sliced.h): a chain's log density split over S workgroups.
+"""Sliced HMC: a chain's log density split over S workgroups, by the term
+interpreter (csrc/sliced.h, k_hmc_sl) and the lane-resident kernel
+(csrc/lanes.h, k_hmc_lr).
 
-The sliced kernel runs the same sampler as k_hmc (reference hmc.py:7-206);
-only fp32 summation order differs (per-slice partial sums, combined in slice
-order).  Parity bars:
+Both run the same sampler as k_hmc (reference hmc.py:7-206); only fp32
+summation order differs (per-slice partial sums, combined in slice order).
+Every test runs both kernels.  Parity bars:
   * accept decisions and step sizes identical to the unsliced kernel on every
     chain for the whole (short) run, positions within rtol 1e-3 — on models
     that cover every operand combination the planner handles (shared-only
@@ -83,12 +85,17 @@ MODELS = {"iid": model_iid, "scale_vec": model_scale_vec, "value_pp": model_valu
           "hier_small": model_hier_small}
 
 
-def _run(lp, init, slices, C=8, warm=10, samp=10, L=8, eps=0.02, seed=3, chain_offset=0):
+KERNELS = ["interpreter", "lanes"]
+
+
+def _run(lp, init, slices, C=8, warm=10, samp=10, L=8, eps=0.02, seed=3, chain_offset=0,
+         kernel="auto"):
     m = _m()
     s, rate, info = m.hmc(lp, init, num_samples=samp, num_warmup=warm, step_size=eps,
                           num_leapfrog_steps=L, key=m.random.key(seed), num_chains=C,
                           chain_offset=chain_offset, progress=False, return_info=True,
-                          return_trace=True, num_slices=slices)
+                          return_trace=True, num_slices=slices,
+                          slice_kernel=kernel if slices != 1 else "auto")
     return s, info
 
 
@@ -98,7 +105,9 @@ def test_auto_slicing_large_and_small(gpu):
 
     G, N = W.SHAPES["large"]
     big = _trace.compile_model(*W.hierarchical(W.ns_product(), G, N))
-    assert big.num_slices == 16
+    assert big.num_slices == 16 and big.slice_kernel == "lanes"
+    big.set_slice_kernel("interpreter")
+    assert big.slice_kernel == "interpreter"
     small = _trace.compile_model(*W.simple_normal(W.ns_product()))
     assert small.num_slices == 1
 
@@ -117,12 +126,13 @@ def test_unsliceable_program_is_rejected(gpu):
     assert prog.num_slices == 1
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("name", sorted(MODELS))
 @pytest.mark.parametrize("S", [2, 3])
-def test_sliced_matches_unsliced(gpu, name, S):
+def test_sliced_matches_unsliced(gpu, name, S, kernel):
     lp, init = MODELS[name](W.ns_product())
     a, ia = _run(lp, init, 1)
-    b, ib = _run(lp, init, S)
+    b, ib = _run(lp, init, S, kernel=kernel)
     np.testing.assert_array_equal(ia.trace["accepted"], ib.trace["accepted"])
     np.testing.assert_array_equal(ia.trace["step_size"], ib.trace["step_size"])
     for k in a:
@@ -130,18 +140,20 @@ def test_sliced_matches_unsliced(gpu, name, S):
     np.testing.assert_allclose(ib.trace["energy"], ia.trace["energy"], rtol=1e-4, atol=1e-3)
 
 
-def test_sliced_determinism_chain_split_and_block_size(gpu):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_sliced_determinism_chain_split_and_block_size(gpu, kernel):
     lp, init = model_hier_small(W.ns_product())
-    full, _ = _run(lp, init, 4, C=24)          # 16-chain blocks
-    again, _ = _run(lp, init, 4, C=24)
+    full, _ = _run(lp, init, 4, C=24, kernel=kernel)          # 16-chain blocks
+    again, _ = _run(lp, init, 4, C=24, kernel=kernel)
     for k in full:
         np.testing.assert_array_equal(full[k], again[k])
-    part, _ = _run(lp, init, 4, C=4, chain_offset=10)   # 8-chain block, 4 used
+    part, _ = _run(lp, init, 4, C=4, chain_offset=10, kernel=kernel)  # a part-filled block
     for k in full:
         np.testing.assert_array_equal(full[k][10:14], part[k])
 
 
-def test_sliced_golden_hmc_trace(gpu):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_sliced_golden_hmc_trace(gpu, kernel):
     m = _m()
     with open(os.path.join(os.path.dirname(__file__), "golden", "hmc_simple.json")) as f:
         h = json.load(f)
@@ -149,33 +161,35 @@ def test_sliced_golden_hmc_trace(gpu):
     _, _, info = m.hmc(lp, init, num_samples=h["num_samples"], num_warmup=h["num_warmup"],
                        step_size=h["step_size"], num_leapfrog_steps=h["num_leapfrog_steps"],
                        key=m.random.key(h["seed"]), progress=False, return_info=True,
-                       return_trace=True, num_slices=2)
+                       return_trace=True, num_slices=2, slice_kernel=kernel)
     acc = info.trace["accepted"][0].astype(bool).tolist()
     same = next((i for i, (x, y) in enumerate(zip(acc, h["accepted"])) if x != y), len(acc))
     assert same >= 50
     np.testing.assert_array_equal(info.trace["step_size"][0][:same], h["eps"][:same])
 
 
-def test_sliced_large_matches_unsliced(gpu):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_sliced_large_matches_unsliced(gpu, kernel):
     """bench.py's workload: decisions and energies agree with k_hmc."""
     G, N = W.SHAPES["large"]
     lp, init = W.hierarchical(W.ns_product(), G, N)
     a, ia = _run(lp, init, 1, C=16, warm=5, samp=5, L=20, eps=0.01)
-    b, ib = _run(lp, init, 0, C=16, warm=5, samp=5, L=20, eps=0.01)
+    b, ib = _run(lp, init, 0, C=16, warm=5, samp=5, L=20, eps=0.01, kernel=kernel)
     np.testing.assert_array_equal(ia.trace["accepted"], ib.trace["accepted"])
     np.testing.assert_allclose(ib.trace["energy"], ia.trace["energy"], rtol=1e-5)
     for k in a:
         np.testing.assert_allclose(b[k], a[k], rtol=1e-3, atol=1e-4)
 
 
-def test_sliced_posterior(gpu):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_sliced_posterior(gpu, kernel):
     """Reference-style statistical check through the sliced path
     (tests/test_hmc.py:13-40 posterior of the simple normal model)."""
     m = _m()
     lp, init = W.simple_normal(W.ns_product())
     s, rate = m.hmc(lp, init, num_samples=1000, num_warmup=500, step_size=0.1,
                     num_leapfrog_steps=10, key=m.random.key(0), num_chains=16, progress=False,
-                    num_slices=2)
+                    num_slices=2, slice_kernel=kernel)
     assert abs(float(np.mean(s["mu"])) - 5.0) < 0.6
     assert 1.4 < float(np.mean(s["sigma"])) < 2.6
     assert 0.3 < float(np.mean(rate)) <= 1.0
