@@ -77,7 +77,9 @@ struct LanePlan {
     std::vector<float> data;
     std::vector<int64_t> blocks;
     std::vector<int32_t> gidx;
+    std::vector<LrSterm> sterms;
     LrTerm* d_terms = nullptr;
+    LrSterm* d_sterms = nullptr;
     float* d_data = nullptr;
     int64_t* d_blocks = nullptr;
     int32_t* d_gidx = nullptr;
@@ -711,6 +713,7 @@ static void free_lanes(LanePlan& L) {
     if (L.d_data) (void)hipFree(L.d_data);
     if (L.d_blocks) (void)hipFree(L.d_blocks);
     if (L.d_gidx) (void)hipFree(L.d_gidx);
+    if (L.d_sterms) (void)hipFree(L.d_sterms);
     L = LanePlan();
 }
 
@@ -723,9 +726,9 @@ static LrCtx lrctx_of(const mc_program* p) {
     c.data = L.d_data;
     c.blocks = L.d_blocks;
     c.gidx = L.d_gidx;
-    c.sterms = P.d_sterms;
+    c.sterms = L.d_sterms;
     c.n_terms = (int32_t)p->raw.size();
-    c.n_sterms = (int32_t)P.sterms.size();
+    c.n_sterms = (int32_t)L.sterms.size();
     c.S = P.S;
     c.Dsh = P.Dsh;
     c.D = p->D;
@@ -801,7 +804,7 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         while (L.data.size() % 4) L.data.push_back(0.0f);
         const int64_t blk0 = (int64_t)L.data.size();
         int nact = 0;
-        std::vector<LrTerm> swept, rest;
+        std::vector<LrTerm> swept, direct, rest;
         for (int t = 0; t < nT; ++t) {
             if (part.scalar[t]) continue;
             const DevTerm& rt = raw[t];
@@ -898,12 +901,17 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
             L.data.resize(lo + lens.size());
             std::memcpy(&L.data[lo], lens.data(), lens.size() * 4);
             lt.len_off = (int32_t)(lo - blk0);
+            int32_t maxlen = 0;
+            for (int32_t x : lens) maxlen = std::max(maxlen, x);
+            const bool dir = (lt.sig == LS_PP_SH_SH || lt.sig == LS_PP_C_C) && maxlen <= 1;
             const bool sw = lt.sig == LS_DATA_PP_SH || lt.sig == LS_DATA_PP_C ||
                             lt.sig == LS_PP_C_C || lt.sig == LS_PP_DATA_SH;
-            if (sw && (int)swept.size() < kLrSweep) swept.push_back(lt);
+            if (dir && (int)direct.size() < kLrDirect) direct.push_back(lt);
+            else if (sw && (int)swept.size() < kLrSweep) swept.push_back(lt);
             else rest.push_back(lt);
         }
         for (const LrTerm& lt : swept) L.terms[(size_t)s * nT + nact++] = lt;
+        for (const LrTerm& lt : direct) L.terms[(size_t)s * nT + nact++] = lt;
         for (const LrTerm& lt : rest) L.terms[(size_t)s * nT + nact++] = lt;
         while (L.data.size() % 4) L.data.push_back(0.0f);
         const int64_t blen = (int64_t)L.data.size() - blk0;
@@ -911,10 +919,29 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         L.blocks[4 * s] = blk0;
         L.blocks[4 * s + 1] = blen;
         L.blocks[4 * s + 2] = nact;
-        L.blocks[4 * s + 3] = (int64_t)swept.size();
+        L.blocks[4 * s + 3] = (int64_t)swept.size() | ((int64_t)direct.size() << 8);
         L.sdata_floats = std::max<int>(L.sdata_floats, (int)blen);
     }
-    if ((int64_t)L.sdata_floats * 4 > kSlLdsBudget) return no("slice data exceed the LDS budget");
+    // the scalar terms, compact (LDS copy in every workgroup)
+    for (const SlTerm& st : SP.sterms) {
+        LrSterm x;
+        std::memset(&x, 0, sizeof(x));
+        x.dist = st.dist;
+        x.kinds = st.kind[0] | (st.kind[1] << 4) | (st.kind[2] << 8);
+        x.jsh = (st.kind[0] == SK_SHARED ? st.jsh[0] : 0) |
+                ((st.kind[1] == SK_SHARED ? st.jsh[1] : 0) << 4) |
+                ((st.kind[2] == SK_SHARED ? st.jsh[2] : 0) << 8);
+        x.c0 = st.c0;
+        for (int a = 0; a < 3; ++a) x.cval[a] = st.cval[a];
+        x.clogs = st.clogs;
+        x.clg = st.clg;
+        x.wn = st.weight * (float)st.niter;
+        L.sterms.push_back(x);
+    }
+    L.sdata_floats = (L.sdata_floats + 3) / 4 * 4;  // the scalar terms follow, 16-byte aligned
+    if ((int64_t)L.sdata_floats * 4 + (int64_t)L.sterms.size() * (int64_t)sizeof(LrSterm) >
+        kSlLdsBudget)
+        return no("slice data exceed the LDS budget");
     if (L.data.empty()) L.data.assign(4, 0.0f);
     L.ok = 1;
     return MC_OK;
@@ -980,6 +1007,7 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
         if (e == hipSuccess) e = upload(&LP.d_data, LP.data);
         if (e == hipSuccess) e = upload(&LP.d_blocks, LP.blocks);
         if (e == hipSuccess) e = upload(&LP.d_gidx, LP.gidx);
+        if (e == hipSuccess && !LP.sterms.empty()) e = upload(&LP.d_sterms, LP.sterms);
         if (e != hipSuccess) {
             free_lanes(LP);
             free_slices(p->sl);
@@ -1594,7 +1622,7 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
     std::memset(&A, 0, sizeof(A));
     A.cfg = *cfg;
     const LrCtx ctx = lrctx_of(p);
-    const size_t lds = (size_t)p->lr.sdata_floats * 4;
+    const size_t lds = (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm);
     MC_HIP_TRY(allow_lds(k_hmc_lr<RS, NSH>, lds));
     const int64_t C = cfg->num_chains;
     const int64_t groups = (C + kLrNB - 1) / kLrNB;

@@ -70,19 +70,32 @@ enum : int32_t {
     LS_DATA_SH_SH = 6,   // y ~ Normal(mu, sigma)              chunked likelihood
 };
 
+// A scalar term (constants and shared parameters only), compact for LDS.
+struct LrSterm {
+    int32_t dist;
+    int32_t kinds;  // SK_* of value | loc << 4 | scale << 8
+    int32_t jsh;    // shared ordinals: value | loc << 4 | scale << 8
+    float c0;
+    float cval[3];
+    float clogs;    // CONST scale: f32 log(scale)
+    float clg;      // gammaln normaliser (constant shapes)
+    float wn;       // weight * element count
+    int32_t pad[2];
+};
+
 struct LrCtx {
     const LrTerm* terms;    // [S][n_terms], the slice's active terms first
     const float* data;      // slice blocks
     const int64_t* blocks;  // per slice {data offset, floats, active terms, swept terms}
     const int32_t* gidx;    // [S][kLrMaxSlots][64]: global parameter of (slot, lane), -1
-    const SlTerm* sterms;   // scalar terms (constants / shared parameters only)
+    const LrSterm* sterms;  // scalar terms (constants / shared parameters only)
     int32_t n_terms;
     int32_t n_sterms;
     int32_t S;
     int32_t Dsh;
     int32_t D;
     int32_t nitems;         // record per chain: lp, Dsh cotangents, K0, K1
-    int32_t sdata_floats;
+    int32_t sdata_floats;   // LDS floats of a slice block (the scalar terms follow)
     float lp_const;
     int32_t shl[kLrMaxShared];  // global index of shared parameter k
 };
@@ -280,19 +293,33 @@ MC_DEV void lr_sweep(const MC_CONST LrTerm* tt, int nsweep, const float* sd, int
     }
 }
 
-// Finish the swept terms from their moment sums at the current shared values.
+// A "direct" term: theta ~ Normal(loc, scale) with value = the lane's private
+// parameter, loc / scale broadcast (shared or constant), at most one element
+// per parameter in this slice (hierarchical priors).  Evaluated in the finish
+// from registers, with the moment branch's arithmetic at count 1.
+constexpr int kLrDirect = 2;
+
+// Per-lane element counts of the swept terms and presence of the direct
+// terms, read once per launch from the slices' length tables.
 template <int RS>
-MC_DEV void lr_finish_swept(const MC_CONST LrTerm* tt, int nsweep, const float* sd, int j,
-                            LrPriv<RS>& R, const LrShared& sh, const LrMoments<RS>& M,
-                            float (&lpp)[2], float (&gshp)[kLrMaxShared][2]) {
+struct LrCounts {
+    float cs[kLrSweep][RS];
+    bool pd[kLrDirect][RS];
+};
+
+// Finish the swept terms from their moment sums, and evaluate the direct
+// terms, at the current shared values.
+template <int RS>
+MC_DEV void lr_finish(const MC_CONST LrTerm* tt, int nsweep, int ndirect, LrPriv<RS>& R,
+                      const LrShared& sh, const LrMoments<RS>& M, const LrCounts<RS>& K,
+                      float (&lpp)[2], float (&gshp)[kLrMaxShared][2]) {
 #pragma unroll
     for (int t = 0; t < kLrSweep; ++t) {
         if (t >= nsweep) break;
         const MC_CONST LrTerm* T = tt + t;
-        const int nslot = T->nslot, pp = T->pp, j2 = T->jsh[2];
+        const int pp = T->pp, j2 = T->jsh[2];
         const bool shs = T->kind[2] == SK_SHARED;
         const float w = T->weight, c0 = T->c0;
-        const int32_t* lens = (const int32_t*)sd + T->len_off;
         float is[2], iv[2], lg[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -303,10 +330,8 @@ MC_DEV void lr_finish_swept(const MC_CONST LrTerm* tt, int nsweep, const float* 
         float ps[2] = {0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
-            if (r >= nslot) break;
-            const int len = lens[r * 64 + j];
-            if (len <= 0) continue;
-            const float cnt = (float)len;
+            const float cnt = K.cs[t][r];
+            if (cnt == 0.0f) continue;
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
                 const float s1 = M.s1[t][r][c], s2 = M.s2[t][r][c];
@@ -320,6 +345,43 @@ MC_DEV void lr_finish_swept(const MC_CONST LrTerm* tt, int nsweep, const float* 
         if (shs) {
             add4(gshp, j2, 0, ps[0]);
             add4(gshp, j2, 1, ps[1]);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < kLrDirect; ++t) {
+        if (t >= ndirect) break;
+        const MC_CONST LrTerm* T = tt + nsweep + t;
+        const int j1 = T->jsh[1], j2 = T->jsh[2];
+        const bool shm = T->kind[1] == SK_SHARED, shs = T->kind[2] == SK_SHARED;
+        const float w = T->weight, c0 = T->c0;
+        float um[2], is[2], iv[2], lg[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            um[c] = shm ? rl(sh.q, 2 * j1 + c) : T->cval[1];
+            is[c] = shs ? rl(sh.is, 2 * j2 + c) : T->cinv;
+            iv[c] = shs ? rl(sh.iv, 2 * j2 + c) : T->cinv2;
+            lg[c] = shs ? rl(sh.lg, 2 * j2 + c) : T->clogs;
+        }
+        float pm[2] = {0.f, 0.f}, ps[2] = {0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            if (!K.pd[t][r]) continue;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const float d = R.q[r][c] - um[c];
+                const float s2 = fmaf(d, d, 0.0f);
+                const float lpt = 1.0f * (c0 - lg[c]) - (0.5f * s2) * iv[c];
+                lpp[c] += w * lpt;
+                const float u = w * (d * iv[c]);
+                R.g[r][c] += -u;
+                pm[c] += u;
+                ps[c] += w * ((s2 * iv[c] - 1.0f) * is[c]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (shm) add4(gshp, j1, c, pm[c]);
+            if (shs) add4(gshp, j2, c, ps[c]);
         }
     }
 }
@@ -474,50 +536,66 @@ MC_DEV void lr_eval(const MC_CONST LrTerm* tt, int t0, int nact, const float* sd
     }
 }
 
-// The scalar terms (constants and shared parameters only), lane-parallel:
-// lane x evaluates term t0 + x / 2 for chain x % 2; the rows are then summed
-// over the terms in term order for each chain (uniform results in lp[c],
-// gs[k][c]).  Every slice computes the same sums and adds them to the
-// exchanged totals, so they run while the records travel.
-MC_DEV void lr_scalar_terms(const LrCtx& P, const LrShared& sh, int j, float (&lp)[2],
-                            float (&gs)[kLrMaxShared][2]) {
-    for (int t0 = 0; t0 < P.n_sterms; t0 += 32) {
+// The scalar terms (constants and shared parameters only), lane-parallel
+// from their LDS copy: lane x evaluates term t0 + x / 2 for chain x % 2; the
+// rows are summed per chain with wave_sum8 (a fixed tree: the same sums in
+// every slice, which add them to the exchanged totals).  Results uniform:
+// lp[c], gs[k][c].
+MC_DEV void wave_sum8(const float (&v)[8], float (&out)[8]);
+MC_DEV void lr_scalar_terms(int n_sterms, const LrSterm* st, const LrShared& sh, int j, int nsh,
+                            float (&lp)[2], float (&gs)[kLrMaxShared][2]) {
+    for (int t0 = 0; t0 < n_sterms; t0 += 32) {
         const int t = t0 + (j >> 1), c = j & 1;
-        const bool on = t < P.n_sterms;
-        const SlTerm* T = P.sterms + (on ? t : 0);  // per-lane term: vector loads
-        const int k0 = T->kind[0], k1 = T->kind[1], k2 = T->kind[2];
+        const bool on = t < n_sterms;
+        const LrSterm T = st[on ? t : 0];
+        const int k0 = T.kinds & 15, k1 = (T.kinds >> 4) & 15, k2 = (T.kinds >> 8) & 15;
+        const int j0 = T.jsh & 15, j1 = (T.jsh >> 4) & 15, j2 = (T.jsh >> 8) & 15;
         // chain c's shared values live in lane 2 jsh + c (all lanes active here)
-        const float q0 = __shfl(sh.q, 2 * T->jsh[0] + c);
-        const float q1 = __shfl(sh.q, 2 * T->jsh[1] + c);
-        const float q2 = __shfl(sh.q, 2 * T->jsh[2] + c);
+        const float q0 = __shfl(sh.q, 2 * j0 + c), q1 = __shfl(sh.q, 2 * j1 + c);
+        const float q2 = __shfl(sh.q, 2 * j2 + c);
         float lpx = 0.0f, gx[kLrMaxShared] = {0.f, 0.f, 0.f, 0.f};
         if (on) {
-            const float v = k0 == SK_SHARED ? q0 : (k0 == SK_CONST ? T->cval[0] : 0.f);
-            const float m = k1 == SK_SHARED ? q1 : (k1 == SK_CONST ? T->cval[1] : 0.f);
-            const float sc = k2 == SK_SHARED ? q2 : (k2 == SK_CONST ? T->cval[2] : 0.f);
-            const float ls = (k2 == SK_CONST) ? T->clogs : logf(sc);
+            const float v = k0 == SK_SHARED ? q0 : (k0 == SK_CONST ? T.cval[0] : 0.f);
+            const float m = k1 == SK_SHARED ? q1 : (k1 == SK_CONST ? T.cval[1] : 0.f);
+            const float sc = k2 == SK_SHARED ? q2 : (k2 == SK_CONST ? T.cval[2] : 0.f);
+            const float ls = (k2 == SK_CONST) ? T.clogs : logf(sc);
             const float lgx =
-                (k1 == SK_SHARED || k2 == SK_SHARED) ? lgamma_norm(T->dist, m, sc) : T->clg;
-            const ElemOut e = elem_eval(T->dist, T->c0, v, m, sc, ls, lgx);
-            const float wn = T->weight * (float)T->niter;
-            lpx = wn * e.lp;
+                (k1 == SK_SHARED || k2 == SK_SHARED) ? lgamma_norm(T.dist, m, sc) : T.clg;
+            const ElemOut e = elem_eval(T.dist, T.c0, v, m, sc, ls, lgx);
+            lpx = T.wn * e.lp;
 #pragma unroll
             for (int k = 0; k < kLrMaxShared; ++k) {
                 float y = 0.0f;
-                if (k0 == SK_SHARED && T->jsh[0] == k) y += wn * e.dv;
-                if (k1 == SK_SHARED && T->jsh[1] == k) y += wn * e.dm;
-                if (k2 == SK_SHARED && T->jsh[2] == k) y += wn * e.ds;
+                if (k0 == SK_SHARED && j0 == k) y += T.wn * e.dv;
+                if (k1 == SK_SHARED && j1 == k) y += T.wn * e.dm;
+                if (k2 == SK_SHARED && j2 == k) y += T.wn * e.ds;
                 gx[k] = y;
             }
         }
-        const int nt = min(32, P.n_sterms - t0);
-        for (int u = 0; u < nt; ++u) {
+        float v8[8], t8[8];
+        v8[0] = c ? 0.0f : lpx;
+        v8[1] = c ? lpx : 0.0f;
 #pragma unroll
-            for (int cc = 0; cc < 2; ++cc) {
-                lp[cc] += rl(lpx, 2 * u + cc);
+        for (int k = 0; k < 3; ++k) {
+            v8[2 + 2 * k] = c ? 0.0f : gx[k];
+            v8[3 + 2 * k] = c ? gx[k] : 0.0f;
+        }
+        wave_sum8(v8, t8);
+        lp[0] += t8[0];
+        lp[1] += t8[1];
 #pragma unroll
-                for (int k = 0; k < kLrMaxShared; ++k) gs[k][cc] += rl(gx[k], 2 * u + cc);
-            }
+        for (int k = 0; k < 3; ++k) {
+            gs[k][0] += t8[2 + 2 * k];
+            gs[k][1] += t8[3 + 2 * k];
+        }
+        if (nsh > 3) {  // a 4th shared parameter
+            v8[0] = c ? 0.0f : gx[3];
+            v8[1] = c ? gx[3] : 0.0f;
+#pragma unroll
+            for (int x = 2; x < 8; ++x) v8[x] = 0.0f;
+            wave_sum8(v8, t8);
+            gs[3][0] += t8[0];
+            gs[3][1] += t8[1];
         }
     }
 }
@@ -610,9 +688,14 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     const int64_t doff = blk[0];
     const int dlen = (int)blk[1];
     const int nact = (int)blk[2];
-    const int nsweep = (int)blk[3];  // the first nsweep active terms are swept
+    const int nsweep = (int)(blk[3] & 255);          // active terms [0, nsweep): swept,
+    const int ndirect = (int)((blk[3] >> 8) & 255);  // then ndirect direct terms
+    const int nfast = nsweep + ndirect;
     for (int i = tid; 4 * i < dlen; i += 512)
         *(float4*)(sd + 4 * i) = *(const float4*)(P.data + doff + 4 * i);
+    LrSterm* sst = (LrSterm*)(smem + P.sdata_floats);  // the scalar terms, after the block
+    for (int i = tid; i < P.n_sterms * (int)(sizeof(LrSterm) / 16); i += 512)
+        ((float4*)sst)[i] = ((const float4*)P.sterms)[i];
 
     // ---- registers: private slots and the lane's shared parameter ----------------
     LrPriv<RS> R;
@@ -647,6 +730,24 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     __syncthreads();  // the slice block is in LDS
 
     const MC_CONST LrTerm* tt = cptr(P.terms) + (int64_t)slice * P.n_terms;
+    LrCounts<RS> KC;
+#pragma unroll
+    for (int t = 0; t < kLrSweep; ++t)
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            KC.cs[t][r] = 0.0f;
+            if (t < nsweep && r < tt[t].nslot)
+                KC.cs[t][r] = (float)((const int32_t*)sd)[tt[t].len_off + r * 64 + j];
+        }
+#pragma unroll
+    for (int t = 0; t < kLrDirect; ++t)
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            KC.pd[t][r] = false;
+            if (t < ndirect && r < tt[nsweep + t].nslot)
+                KC.pd[t][r] = ((const int32_t*)sd)[tt[nsweep + t].len_off + r * 64 + j] > 0;
+        }
+
     const int L = cfg.num_leapfrog_steps;
     uint32_t epoch = 0;
     bool ok = true;
@@ -761,8 +862,8 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             for (int k = 0; k < kLrMaxShared; ++k) gshp[k][0] = gshp[k][1] = 0.0f;
 #pragma unroll
             for (int r = 0; r < RS; ++r) R.g[r][0] = R.g[r][1] = 0.0f;
-            lr_finish_swept<RS>(tt, nsweep, sd, j, R, sh, M, lpp, gshp);
-            lr_eval<RS>(tt, nsweep, nact, sd, j, R, sh, lpp, gshp);
+            lr_finish<RS>(tt, nsweep, ndirect, R, sh, M, KC, lpp, gshp);
+            lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp);
             MC_STAMP(1);
             // the wave totals of the record, pair-indexed (2 item + chain)
             float rec[NPAIR];
@@ -826,7 +927,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             float sgs[kLrMaxShared][2];
 #pragma unroll
             for (int k = 0; k < kLrMaxShared; ++k) sgs[k][0] = sgs[k][1] = 0.0f;
-            lr_scalar_terms(P, sh, j, slp, sgs);
+            lr_scalar_terms(P.n_sterms, sst, sh, j, Dsh, slp, sgs);
             MC_STAMP(7);
             // poll: pass ps, lane x -> pair 4 ps + x / 16, slice x % 16
             unsigned long long* gp = par ? gpoll[1] : gpoll[0];

@@ -26,11 +26,11 @@ def per_dispatch(d, counter, match):
 
 def main():
     fdir, wdir, shape = sys.argv[1], sys.argv[2], sys.argv[3]
-    kern = "k_hmc_sl"
-    f = per_dispatch(fdir, "FETCH_SIZE", kern)
-    if not f:
-        kern = "k_hmc"
+    f = {}
+    for kern in ("k_hmc_lr", "k_hmc_sl", "k_hmc"):  # the sampler kernel bench.py ran
         f = per_dispatch(fdir, "FETCH_SIZE", kern)
+        if f:
+            break
     w = per_dispatch(wdir, "WRITE_SIZE", kern)
     fk = sum(f.values()) / max(len(f), 1)
     wk = sum(w.values()) / max(len(w), 1)

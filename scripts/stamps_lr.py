@@ -23,10 +23,25 @@ import workloads as W  # noqa: E402
 from mlx_mcmc_amd import _engine, _trace  # noqa: E402
 
 C = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+VAR = sys.argv[2] if len(sys.argv) > 2 else "full"
 G, N = W.SHAPES["large"]
 fn, init = W.hierarchical(W.ns_product(), G, N)
+if VAR != "full":  # one term family only (diagnostic)
+    ns = W.ns_product()
+    y, group = W.hierarchical_data(G, N)
+
+    def lik(p):
+        return ns.sum(ns.Normal(p["theta"][group], p["sigma"]).log_prob(ns.array(y)))
+
+    def lik_prior(p):
+        return lik(p) + ns.sum(ns.Normal(p["mu"], p["tau"]).log_prob(p["theta"]))
+
+    fn = {"lik": lik, "lik_prior": lik_prior}[VAR]
+    init = ({"sigma": np.float32(1), "theta": init["theta"]} if VAR == "lik" else
+            {"mu": np.float32(1), "tau": np.float32(2), "sigma": np.float32(1),
+             "theta": init["theta"]})
 prog = _trace.compile_model(fn, init, slice_kernel="lanes")
-print(f"slices={prog.num_slices} kernel={prog.slice_kernel} chains={C}")
+print(f"variant={VAR} slices={prog.num_slices} kernel={prog.slice_kernel} chains={C}")
 cs = _engine.ChainSet(prog, C, prog.layout.flatten(init), 1e-4)
 L = 20
 cfg = dict(chain_offset=0, num_warmup=0, num_samples=10, sample_begin=0, sample_capacity=0,
