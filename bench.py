@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=15,
                     help="processes of the aggregate CPU baseline (0: skip)")
     ap.add_argument("--no-ess", action="store_true")
+    ap.add_argument("--slices", type=int, default=0,
+                    help="data slices per chain (0: the engine's automatic choice)")
     ap.add_argument("--slice-kernel", default="auto", choices=["auto", "interpreter", "lanes"],
                     help="kernel of the sliced program (csrc/lanes.h or csrc/sliced.h)")
     ap.add_argument("--gather", action="store_true",
@@ -166,7 +168,7 @@ def main():
     K = args.steps
     Wm = args.warmup
     lp_fn, init = W.hierarchical(W.ns_product(), G, N)
-    prog = _trace.compile_model(lp_fn, init, slice_kernel=args.slice_kernel)
+    prog = _trace.compile_model(lp_fn, init, slices=args.slices, slice_kernel=args.slice_kernel)
     chains = _engine.ChainSet(prog, C, prog.layout.flatten(init), args.step_size, device=dev)
     samples = torch.empty((C, max(K, 1), D), dtype=torch.float32, device=dev)
     chain_offset, _ = shard(C * world, world, rank)   # weak scaling: C chains per GPU

@@ -1595,8 +1595,12 @@ static int64_t sl_groups_per_launch(const mc_program* p, int64_t C) {
     return std::min(groups, cap);
 }
 static constexpr int64_t kSlStatusBytes = 256;
+// waves per workgroup of the lane-resident kernel: 8 (16 chains, two waves per
+// SIMD) for up to 16 slices... 4 (8 chains, one wave per SIMD) for <= 8 slices
+static int lr_nw(const mc_program* p) { return p->sl.S <= 8 ? 4 : 8; }
 static int64_t lr_groups_per_launch(const mc_program* p, int64_t C) {
-    const int64_t groups = (C + kLrNB - 1) / kLrNB;
+    const int nb = 2 * lr_nw(p);
+    const int64_t groups = (C + nb - 1) / nb;
     const int64_t cap = std::max<int64_t>(1, device_cus() / p->sl.S);
     return std::min(groups, cap);
 }
@@ -1605,14 +1609,14 @@ static int64_t sl_workspace_bytes(const mc_program* p, int64_t C) {
     int64_t x = 2 * sl_groups_per_launch(p, C) * p->sl.S * (int64_t)p->sl.nitems * nb * 8;
     if (p->lr.ok)  // either kernel may run on the same workspace (lanes.h: one
                    // 128-byte line per (wave, slice) record)
-        x = std::max(x, 2 * lr_groups_per_launch(p, C) * (kLrNB / 2) * p->sl.S * 128);
+        x = std::max(x, 2 * lr_groups_per_launch(p, C) * lr_nw(p) * p->sl.S * 128);
     return kSlStatusBytes + x;
 }
 static bool use_lanes(const mc_program* p, const mc_run_config* cfg) {
     return p->lr.ok && p->slice_kernel != 1 && cfg->num_leapfrog_steps > 0;
 }
 
-template <int RS, int NSH>
+template <int RS, int NSH, int NW>
 static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* state,
                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
     int64_t qo, go;
@@ -1623,9 +1627,10 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
     A.cfg = *cfg;
     const LrCtx ctx = lrctx_of(p);
     const size_t lds = (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm);
-    MC_HIP_TRY(allow_lds(k_hmc_lr<RS, NSH>, lds));
+    MC_HIP_TRY(allow_lds(k_hmc_lr<RS, NSH, NW>, lds));
     const int64_t C = cfg->num_chains;
-    const int64_t groups = (C + kLrNB - 1) / kLrNB;
+    constexpr int NB = 2 * NW;
+    const int64_t groups = (C + NB - 1) / NB;
     const int64_t gpl = lr_groups_per_launch(p, C);
     const int64_t used = sl_workspace_bytes(p, C);
     int* status = (int*)ws;
@@ -1634,8 +1639,8 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
         const int64_t ng = std::min(gpl, groups - g0);
         MC_HIP_TRY(hipMemsetAsync(g0 == 0 ? ws : (void*)xch, 0,
                                   g0 == 0 ? used : used - kSlStatusBytes, st));
-        hipLaunchKernelGGL((k_hmc_lr<RS, NSH>), dim3((unsigned)(ng * p->sl.S)), dim3(512), lds, st, ctx,
-                           A, g0 * kLrNB, ng, (mc_chain_scalars*)b, (float*)(b + qo),
+        hipLaunchKernelGGL((k_hmc_lr<RS, NSH, NW>), dim3((unsigned)(ng * p->sl.S)), dim3(64 * NW),
+                           lds, st, ctx, A, g0 * NB, ng, (mc_chain_scalars*)b, (float*)(b + qo),
                            (float*)(b + go), samples, trace_of(tr), xch, status);
         MC_HIP_TRY(hipGetLastError());
     }
@@ -1728,15 +1733,16 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
         if (device_cus() <= 0) return fail(MC_ERR_HIP, "no HIP device");
         if (use_lanes(p, cfg)) {
             hipStream_t st = (hipStream_t)stream;
-            const bool n4 = p->sl.Dsh > 3;
+            const bool n4 = p->sl.Dsh > 3, w4 = lr_nw(p) == 4;
+#define MC_LR(RS_, NSH_)                                                                   \
+    return w4 ? launch_hmc_lr<RS_, NSH_, 4>(p, cfg, state, samples, tr, ws, st)            \
+              : launch_hmc_lr<RS_, NSH_, 8>(p, cfg, state, samples, tr, ws, st)
             switch (p->lr.rs) {
-                case 1: return n4 ? launch_hmc_lr<1, 4>(p, cfg, state, samples, tr, ws, st)
-                                  : launch_hmc_lr<1, 3>(p, cfg, state, samples, tr, ws, st);
-                case 2: return n4 ? launch_hmc_lr<2, 4>(p, cfg, state, samples, tr, ws, st)
-                                  : launch_hmc_lr<2, 3>(p, cfg, state, samples, tr, ws, st);
-                default: return n4 ? launch_hmc_lr<4, 4>(p, cfg, state, samples, tr, ws, st)
-                                   : launch_hmc_lr<4, 3>(p, cfg, state, samples, tr, ws, st);
+                case 1: if (n4) MC_LR(1, 4); else MC_LR(1, 3);
+                case 2: if (n4) MC_LR(2, 4); else MC_LR(2, 3);
+                default: if (n4) MC_LR(4, 4); else MC_LR(4, 3);
             }
+#undef MC_LR
         }
         return sl_nb_for(p, cfg->num_chains) == 16
                    ? launch_hmc_sl<16>(p, cfg, state, samples, tr, ws, (hipStream_t)stream)

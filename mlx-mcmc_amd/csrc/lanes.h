@@ -36,7 +36,7 @@ namespace mc {
 
 constexpr int kLrMaxSlots = 4;   // private parameters per lane
 constexpr int kLrMaxShared = 4;  // broadcast parameters
-constexpr int kLrNB = 16;        // chains per block: 8 waves x 2 chains
+constexpr int kLrMaxNB = 16;     // chains per block: up to 8 waves x 2 chains
 constexpr int kLrSlices = 16;    // max slices (one 16-lane DPP row per item)
 
 // One term restricted to one slice.
@@ -115,10 +115,14 @@ MC_DEV float pick4(const float (&a)[kLrMaxShared], int k) {
     for (int kk = 1; kk < kLrMaxShared; ++kk) v = (k == kk) ? a[kk] : v;
     return v;
 }
+// (selects, not an indexed store: a runtime index would put the array in scratch)
 MC_DEV void add4(float (&a)[kLrMaxShared][2], int k, int c, float x) {
 #pragma unroll
-    for (int kk = 0; kk < kLrMaxShared; ++kk)
-        if (k == kk) a[kk][c] += x;
+    for (int kk = 0; kk < kLrMaxShared; ++kk) {
+        const float y0 = a[kk][0] + x, y1 = a[kk][1] + x;
+        a[kk][0] = (k == kk && c == 0) ? y0 : a[kk][0];
+        a[kk][1] = (k == kk && c == 1) ? y1 : a[kk][1];
+    }
 }
 
 // Moment sums of one lane's run for both chains (packed): DC bit 0 value is
@@ -553,15 +557,36 @@ MC_DEV void lr_scalar_terms(int n_sterms, const LrSterm* st, const LrShared& sh,
         // chain c's shared values live in lane 2 jsh + c (all lanes active here)
         const float q0 = __shfl(sh.q, 2 * j0 + c), q1 = __shfl(sh.q, 2 * j1 + c);
         const float q2 = __shfl(sh.q, 2 * j2 + c);
+        // the scale's derived values: from the descriptor (constant scale) or
+        // from the lane holding the shared scale
+        const float is2 = __shfl(sh.is, 2 * j2 + c), iv2 = __shfl(sh.iv, 2 * j2 + c);
+        const float lg2 = __shfl(sh.lg, 2 * j2 + c);
         float lpx = 0.0f, gx[kLrMaxShared] = {0.f, 0.f, 0.f, 0.f};
         if (on) {
             const float v = k0 == SK_SHARED ? q0 : (k0 == SK_CONST ? T.cval[0] : 0.f);
             const float m = k1 == SK_SHARED ? q1 : (k1 == SK_CONST ? T.cval[1] : 0.f);
             const float sc = k2 == SK_SHARED ? q2 : (k2 == SK_CONST ? T.cval[2] : 0.f);
-            const float ls = (k2 == SK_CONST) ? T.clogs : logf(sc);
-            const float lgx =
-                (k1 == SK_SHARED || k2 == SK_SHARED) ? lgamma_norm(T.dist, m, sc) : T.clg;
-            const ElemOut e = elem_eval(T.dist, T.c0, v, m, sc, ls, lgx);
+            ElemOut e;
+            if (T.dist == MC_DIST_NORMAL || T.dist == MC_DIST_HALFNORMAL) {
+                // moment form with the scale's reciprocals (no divisions), as
+                // the sliced terms: d = value - loc (HalfNormal: the value)
+                const float cinv = k2 == SK_CONST ? 1.0f / T.cval[2] : is2;
+                const float cinv2 = k2 == SK_CONST ? cinv * cinv : iv2;
+                const float ls = k2 == SK_CONST ? T.clogs : lg2;
+                const float d = T.dist == MC_DIST_NORMAL ? v - m : v;
+                const float d2 = d * d;
+                const bool out = T.dist == MC_DIST_HALFNORMAL && !(v >= 0.0f);
+                e.lp = out ? -__builtin_inff() : (T.c0 - ls) - (0.5f * d2) * cinv2;
+                const float t = d * cinv2;
+                e.dv = out ? 0.0f : -t;
+                e.dm = (T.dist == MC_DIST_NORMAL) ? t : 0.0f;
+                e.ds = out ? 0.0f : (d2 * cinv2 - 1.0f) * cinv;
+            } else {
+                const float ls = (k2 == SK_CONST) ? T.clogs : logf(sc);
+                const float lgx =
+                    (k1 == SK_SHARED || k2 == SK_SHARED) ? lgamma_norm(T.dist, m, sc) : T.clg;
+                e = elem_eval(T.dist, T.c0, v, m, sc, ls, lgx);
+            }
             lpx = T.wn * e.lp;
 #pragma unroll
             for (int k = 0; k < kLrMaxShared; ++k) {
@@ -637,12 +662,12 @@ MC_DEV void wave_sum8(const float (&v)[8], float (&out)[8]) {
 // ---------------------------------------------------------------------------
 // the sampler
 // ---------------------------------------------------------------------------
-template <int RS, int NSH>
-__global__ void __launch_bounds__(512)
+template <int RS, int NSH, int NW>
+__global__ void __launch_bounds__(64 * NW)
 k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scalars* scal,
          float* st_q, float* st_g, float* samples, TraceDev tr, unsigned long long* xch,
          int* status) {
-    constexpr int NB = kLrNB;
+    constexpr int NB = 2 * NW;  // chains per block: wave w owns chains 2w, 2w + 1
     // record items: 0 lp, 1..NSH shared cotangents, NSH+1 K0, NSH+2 K1; pair
     // 2 item + c (chain c) is granule `pair` of the wave's line
     constexpr int NPAIR = 2 * (NSH + 3), NPASS = (NPAIR + 3) / 4;
@@ -691,10 +716,10 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     const int nsweep = (int)(blk[3] & 255);          // active terms [0, nsweep): swept,
     const int ndirect = (int)((blk[3] >> 8) & 255);  // then ndirect direct terms
     const int nfast = nsweep + ndirect;
-    for (int i = tid; 4 * i < dlen; i += 512)
+    for (int i = tid; 4 * i < dlen; i += 64 * NW)
         *(float4*)(sd + 4 * i) = *(const float4*)(P.data + doff + 4 * i);
     LrSterm* sst = (LrSterm*)(smem + P.sdata_floats);  // the scalar terms, after the block
-    for (int i = tid; i < P.n_sterms * (int)(sizeof(LrSterm) / 16); i += 512)
+    for (int i = tid; i < P.n_sterms * (int)(sizeof(LrSterm) / 16); i += 64 * NW)
         ((float4*)sst)[i] = ((const float4*)P.sterms)[i];
 
     // ---- registers: private slots and the lane's shared parameter ----------------
@@ -923,22 +948,26 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 drift_private(true);
                 lr_sweep<RS>(tt, nsweep, sd, j, R, M);
             }
+            // poll: pass ps, lane x -> pair 4 ps + x / 16, slice x % 16.  The
+            // first round is issued now and checked after the scalar terms
+            unsigned long long* gp = par ? gpoll[1] : gpoll[0];
+            unsigned long long y0[NPASS];
+#pragma unroll
+            for (int ps = 0; ps < NPASS; ++ps)
+                y0[ps] = (poll_lane && 4 * ps + (j >> 4) < NPAIR) ? granule_load(gp + 4 * ps) : 0ull;
             float slp[2] = {0.f, 0.f};
             float sgs[kLrMaxShared][2];
 #pragma unroll
             for (int k = 0; k < kLrMaxShared; ++k) sgs[k][0] = sgs[k][1] = 0.0f;
             lr_scalar_terms(P.n_sterms, sst, sh, j, Dsh, slp, sgs);
             MC_STAMP(7);
-            // poll: pass ps, lane x -> pair 4 ps + x / 16, slice x % 16
-            unsigned long long* gp = par ? gpoll[1] : gpoll[0];
             float vals[NPASS];
             uint32_t need = 0;
 #pragma unroll
             for (int ps = 0; ps < NPASS; ++ps) {
                 vals[ps] = 0.0f;
                 if (poll_lane && 4 * ps + (j >> 4) < NPAIR) {
-                    const unsigned long long y = granule_load(gp + 4 * ps);
-                    if ((uint32_t)(y >> 32) == epoch) vals[ps] = __uint_as_float((uint32_t)y);
+                    if ((uint32_t)(y0[ps] >> 32) == epoch) vals[ps] = __uint_as_float((uint32_t)y0[ps]);
                     else need |= 1u << ps;
                 }
             }
