@@ -72,6 +72,7 @@ struct LanePlan {
     int rs = 1;          // register slots per lane (1, 2 or 4)
     int sdata_floats = 0;
     int32_t shl[kLrMaxShared] = {0, 0, 0, 0};  // shared parameters by ordinal
+    int32_t n_generic = 0;  // scalar terms that are not "own" priors
     std::string why;     // why it does not qualify
     std::vector<LrTerm> terms;
     std::vector<float> data;
@@ -729,6 +730,7 @@ static LrCtx lrctx_of(const mc_program* p) {
     c.sterms = L.d_sterms;
     c.n_terms = (int32_t)p->raw.size();
     c.n_sterms = (int32_t)L.sterms.size();
+    c.n_sterms_generic = L.n_generic;
     c.S = P.S;
     c.Dsh = P.Dsh;
     c.D = p->D;
@@ -923,6 +925,7 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         L.sdata_floats = std::max<int>(L.sdata_floats, (int)blen);
     }
     // the scalar terms, compact (LDS copy in every workgroup)
+    uint32_t own_mask = 0;
     for (const SlTerm& st : SP.sterms) {
         LrSterm x;
         std::memset(&x, 0, sizeof(x));
@@ -936,6 +939,14 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         x.clogs = st.clogs;
         x.clg = st.clg;
         x.wn = st.weight * (float)st.niter;
+        // one "own" prior per shared parameter (lanes.h LrOwn)
+        x.own = st.kind[0] == SK_SHARED &&
+                (st.dist == MC_DIST_NORMAL || st.dist == MC_DIST_HALFNORMAL) &&
+                (st.kind[1] == SK_CONST || st.kind[1] == SK_NONE) && st.kind[2] == SK_CONST &&
+                !(own_mask >> st.jsh[0] & 1);
+        if (x.own) own_mask |= 1u << st.jsh[0];
+        x.cinv = st.kind[2] == SK_CONST ? 1.0f / st.cval[2] : 0.0f;
+        if (!x.own) ++L.n_generic;
         L.sterms.push_back(x);
     }
     L.sdata_floats = (L.sdata_floats + 3) / 4 * 4;  // the scalar terms follow, 16-byte aligned

@@ -80,7 +80,9 @@ struct LrSterm {
     float clogs;    // CONST scale: f32 log(scale)
     float clg;      // gammaln normaliser (constant shapes)
     float wn;       // weight * element count
-    int32_t pad[2];
+    int32_t own;    // a prior of one shared parameter: value shared, Normal /
+                    // HalfNormal with constant loc and scale
+    float cinv;     // CONST scale: 1/scale
 };
 
 struct LrCtx {
@@ -91,6 +93,7 @@ struct LrCtx {
     const LrSterm* sterms;  // scalar terms (constants / shared parameters only)
     int32_t n_terms;
     int32_t n_sterms;
+    int32_t n_sterms_generic;  // scalar terms that are not "own" priors
     int32_t S;
     int32_t Dsh;
     int32_t D;
@@ -115,13 +118,18 @@ MC_DEV float pick4(const float (&a)[kLrMaxShared], int k) {
     for (int kk = 1; kk < kLrMaxShared; ++kk) v = (k == kk) ? a[kk] : v;
     return v;
 }
-// (selects, not an indexed store: a runtime index would put the array in scratch)
+// k is wave-uniform: a branch on it (an indexed store would put the array in
+// scratch, selects would cost 4 adds per call)
 MC_DEV void add4(float (&a)[kLrMaxShared][2], int k, int c, float x) {
-#pragma unroll
-    for (int kk = 0; kk < kLrMaxShared; ++kk) {
-        const float y0 = a[kk][0] + x, y1 = a[kk][1] + x;
-        a[kk][0] = (k == kk && c == 0) ? y0 : a[kk][0];
-        a[kk][1] = (k == kk && c == 1) ? y1 : a[kk][1];
+    k = __builtin_amdgcn_readfirstlane(k);
+    if (k == 0) {
+        if (c) a[0][1] += x; else a[0][0] += x;
+    } else if (k == 1) {
+        if (c) a[1][1] += x; else a[1][0] += x;
+    } else if (k == 2) {
+        if (c) a[2][1] += x; else a[2][0] += x;
+    } else {
+        if (c) a[3][1] += x; else a[3][0] += x;
     }
 }
 
@@ -312,39 +320,40 @@ struct LrCounts {
 };
 
 // Finish the swept terms from their moment sums, and evaluate the direct
-// terms, at the current shared values.
+// terms, at the current shared values.  Both chains at once in packed FP32
+// (every lane operation rounds exactly as its scalar counterpart).
+MC_DEV f2 f2s(float x) { return (f2){x, x}; }
 template <int RS>
 MC_DEV void lr_finish(const MC_CONST LrTerm* tt, int nsweep, int ndirect, LrPriv<RS>& R,
                       const LrShared& sh, const LrMoments<RS>& M, const LrCounts<RS>& K,
-                      float (&lpp)[2], float (&gshp)[kLrMaxShared][2]) {
+                      f2& lpp, float (&gshp)[kLrMaxShared][2]) {
 #pragma unroll
     for (int t = 0; t < kLrSweep; ++t) {
         if (t >= nsweep) break;
         const MC_CONST LrTerm* T = tt + t;
         const int pp = T->pp, j2 = T->jsh[2];
         const bool shs = T->kind[2] == SK_SHARED;
-        const float w = T->weight, c0 = T->c0;
-        float is[2], iv[2], lg[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            is[c] = shs ? rl(sh.is, 2 * j2 + c) : T->cinv;
-            iv[c] = shs ? rl(sh.iv, 2 * j2 + c) : T->cinv2;
-            lg[c] = shs ? rl(sh.lg, 2 * j2 + c) : T->clogs;
-        }
-        float ps[2] = {0.f, 0.f};
+        const f2 w = f2s(T->weight), c0 = f2s(T->c0);
+        const f2 is = shs ? (f2){rl(sh.is, 2 * j2), rl(sh.is, 2 * j2 + 1)} : f2s(T->cinv);
+        const f2 iv = shs ? (f2){rl(sh.iv, 2 * j2), rl(sh.iv, 2 * j2 + 1)} : f2s(T->cinv2);
+        const f2 lg = shs ? (f2){rl(sh.lg, 2 * j2), rl(sh.lg, 2 * j2 + 1)} : f2s(T->clogs);
+        f2 ps = {0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
-            const float cnt = K.cs[t][r];
-            if (cnt == 0.0f) continue;
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const float s1 = M.s1[t][r][c], s2 = M.s2[t][r][c];
-                const float lpt = cnt * (c0 - lg[c]) - (0.5f * s2) * iv[c];
-                lpp[c] += w * lpt;
-                const float u = w * (s1 * iv[c]);
-                R.g[r][c] += (pp == 0) ? -u : u;
-                ps[c] += w * ((s2 * iv[c] - cnt) * is[c]);
+            const float cn = K.cs[t][r];
+            if (cn == 0.0f) continue;
+            const f2 cnt = f2s(cn), s1 = M.s1[t][r], s2 = M.s2[t][r];
+            const f2 lpt = cnt * (c0 - lg) - (f2s(0.5f) * s2) * iv;
+            lpp += w * lpt;
+            const f2 u = w * (s1 * iv);
+            if (pp == 0) {
+                R.g[r][0] += -u[0];
+                R.g[r][1] += -u[1];
+            } else {
+                R.g[r][0] += u[0];
+                R.g[r][1] += u[1];
             }
+            ps += w * ((s2 * iv - cnt) * is);
         }
         if (shs) {
             add4(gshp, j2, 0, ps[0]);
@@ -357,35 +366,32 @@ MC_DEV void lr_finish(const MC_CONST LrTerm* tt, int nsweep, int ndirect, LrPriv
         const MC_CONST LrTerm* T = tt + nsweep + t;
         const int j1 = T->jsh[1], j2 = T->jsh[2];
         const bool shm = T->kind[1] == SK_SHARED, shs = T->kind[2] == SK_SHARED;
-        const float w = T->weight, c0 = T->c0;
-        float um[2], is[2], iv[2], lg[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            um[c] = shm ? rl(sh.q, 2 * j1 + c) : T->cval[1];
-            is[c] = shs ? rl(sh.is, 2 * j2 + c) : T->cinv;
-            iv[c] = shs ? rl(sh.iv, 2 * j2 + c) : T->cinv2;
-            lg[c] = shs ? rl(sh.lg, 2 * j2 + c) : T->clogs;
-        }
-        float pm[2] = {0.f, 0.f}, ps[2] = {0.f, 0.f};
+        const f2 w = f2s(T->weight), c0 = f2s(T->c0);
+        const f2 um = shm ? (f2){rl(sh.q, 2 * j1), rl(sh.q, 2 * j1 + 1)} : f2s(T->cval[1]);
+        const f2 is = shs ? (f2){rl(sh.is, 2 * j2), rl(sh.is, 2 * j2 + 1)} : f2s(T->cinv);
+        const f2 iv = shs ? (f2){rl(sh.iv, 2 * j2), rl(sh.iv, 2 * j2 + 1)} : f2s(T->cinv2);
+        const f2 lg = shs ? (f2){rl(sh.lg, 2 * j2), rl(sh.lg, 2 * j2 + 1)} : f2s(T->clogs);
+        f2 pm = {0.f, 0.f}, ps = {0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             if (!K.pd[t][r]) continue;
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const float d = R.q[r][c] - um[c];
-                const float s2 = fmaf(d, d, 0.0f);
-                const float lpt = 1.0f * (c0 - lg[c]) - (0.5f * s2) * iv[c];
-                lpp[c] += w * lpt;
-                const float u = w * (d * iv[c]);
-                R.g[r][c] += -u;
-                pm[c] += u;
-                ps[c] += w * ((s2 * iv[c] - 1.0f) * is[c]);
-            }
+            const f2 d = (f2){R.q[r][0], R.q[r][1]} - um;
+            const f2 s2 = pk_fma(d, d, f2s(0.0f));
+            const f2 lpt = f2s(1.0f) * (c0 - lg) - (f2s(0.5f) * s2) * iv;
+            lpp += w * lpt;
+            const f2 u = w * (d * iv);
+            R.g[r][0] += -u[0];
+            R.g[r][1] += -u[1];
+            pm += u;
+            ps += w * ((s2 * iv - f2s(1.0f)) * is);
         }
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            if (shm) add4(gshp, j1, c, pm[c]);
-            if (shs) add4(gshp, j2, c, ps[c]);
+        if (shm) {
+            add4(gshp, j1, 0, pm[0]);
+            add4(gshp, j1, 1, pm[1]);
+        }
+        if (shs) {
+            add4(gshp, j2, 0, ps[0]);
+            add4(gshp, j2, 1, ps[1]);
         }
     }
 }
@@ -540,89 +546,88 @@ MC_DEV void lr_eval(const MC_CONST LrTerm* tt, int t0, int nact, const float* sd
     }
 }
 
-// The scalar terms (constants and shared parameters only), lane-parallel
-// from their LDS copy: lane x evaluates term t0 + x / 2 for chain x % 2; the
-// rows are summed per chain with wave_sum8 (a fixed tree: the same sums in
-// every slice, which add them to the exchanged totals).  Results uniform:
-// lp[c], gs[k][c].
+// The scalar terms (constants and shared parameters only).  Priors of one
+// shared parameter ("own" terms) are evaluated by the lane holding that
+// parameter (lane 2k + c): its cotangent stays in the lane, the log p terms
+// are summed over k in order.  Any other scalar term is evaluated
+// lane-parallel from the LDS copy (lane x: term x / 2, chain x % 2) and summed
+// per chain with wave_sum8.  Every slice computes the same sums and adds them
+// to the exchanged totals.  Results: lp[c] (uniform), g_self (this lane's
+// shared parameter, lanes < 2 nsh).
+// The lane's own prior (lanes < 2 Dsh; the planner keeps one per shared
+// parameter), read once per launch.
+struct LrOwn {
+    bool on, hn;            // present; HalfNormal (else Normal)
+    float m, cinv, cinv2;   // constant loc; 1/scale, 1/scale^2
+    float c0l, wn;          // c0 - log(scale); weight * count
+};
+MC_DEV LrOwn lr_own_prior(int n_sterms, const LrSterm* st, int j, int nsh) {
+    LrOwn o = {false, false, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (j >= 2 * nsh) return o;
+    for (int t = 0; t < n_sterms; ++t) {
+        const LrSterm& T = st[t];
+        if (!T.own || (T.jsh & 15) != (j >> 1)) continue;
+        o.on = true;
+        o.hn = T.dist == MC_DIST_HALFNORMAL;
+        o.m = ((T.kinds >> 4) & 15) == SK_CONST ? T.cval[1] : 0.0f;
+        o.cinv = T.cinv;
+        o.cinv2 = T.cinv * T.cinv;
+        o.c0l = T.c0 - T.clogs;
+        o.wn = T.wn;
+        break;
+    }
+    return o;
+}
+
 MC_DEV void wave_sum8(const float (&v)[8], float (&out)[8]);
-MC_DEV void lr_scalar_terms(int n_sterms, const LrSterm* st, const LrShared& sh, int j, int nsh,
-                            float (&lp)[2], float (&gs)[kLrMaxShared][2]) {
-    for (int t0 = 0; t0 < n_sterms; t0 += 32) {
-        const int t = t0 + (j >> 1), c = j & 1;
-        const bool on = t < n_sterms;
-        const LrSterm T = st[on ? t : 0];
+MC_DEV void lr_scalar_terms(int n_sterms, int n_generic, const LrSterm* st, const LrOwn& own,
+                            const LrShared& sh, int j, int nsh, float (&lp)[2], float& g_self) {
+    const int xk = j >> 1;
+    float lp_own = 0.0f, g_own = 0.0f;
+    if (own.on) {
+        // moment form with the constant scale's reciprocals, as the sliced terms
+        const float v = sh.q;
+        const float d = own.hn ? v : v - own.m;
+        const float d2 = d * d;
+        const bool out = own.hn && !(v >= 0.0f);
+        const float lpe = out ? -__builtin_inff() : own.c0l - (0.5f * d2) * own.cinv2;
+        lp_own = own.wn * lpe;
+        g_own = out ? 0.0f : own.wn * -(d * own.cinv2);
+    }
+    for (int k = 0; k < nsh; ++k) {
+        lp[0] += rl(lp_own, 2 * k);
+        lp[1] += rl(lp_own, 2 * k + 1);
+    }
+    g_self = g_own;
+    if (n_generic == 0) return;
+    // other scalar terms: every lane evaluates them for its chain c = j % 2 and
+    // keeps the cotangent of its own shared parameter (k = j / 2); lanes 0 / 1
+    // hold the chains' log p sums (term order)
+    const int c = j & 1;
+    float lpg = 0.0f;
+    for (int t = 0; t < n_sterms; ++t) {
+        const LrSterm& T = st[t];  // uniform address: LDS broadcast
+        if (T.own) continue;
         const int k0 = T.kinds & 15, k1 = (T.kinds >> 4) & 15, k2 = (T.kinds >> 8) & 15;
         const int j0 = T.jsh & 15, j1 = (T.jsh >> 4) & 15, j2 = (T.jsh >> 8) & 15;
-        // chain c's shared values live in lane 2 jsh + c (all lanes active here)
         const float q0 = __shfl(sh.q, 2 * j0 + c), q1 = __shfl(sh.q, 2 * j1 + c);
         const float q2 = __shfl(sh.q, 2 * j2 + c);
-        // the scale's derived values: from the descriptor (constant scale) or
-        // from the lane holding the shared scale
-        const float is2 = __shfl(sh.is, 2 * j2 + c), iv2 = __shfl(sh.iv, 2 * j2 + c);
-        const float lg2 = __shfl(sh.lg, 2 * j2 + c);
-        float lpx = 0.0f, gx[kLrMaxShared] = {0.f, 0.f, 0.f, 0.f};
-        if (on) {
-            const float v = k0 == SK_SHARED ? q0 : (k0 == SK_CONST ? T.cval[0] : 0.f);
-            const float m = k1 == SK_SHARED ? q1 : (k1 == SK_CONST ? T.cval[1] : 0.f);
-            const float sc = k2 == SK_SHARED ? q2 : (k2 == SK_CONST ? T.cval[2] : 0.f);
-            ElemOut e;
-            if (T.dist == MC_DIST_NORMAL || T.dist == MC_DIST_HALFNORMAL) {
-                // moment form with the scale's reciprocals (no divisions), as
-                // the sliced terms: d = value - loc (HalfNormal: the value)
-                const float cinv = k2 == SK_CONST ? 1.0f / T.cval[2] : is2;
-                const float cinv2 = k2 == SK_CONST ? cinv * cinv : iv2;
-                const float ls = k2 == SK_CONST ? T.clogs : lg2;
-                const float d = T.dist == MC_DIST_NORMAL ? v - m : v;
-                const float d2 = d * d;
-                const bool out = T.dist == MC_DIST_HALFNORMAL && !(v >= 0.0f);
-                e.lp = out ? -__builtin_inff() : (T.c0 - ls) - (0.5f * d2) * cinv2;
-                const float t = d * cinv2;
-                e.dv = out ? 0.0f : -t;
-                e.dm = (T.dist == MC_DIST_NORMAL) ? t : 0.0f;
-                e.ds = out ? 0.0f : (d2 * cinv2 - 1.0f) * cinv;
-            } else {
-                const float ls = (k2 == SK_CONST) ? T.clogs : logf(sc);
-                const float lgx =
-                    (k1 == SK_SHARED || k2 == SK_SHARED) ? lgamma_norm(T.dist, m, sc) : T.clg;
-                e = elem_eval(T.dist, T.c0, v, m, sc, ls, lgx);
-            }
-            lpx = T.wn * e.lp;
-#pragma unroll
-            for (int k = 0; k < kLrMaxShared; ++k) {
-                float y = 0.0f;
-                if (k0 == SK_SHARED && j0 == k) y += T.wn * e.dv;
-                if (k1 == SK_SHARED && j1 == k) y += T.wn * e.dm;
-                if (k2 == SK_SHARED && j2 == k) y += T.wn * e.ds;
-                gx[k] = y;
-            }
-        }
-        float v8[8], t8[8];
-        v8[0] = c ? 0.0f : lpx;
-        v8[1] = c ? lpx : 0.0f;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            v8[2 + 2 * k] = c ? 0.0f : gx[k];
-            v8[3 + 2 * k] = c ? gx[k] : 0.0f;
-        }
-        wave_sum8(v8, t8);
-        lp[0] += t8[0];
-        lp[1] += t8[1];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            gs[k][0] += t8[2 + 2 * k];
-            gs[k][1] += t8[3 + 2 * k];
-        }
-        if (nsh > 3) {  // a 4th shared parameter
-            v8[0] = c ? 0.0f : gx[3];
-            v8[1] = c ? gx[3] : 0.0f;
-#pragma unroll
-            for (int x = 2; x < 8; ++x) v8[x] = 0.0f;
-            wave_sum8(v8, t8);
-            gs[3][0] += t8[0];
-            gs[3][1] += t8[1];
-        }
+        const float v = k0 == SK_SHARED ? q0 : (k0 == SK_CONST ? T.cval[0] : 0.f);
+        const float m = k1 == SK_SHARED ? q1 : (k1 == SK_CONST ? T.cval[1] : 0.f);
+        const float sc = k2 == SK_SHARED ? q2 : (k2 == SK_CONST ? T.cval[2] : 0.f);
+        const float ls = (k2 == SK_CONST) ? T.clogs : logf(sc);
+        const float lgx =
+            (k1 == SK_SHARED || k2 == SK_SHARED) ? lgamma_norm(T.dist, m, sc) : T.clg;
+        const ElemOut e = elem_eval(T.dist, T.c0, v, m, sc, ls, lgx);
+        lpg += T.wn * e.lp;
+        float y = 0.0f;
+        if (k0 == SK_SHARED && j0 == xk) y += T.wn * e.dv;
+        if (k1 == SK_SHARED && j1 == xk) y += T.wn * e.dm;
+        if (k2 == SK_SHARED && j2 == xk) y += T.wn * e.ds;
+        g_self += y;
     }
+    lp[0] += rl(lpg, 0);
+    lp[1] += rl(lpg, 1);
 }
 
 // Wave totals of 8 values at once (a fixed tree, the same in every wave):
@@ -755,6 +760,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     __syncthreads();  // the slice block is in LDS
 
     const MC_CONST LrTerm* tt = cptr(P.terms) + (int64_t)slice * P.n_terms;
+    const LrOwn own = lr_own_prior(P.n_sterms, sst, j, Dsh);
     LrCounts<RS> KC;
 #pragma unroll
     for (int t = 0; t < kLrSweep; ++t)
@@ -881,13 +887,14 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             MC_STAMP(0);
             // step l at the point q(l+1): finish the swept terms (shared values
             // of this step are known), evaluate the others
-            float lpp[2] = {0.f, 0.f};
             float gshp[kLrMaxShared][2];
 #pragma unroll
             for (int k = 0; k < kLrMaxShared; ++k) gshp[k][0] = gshp[k][1] = 0.0f;
 #pragma unroll
             for (int r = 0; r < RS; ++r) R.g[r][0] = R.g[r][1] = 0.0f;
-            lr_finish<RS>(tt, nsweep, ndirect, R, sh, M, KC, lpp, gshp);
+            f2 lpp2 = {0.f, 0.f};
+            lr_finish<RS>(tt, nsweep, ndirect, R, sh, M, KC, lpp2, gshp);
+            float lpp[2] = {lpp2[0], lpp2[1]};
             lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp);
             MC_STAMP(1);
             // the wave totals of the record, pair-indexed (2 item + chain)
@@ -955,11 +962,8 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
 #pragma unroll
             for (int ps = 0; ps < NPASS; ++ps)
                 y0[ps] = (poll_lane && 4 * ps + (j >> 4) < NPAIR) ? granule_load(gp + 4 * ps) : 0ull;
-            float slp[2] = {0.f, 0.f};
-            float sgs[kLrMaxShared][2];
-#pragma unroll
-            for (int k = 0; k < kLrMaxShared; ++k) sgs[k][0] = sgs[k][1] = 0.0f;
-            lr_scalar_terms(P.n_sterms, sst, sh, j, Dsh, slp, sgs);
+            float slp[2] = {0.f, 0.f}, sg_self = 0.0f;
+            lr_scalar_terms(P.n_sterms, P.n_sterms_generic, sst, own, sh, j, Dsh, slp, sg_self);
             MC_STAMP(7);
             float vals[NPASS];
             uint32_t need = 0;
@@ -1013,8 +1017,8 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 float gx = 0.0f;
 #pragma unroll
                 for (int k = 0; k < NSH; ++k)
-                    if (xk == k) gx = xc ? tot[2 + 2 * k + 1] + sgs[k][1] : tot[2 + 2 * k] + sgs[k][0];
-                sh.g = xon ? gx : 0.0f;
+                    if (xk == k) gx = xc ? tot[2 + 2 * k + 1] : tot[2 + 2 * k];
+                sh.g = xon ? gx + sg_self : 0.0f;
             }
 #pragma unroll
             for (int c = 0; c < 2; ++c) {

@@ -81,8 +81,28 @@ def model_hier_small(ns):
     return W.hierarchical(ns, G, N)
 
 
+def model_scalar_mix(ns):
+    """Hierarchical model whose scalar terms are not all single-parameter
+    Normal / HalfNormal priors: z ~ Normal(mu, sigma) couples two shared
+    parameters, tau ~ Gamma(2, 1) (the lane-resident kernel's generic scalar path)."""
+    rng = np.random.default_rng(6)
+    G, N = 12, 1200
+    group = (np.arange(N) * G) // N
+    y = (rng.normal(1.0, 1.0, G)[group] + rng.normal(0.0, 0.7, N)).astype(np.float32)
+
+    def lp(p):
+        mu, tau, sigma, z, th = p["mu"], p["tau"], p["sigma"], p["z"], p["theta"]
+        out = ns.Normal(0.0, 5.0).log_prob(mu) + ns.Gamma(2.0, 1.0).log_prob(tau)
+        out = out + ns.HalfNormal(2.0).log_prob(sigma) + ns.Normal(mu, sigma).log_prob(z)
+        out = out + ns.sum(ns.Normal(mu, tau).log_prob(th))
+        return out + ns.sum(ns.Normal(th[group], sigma).log_prob(ns.array(y)))
+
+    return lp, {"mu": 0.5, "tau": 1.0, "sigma": 0.8, "z": 0.3,
+                "theta": np.full(G, 0.9, np.float32)}
+
+
 MODELS = {"iid": model_iid, "scale_vec": model_scale_vec, "value_pp": model_value_pp,
-          "hier_small": model_hier_small}
+          "hier_small": model_hier_small, "scalar_mix": model_scalar_mix}
 
 
 KERNELS = ["interpreter", "lanes"]
