@@ -14,7 +14,7 @@
 //   uniform f32 in (0,1):   ((w >> 9) + 0.5) * 2^-23          (exact in f32)
 //   uniform f64 in (0,1):   (w + 0.5) * 2^-32                  (exact in f64)
 //   normal pair:            double Box-Muller on two f64 uniforms, each
-//                           result rounded once to f32.
+//                           result rounded once to f32 (device: sincospi).
 // Doing Box-Muller and every log/exp that feeds a decision in double and
 // rounding once makes the GPU and the CPU oracle agree bit-for-bit except when
 // a double result lies within ~1 ulp(f64) of an f32 rounding boundary
@@ -72,13 +72,18 @@ MC_HD double mc_u01_f64(uint32_t w) {
     return ((double)w + 0.5) * 2.3283064365386962890625e-10;  // 2^-32
 }
 
-MC_HD void mc_box_muller(uint32_t a, uint32_t b, float* z0, float* z1) {
+// Device only.  cos / sin of 2 pi u2 through sincospi(2 u2) (2 u2 is exact):
+// one call, no Payne-Hanek reduction; the f64 values agree with the oracle's
+// numpy cos / sin(2 pi u2) to ~1 ulp(f64), so the f32 results are identical
+// except within ~1 ulp(f64) of an f32 rounding boundary.
+__device__ inline void mc_box_muller(uint32_t a, uint32_t b, float* z0, float* z1) {
     const double u1 = mc_u01_f64(a);
     const double u2 = mc_u01_f64(b);
     const double r = sqrt(-2.0 * log(u1));
-    const double t = 6.283185307179586 * u2;
-    *z0 = (float)(r * cos(t));
-    *z1 = (float)(r * sin(t));
+    double s, c;
+    sincospi(2.0 * u2, &s, &c);
+    *z0 = (float)(r * c);
+    *z1 = (float)(r * s);
 }
 
 // f32 log / exp "as IEEE would round them": evaluated in double, rounded once.
