@@ -241,6 +241,12 @@ typedef struct mc_trace {
  * NULL.  workspace: mc_hmc_workspace_bytes() bytes of device memory (may be
  * 0 bytes when the per-chain arena fits in LDS).                            */
 int64_t mc_hmc_workspace_bytes(const mc_program* prog, int64_t num_chains);
+/* The lane-resident kernel continues its exchange tags across launches on a
+ * workspace and clears the workspace only the first time it sees its address
+ * (and after another kernel used it or a timeout was reported).  A caller
+ * that frees or repurposes a workspace between sliced HMC launches calls
+ * mc_workspace_release(ws) first.                                           */
+int mc_workspace_release(const void* workspace_dev);
 /* After a sliced mc_hmc_run: MC_OK, or MC_ERR_TIMEOUT if an exchange timed
  * out (the launch then left its chains' state unchanged or partial).
  * Synchronises the stream.  Always MC_OK for an unsliced program.         */

@@ -109,8 +109,22 @@ class ChainSet:
         if nbytes <= 0:
             return None
         if self._ws is None or self._ws.numel() < nbytes:
+            self._release_workspace()
             self._ws = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
         return self._ws
+
+    def _release_workspace(self):
+        """Tell the library a workspace is going away (mc_workspace_release: the
+        sliced kernel's exchange tags continue across launches on one address)."""
+        if self._ws is not None:
+            self.lib.mc_workspace_release(_lib.ptr(self._ws))
+            self._ws = None
+
+    def __del__(self):
+        try:
+            self._release_workspace()
+        except Exception:  # pragma: no cover - interpreter shutdown
+            pass
 
     def _config(self, *, chain_offset, num_warmup, num_samples, iter_begin, iter_count,
                 sample_begin, sample_capacity, seed, step_size, target_accept,

@@ -8,7 +8,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <numeric>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -1627,6 +1629,33 @@ static bool use_lanes(const mc_program* p, const mc_run_config* cfg) {
     return p->lr.ok && p->slice_kernel != 1 && cfg->num_leapfrog_steps > 0;
 }
 
+// Exchange tags of the lane-resident kernel continue across launches on one
+// workspace: a process-wide counter per workspace address hands every launch
+// a fresh tag range, so the granule lines need clearing only the first time
+// the library sees a workspace (or after it is released, reused by another
+// kernel, or the 32-bit counter would wrap) — not ahead of every launch.
+static std::mutex g_ws_mu;
+static std::unordered_map<const void*, uint32_t> g_ws_epoch;
+static void ws_forget(const void* ws) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    g_ws_epoch.erase(ws);
+}
+// Reserve `need` tags on ws: *base = first tag - 1; returns true if the
+// workspace must be cleared first.
+static bool ws_reserve(const void* ws, uint64_t need, uint32_t* base) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    auto it = g_ws_epoch.find(ws);
+    const bool clear = it == g_ws_epoch.end() || (uint64_t)it->second + need >= 0xFFFFFFF0ull;
+    *base = clear ? 0u : it->second;
+    g_ws_epoch[ws] = (uint32_t)(*base + need);
+    return clear;
+}
+
+extern "C" int mc_workspace_release(const void* ws) {
+    if (ws) ws_forget(ws);
+    return MC_OK;
+}
+
 template <int RS, int NSH, int NW>
 static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* state,
                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
@@ -1646,14 +1675,18 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
     const int64_t used = sl_workspace_bytes(p, C);
     int* status = (int*)ws;
     unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
+    const uint64_t per_launch = (uint64_t)cfg->iter_count * cfg->num_leapfrog_steps + 1;
+    const int64_t nlaunch = (groups + gpl - 1) / gpl;
+    uint32_t base = 0;
+    if (ws_reserve(ws, per_launch * (uint64_t)nlaunch, &base))
+        MC_HIP_TRY(hipMemsetAsync(ws, 0, used, st));  // status word and granule lines
     for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
         const int64_t ng = std::min(gpl, groups - g0);
-        MC_HIP_TRY(hipMemsetAsync(g0 == 0 ? ws : (void*)xch, 0,
-                                  g0 == 0 ? used : used - kSlStatusBytes, st));
         hipLaunchKernelGGL((k_hmc_lr<RS, NSH, NW>), dim3((unsigned)(ng * p->sl.S)), dim3(64 * NW),
                            lds, st, ctx, A, g0 * NB, ng, (mc_chain_scalars*)b, (float*)(b + qo),
-                           (float*)(b + go), samples, trace_of(tr), xch, status);
+                           (float*)(b + go), samples, trace_of(tr), xch, status, base);
         MC_HIP_TRY(hipGetLastError());
+        base += (uint32_t)per_launch;
     }
     return MC_OK;
 }
@@ -1676,6 +1709,7 @@ static int launch_hmc_sl(const mc_program* p, const mc_run_config* cfg, void* st
     const int64_t used = sl_workspace_bytes(p, C);
     int* status = (int*)ws;
     unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
+    ws_forget(ws);  // its tags restart at 1: the lane-resident kernel must clear again
     for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
         const int64_t ng = std::min(gpl, groups - g0);
         // the exchange tags restart at 1 in every launch: clear the granules
@@ -1698,7 +1732,10 @@ extern "C" int mc_workspace_status(const mc_program* p, const void* ws, int64_t 
     int v = 0;
     MC_HIP_TRY(hipMemcpyAsync(&v, ws, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
     MC_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    if (v != 0) return fail(MC_ERR_TIMEOUT, "sliced HMC: a cross-workgroup exchange timed out");
+    if (v != 0) {
+        ws_forget(ws);  // the next launch clears the status word and the granules
+        return fail(MC_ERR_TIMEOUT, "sliced HMC: a cross-workgroup exchange timed out");
+    }
     return MC_OK;
 }
 
@@ -1759,6 +1796,7 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
                    ? launch_hmc_sl<16>(p, cfg, state, samples, tr, ws, (hipStream_t)stream)
                    : launch_hmc_sl<8>(p, cfg, state, samples, tr, ws, (hipStream_t)stream);
     }
+    ws_forget(ws);
     const bool lds = hmc_use_lds(p);
     const int64_t need = mc_hmc_workspace_bytes(p, cfg->num_chains);
     if (!lds && (ws == nullptr || ws_bytes < need))
@@ -1821,6 +1859,7 @@ extern "C" int mc_mh_run(const mc_program* p, const mc_run_config* cfg, double p
     const int64_t need = mc_mh_workspace_bytes(p, cfg->num_chains);
     if (!lds && (ws == nullptr || ws_bytes < need))
         return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
+    ws_forget(ws);  // another kernel's data: a later sliced launch clears it
     hipStream_t st = (hipStream_t)stream;
     float* w = (float*)ws;
     const float sc = (float)proposal_scale;  // f32(proposal_scale): MLX's weak scalar
@@ -1871,6 +1910,7 @@ extern "C" int mc_nuts_run(const mc_program* p, const mc_run_config* cfg, void* 
     const int64_t need = mc_nuts_workspace_bytes(p, cfg->num_chains, cfg->max_tree_depth);
     if (ws == nullptr || ws_bytes < need)
         return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
+    ws_forget(ws);  // another kernel's data: a later sliced launch clears it
     hipStream_t st = (hipStream_t)stream;
     float* w = (float*)ws;
     switch (p->wpc) {

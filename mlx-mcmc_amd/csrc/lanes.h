@@ -671,7 +671,7 @@ template <int RS, int NSH, int NW>
 __global__ void __launch_bounds__(64 * NW)
 k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scalars* scal,
          float* st_q, float* st_g, float* samples, TraceDev tr, unsigned long long* xch,
-         int* status) {
+         int* status, uint32_t ebase) {
     constexpr int NB = 2 * NW;  // chains per block: wave w owns chains 2w, 2w + 1
     // record items: 0 lp, 1..NSH shared cotangents, NSH+1 K0, NSH+2 K1; pair
     // 2 item + c (chain c) is granule `pair` of the wave's line
@@ -780,7 +780,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         }
 
     const int L = cfg.num_leapfrog_steps;
-    uint32_t epoch = 0;
+    uint32_t epoch = ebase;  // tags continue across launches (api.hip ws_reserve)
     bool ok = true;
     // granules: one 128-byte line per (wave, slice) record, written by one
     // store instruction of one wave (lane = pair), so a polled line is never
