@@ -131,7 +131,8 @@ int32_t mc_program_waves_per_chain(const mc_program* prog);
  * per leapfrog step.  Results equal the chain-per-workgroup kernel's up to
  * fp32 summation order and do not depend on how chains are split over
  * launches or GPUs.  num_slices: 0 = automatic (the default chosen by
- * mc_program_create: 16 for >= 65536 elements, 8 for >= 16384, else off),
+ * mc_program_create: 16 for >= 65536 elements, 8 for >= 16384, 4 for >= 2048
+ * when the lane-resident kernel takes the layout, else off),
  * 1 = off, 2..64 = that many (MC_ERR_UNSUPPORTED if the program does not
  * qualify).  NUTS, mc_logp_grad and mc_state_init always use the
  * chain-per-workgroup kernels.                                              */
