@@ -491,7 +491,9 @@ class Program:
         """Kernel of a sliced HMC program (mc_program_set_slice_kernel):
         "auto" (lane-resident when the layout qualifies), "interpreter"
         (k_hmc_sl, csrc/sliced.h) or "lanes" (k_hmc_lr, csrc/lanes.h; raises
-        EngineError when the layout does not qualify)."""
+        EngineError when the layout does not qualify).  On an unsliced program
+        "lanes" plans one slice (no exchange) and "auto" / "interpreter" keep
+        the chain-per-workgroup kernel (k_hmc)."""
         _lib.check(_lib.load().mc_program_set_slice_kernel(self.handle,
                                                            self.SLICE_KERNELS[kernel]))
 

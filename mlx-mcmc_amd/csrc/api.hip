@@ -73,6 +73,7 @@ struct LanePlan {
     int ok = 0;          // the sliced program qualifies
     int rs = 1;          // register slots per lane (1, 2 or 4)
     int sdata_floats = 0;
+    int S = 0, Dsh = 0, nitems = 0;  // slice geometry (S = 1: an unsliced program, no exchange)
     int32_t shl[kLrMaxShared] = {0, 0, 0, 0};  // shared parameters by ordinal
     int32_t n_generic = 0;  // scalar terms that are not "own" priors
     std::string why;     // why it does not qualify
@@ -724,7 +725,6 @@ static LrCtx lrctx_of(const mc_program* p) {
     LrCtx c;
     std::memset(&c, 0, sizeof(c));
     const LanePlan& L = p->lr;
-    const SlicePlan& P = p->sl;
     c.terms = L.d_terms;
     c.data = L.d_data;
     c.blocks = L.d_blocks;
@@ -733,10 +733,10 @@ static LrCtx lrctx_of(const mc_program* p) {
     c.n_terms = (int32_t)p->raw.size();
     c.n_sterms = (int32_t)L.sterms.size();
     c.n_sterms_generic = L.n_generic;
-    c.S = P.S;
-    c.Dsh = P.Dsh;
+    c.S = L.S;
+    c.Dsh = L.Dsh;
     c.D = p->D;
-    c.nitems = P.nitems;
+    c.nitems = L.nitems;
     c.sdata_floats = L.sdata_floats;
     c.lp_const = p->lp_const;
     for (int k = 0; k < kLrMaxShared; ++k) c.shl[k] = L.shl[k];
@@ -774,6 +774,9 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
                 return no("a per-element operand reads a broadcast parameter");
     }
     L.rs = rs;
+    L.S = S;
+    L.Dsh = SP.Dsh;
+    L.nitems = SP.nitems;
     for (int k = 0; k < SP.Dsh; ++k) L.shl[k] = part.shl[k];
     L.terms.assign((size_t)S * nT, LrTerm());
     L.blocks.assign(4 * (size_t)S, 0);
@@ -966,6 +969,14 @@ static hipError_t upload(T** dst, const std::vector<T>& v) {
     if (e == hipSuccess) e = hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
     return e;
 }
+static hipError_t upload_lanes(LanePlan& LP) {
+    hipError_t e = upload(&LP.d_terms, LP.terms);
+    if (e == hipSuccess) e = upload(&LP.d_data, LP.data);
+    if (e == hipSuccess) e = upload(&LP.d_blocks, LP.blocks);
+    if (e == hipSuccess) e = upload(&LP.d_gidx, LP.gidx);
+    if (e == hipSuccess && !LP.sterms.empty()) e = upload(&LP.d_sterms, LP.sterms);
+    return e;
+}
 
 // Element count of a program (the planner's size measure).
 static int64_t program_elements(const mc_program* p) {
@@ -1028,11 +1039,7 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
     // the lane-resident layout of the same slices, when the program qualifies
     LanePlan& LP = p->lr;
     if (plan_lanes(p, Q, part, LP) == MC_OK) {
-        e = upload(&LP.d_terms, LP.terms);
-        if (e == hipSuccess) e = upload(&LP.d_data, LP.data);
-        if (e == hipSuccess) e = upload(&LP.d_blocks, LP.blocks);
-        if (e == hipSuccess) e = upload(&LP.d_gidx, LP.gidx);
-        if (e == hipSuccess && !LP.sterms.empty()) e = upload(&LP.d_sterms, LP.sterms);
+        e = upload_lanes(LP);
         if (e != hipSuccess) {
             free_lanes(LP);
             free_slices(p->sl);
@@ -1054,16 +1061,40 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
 extern "C" int mc_program_set_slice_kernel(mc_program* p, int32_t kernel) {
     if (!p) return fail(MC_ERR_INVALID, "program is NULL");
     if (kernel < 0 || kernel > 2) return fail(MC_ERR_INVALID, "slice kernel must be 0, 1 or 2");
+    if (p->sl.S < 2) {
+        // an unsliced program: kernel 2 runs it on the lane-resident kernel
+        // with one slice (no exchange); 0 and 1 keep the chain-per-workgroup kernel
+        free_lanes(p->lr);
+        if (kernel == 2) {
+            SlicePlan P;
+            SlPartition part;
+            int rc = plan_slices(p, 1, P, &part);
+            if (rc != MC_OK) return rc;
+            if (plan_lanes(p, P, part, p->lr) != MC_OK) {
+                const std::string why = p->lr.why;
+                free_lanes(p->lr);
+                p->lr.why = why;
+                return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: %s", why.c_str());
+            }
+            const hipError_t e = upload_lanes(p->lr);
+            if (e != hipSuccess) {
+                free_lanes(p->lr);
+                return fail(e == hipErrorOutOfMemory ? MC_ERR_NOMEM : MC_ERR_HIP,
+                            "lane plan upload failed: %s", hipGetErrorString(e));
+            }
+        }
+        p->slice_kernel = kernel;
+        return MC_OK;
+    }
     if (kernel == 2 && !p->lr.ok)
-        return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: %s",
-                    p->sl.S < 2 ? "program is not sliced" : p->lr.why.c_str());
+        return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: %s", p->lr.why.c_str());
     p->slice_kernel = kernel;
     return MC_OK;
 }
 
 extern "C" int32_t mc_program_slice_kernel(const mc_program* p) {
     if (!p) return -1;
-    if (p->sl.S < 2) return 0;
+    if (p->sl.S < 2) return (p->lr.ok && p->lr.S == 1) ? 2 : 0;
     if (p->slice_kernel == 1 || !p->lr.ok) return 1;
     return 2;
 }
@@ -1612,6 +1643,8 @@ static int device_cus() {
     return cached[dev];
 }
 static bool sliced(const mc_program* p) { return p->sl.S >= 2 && p->sl.d_terms != nullptr; }
+// an unsliced program planned onto the lane-resident kernel (one slice)
+static bool lanes1(const mc_program* p) { return p->sl.S < 2 && p->lr.ok && p->lr.S == 1; }
 static int sl_nb_for(const mc_program* p, int64_t C) {
     return (p->sl.nb_max >= 16 && C > 8) ? 16 : 8;
 }
@@ -1626,14 +1659,16 @@ static int64_t sl_groups_per_launch(const mc_program* p, int64_t C) {
 static constexpr int64_t kSlStatusBytes = 256;
 // waves per workgroup of the lane-resident kernel: 8 (16 chains, two waves per
 // SIMD) for up to 16 slices... 4 (8 chains, one wave per SIMD) for <= 8 slices
-static int lr_nw(const mc_program* p) { return p->sl.S <= 8 ? 4 : 8; }
+static int lr_nw(const mc_program* p) { return p->lr.S <= 8 ? 4 : 8; }
 static int64_t lr_groups_per_launch(const mc_program* p, int64_t C) {
     const int nb = 2 * lr_nw(p);
     const int64_t groups = (C + nb - 1) / nb;
-    const int64_t cap = std::max<int64_t>(1, device_cus() / p->sl.S);
+    if (p->lr.S == 1) return groups;  // no exchange: no co-residency needed
+    const int64_t cap = std::max<int64_t>(1, device_cus() / p->lr.S);
     return std::min(groups, cap);
 }
 static int64_t sl_workspace_bytes(const mc_program* p, int64_t C) {
+    if (lanes1(p)) return kSlStatusBytes;
     const int nb = sl_nb_for(p, C);
     int64_t x = 2 * sl_groups_per_launch(p, C) * p->sl.S * (int64_t)p->sl.nitems * nb * 8;
     if (p->lr.ok)  // either kernel may run on the same workspace (lanes.h: one
@@ -1698,7 +1733,7 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
         MC_HIP_TRY(hipMemsetAsync(ws, 0, used, st));  // status word and granule lines
     for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
         const int64_t ng = std::min(gpl, groups - g0);
-        hipLaunchKernelGGL((k_hmc_lr<RS, NSH, NW>), dim3((unsigned)(ng * p->sl.S)), dim3(64 * NW),
+        hipLaunchKernelGGL((k_hmc_lr<RS, NSH, NW>), dim3((unsigned)(ng * p->lr.S)), dim3(64 * NW),
                            lds, st, ctx, A, g0 * NB, ng, (mc_chain_scalars*)b, (float*)(b + qo),
                            (float*)(b + go), samples, trace_of(tr), xch, status, base);
         MC_HIP_TRY(hipGetLastError());
@@ -1743,7 +1778,7 @@ static int launch_hmc_sl(const mc_program* p, const mc_run_config* cfg, void* st
 extern "C" int mc_workspace_status(const mc_program* p, const void* ws, int64_t bytes,
                                    void* stream) {
     if (!p) return fail(MC_ERR_INVALID, "program is NULL");
-    if (!sliced(p)) return MC_OK;
+    if (!sliced(p) && !lanes1(p)) return MC_OK;
     if (!ws || bytes < kSlStatusBytes) return fail(MC_ERR_INVALID, "bad workspace");
     int v = 0;
     MC_HIP_TRY(hipMemcpyAsync(&v, ws, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
@@ -1758,8 +1793,10 @@ extern "C" int mc_workspace_status(const mc_program* p, const void* ws, int64_t 
 extern "C" int64_t mc_hmc_workspace_bytes(const mc_program* p, int64_t C) {
     if (!p || C < 0) return -1;
     if (sliced(p)) return sl_workspace_bytes(p, C);
-    if (hmc_use_lds(p)) return 0;
-    return C * 5 * (int64_t)dpad_of(p->D) * 4;
+    // (a lanes1 program runs L = 0 configurations on the unsliced kernel)
+    const int64_t x = lanes1(p) ? sl_workspace_bytes(p, C) : 0;
+    if (hmc_use_lds(p)) return x;
+    return std::max(x, C * 5 * (int64_t)dpad_of(p->D) * 4);
 }
 
 template <int WPC, bool LDS>
@@ -1790,14 +1827,14 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
     if (rc) return rc;
     if (cfg->num_leapfrog_steps < 0) return fail(MC_ERR_INVALID, "num_leapfrog_steps < 0");
     if (cfg->num_chains == 0 || cfg->iter_count == 0) return MC_OK;
-    if (sliced(p)) {
+    if (sliced(p) || (lanes1(p) && use_lanes(p, cfg))) {
         const int64_t need = sl_workspace_bytes(p, cfg->num_chains);
         if (ws == nullptr || ws_bytes < need)
             return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
         if (device_cus() <= 0) return fail(MC_ERR_HIP, "no HIP device");
         if (use_lanes(p, cfg)) {
             hipStream_t st = (hipStream_t)stream;
-            const bool n4 = p->sl.Dsh > 3, w4 = lr_nw(p) == 4;
+            const bool n4 = p->lr.Dsh > 3, w4 = lr_nw(p) == 4;
 #define MC_LR(RS_, NSH_)                                                                   \
     return w4 ? launch_hmc_lr<RS_, NSH_, 4>(p, cfg, state, samples, tr, ws, st)            \
               : launch_hmc_lr<RS_, NSH_, 8>(p, cfg, state, samples, tr, ws, st)

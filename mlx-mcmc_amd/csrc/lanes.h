@@ -940,8 +940,8 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             }
             ++epoch;
             const int par = epoch & 1;
-            // publish: lane x < NPAIR stores pair x
-            if (j < NPAIR) {
+            // publish: lane x < NPAIR stores pair x (one slice: nothing to exchange)
+            if (S > 1 && j < NPAIR) {
                 float v = rec[0];
 #pragma unroll
                 for (int x = 1; x < NPAIR; ++x) v = (j == x) ? rec[x] : v;
@@ -961,54 +961,59 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             unsigned long long y0[NPASS];
 #pragma unroll
             for (int ps = 0; ps < NPASS; ++ps)
-                y0[ps] = (poll_lane && 4 * ps + (j >> 4) < NPAIR) ? granule_load(gp + 4 * ps) : 0ull;
+                y0[ps] = (S > 1 && poll_lane && 4 * ps + (j >> 4) < NPAIR) ? granule_load(gp + 4 * ps) : 0ull;
             float slp[2] = {0.f, 0.f}, sg_self = 0.0f;
             lr_scalar_terms(P.n_sterms, P.n_sterms_generic, sst, own, sh, j, Dsh, slp, sg_self);
             MC_STAMP(7);
-            float vals[NPASS];
-            uint32_t need = 0;
+            float tot[4 * NPASS];
+            if (S == 1) {
 #pragma unroll
-            for (int ps = 0; ps < NPASS; ++ps) {
-                vals[ps] = 0.0f;
-                if (poll_lane && 4 * ps + (j >> 4) < NPAIR) {
-                    if ((uint32_t)(y0[ps] >> 32) == epoch) vals[ps] = __uint_as_float((uint32_t)y0[ps]);
-                    else need |= 1u << ps;
-                }
-            }
-            uint32_t spins = 0;
-            while (__ballot(need != 0)) {
-                if (++spins > kSpinLimit) {
-                    ok = false;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
+                for (int x = 0; x < 4 * NPASS; ++x) tot[x] = x < NPAIR ? rec[x] : 0.0f;
+            } else {
+                float vals[NPASS];
+                uint32_t need = 0;
 #pragma unroll
                 for (int ps = 0; ps < NPASS; ++ps) {
-                    if ((need >> ps) & 1u) {
-                        const unsigned long long y = granule_load(gp + 4 * ps);
-                        if ((uint32_t)(y >> 32) == epoch) {
-                            vals[ps] = __uint_as_float((uint32_t)y);
-                            need &= ~(1u << ps);
+                    vals[ps] = 0.0f;
+                    if (poll_lane && 4 * ps + (j >> 4) < NPAIR) {
+                        if ((uint32_t)(y0[ps] >> 32) == epoch) vals[ps] = __uint_as_float((uint32_t)y0[ps]);
+                        else need |= 1u << ps;
+                    }
+                }
+                uint32_t spins = 0;
+                while (__ballot(need != 0)) {
+                    if (++spins > kSpinLimit) {
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                    for (int ps = 0; ps < NPASS; ++ps) {
+                        if ((need >> ps) & 1u) {
+                            const unsigned long long y = granule_load(gp + 4 * ps);
+                            if ((uint32_t)(y >> 32) == epoch) {
+                                vals[ps] = __uint_as_float((uint32_t)y);
+                                need &= ~(1u << ps);
+                            }
                         }
                     }
                 }
-            }
-            if (!ok) {
-                __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            MC_STAMP(3);
-            // slice sums: a fixed 16-lane DPP tree per pair, read from the row's lane 0
-            float tot[4 * NPASS];
+                if (!ok) {
+                    __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                MC_STAMP(3);
+                // slice sums: a fixed 16-lane DPP tree per pair, read from the row's lane 0
 #pragma unroll
-            for (int ps = 0; ps < NPASS; ++ps) {
-                float t = vals[ps];
-                t += dpp_row<0xB1>(t);
-                t += dpp_row<0x4E>(t);
-                t += dpp_row<0x141>(t);
-                t += dpp_row<0x140>(t);
+                for (int ps = 0; ps < NPASS; ++ps) {
+                    float t = vals[ps];
+                    t += dpp_row<0xB1>(t);
+                    t += dpp_row<0x4E>(t);
+                    t += dpp_row<0x141>(t);
+                    t += dpp_row<0x140>(t);
 #pragma unroll
-                for (int row = 0; row < 4; ++row) tot[4 * ps + row] = rl(t, 16 * row);
+                    for (int row = 0; row < 4; ++row) tot[4 * ps + row] = rl(t, 16 * row);
+                }
             }
             // totals: the slice sum plus the scalar terms' sum
             lpn[0] = (tot[0] + slp[0]) + P.lp_const;

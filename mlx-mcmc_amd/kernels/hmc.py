@@ -13,7 +13,8 @@ streams (for sharding chains over GPUs), ``return_info`` also returns a
 chain per workgroup, >= 2 data slices per chain: csrc/sliced.h), and
 ``slice_kernel`` the kernel of a sliced program ("auto": the lane-resident
 csrc/lanes.h when the layout qualifies, "interpreter": csrc/sliced.h,
-"lanes").
+"lanes"; with ``num_slices=1`` "lanes" runs the unsliced program on the
+lane-resident kernel with one slice).
 Vector-valued parameters are supported (the reference's ``float()`` store,
 hmc.py:192, rejects them — SURVEY Q6).
 """

@@ -22,21 +22,24 @@ def main():
     import workloads as W
 
     out = {}
-    # config 2
+    # config 2, on the chain-per-workgroup kernel and on the lane-resident one
     lp, init = W.iso_normal(W.ns_product(), 100)
-    t = time.perf_counter()
-    s, rate, info = m.hmc(lp, init, num_samples=1000, num_warmup=1000, step_size=0.1,
-                          num_leapfrog_steps=10, key=m.random.key(0), num_chains=64,
-                          progress=False, return_info=True)
-    wall = time.perf_counter() - t
-    steps = 64 * 2000 * 10
-    x = s["x"]
-    out["config2_iso100_hmc"] = {
-        "chains": 64, "leapfrog_steps_per_s": steps / (info.warmup_seconds + info.sampling_seconds),
-        "sampling_steps_per_s": 64 * 1000 * 10 / info.sampling_seconds,
-        "wall_s": wall, "accept_rate": float(np.mean(rate)),
-        "mean_abs_mean": float(np.abs(x.mean(axis=(0, 1))).mean()),
-        "mean_var": float(x.var(axis=(0, 1)).mean())}
+    for label, slices, kernel in (("", 0, "auto"), ("_lanes", 1, "lanes")):
+        t = time.perf_counter()
+        s, rate, info = m.hmc(lp, init, num_samples=1000, num_warmup=1000, step_size=0.1,
+                              num_leapfrog_steps=10, key=m.random.key(0), num_chains=64,
+                              progress=False, return_info=True, num_slices=slices,
+                              slice_kernel=kernel)
+        wall = time.perf_counter() - t
+        steps = 64 * 2000 * 10
+        x = s["x"]
+        out["config2_iso100_hmc" + label] = {
+            "chains": 64,
+            "leapfrog_steps_per_s": steps / (info.warmup_seconds + info.sampling_seconds),
+            "sampling_steps_per_s": 64 * 1000 * 10 / info.sampling_seconds,
+            "wall_s": wall, "accept_rate": float(np.mean(rate)),
+            "mean_abs_mean": float(np.abs(x.mean(axis=(0, 1))).mean()),
+            "mean_var": float(x.var(axis=(0, 1)).mean())}
     # config 5
     lp, init = W.illcond_normal(W.ns_product(), 100)
     t = time.perf_counter()

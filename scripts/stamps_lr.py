@@ -26,7 +26,11 @@ C = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 VAR = sys.argv[2] if len(sys.argv) > 2 else "full"
 G, N = W.SHAPES["large"]
 fn, init = W.hierarchical(W.ns_product(), G, N)
-if VAR != "full":  # one term family only (diagnostic)
+SL = 0
+if VAR == "iso100":  # config 2 on the one-slice lane-resident kernel
+    fn, init = W.iso_normal(W.ns_product(), 100)
+    SL = 1
+elif VAR != "full":  # one term family only (diagnostic)
     ns = W.ns_product()
     y, group = W.hierarchical_data(G, N)
 
@@ -40,10 +44,10 @@ if VAR != "full":  # one term family only (diagnostic)
     init = ({"sigma": np.float32(1), "theta": init["theta"]} if VAR == "lik" else
             {"mu": np.float32(1), "tau": np.float32(2), "sigma": np.float32(1),
              "theta": init["theta"]})
-prog = _trace.compile_model(fn, init, slice_kernel="lanes")
+prog = _trace.compile_model(fn, init, slices=SL, slice_kernel="lanes")
 print(f"variant={VAR} slices={prog.num_slices} kernel={prog.slice_kernel} chains={C}")
 cs = _engine.ChainSet(prog, C, prog.layout.flatten(init), 1e-4)
-L = 20
+L = 10 if VAR == "iso100" else 20
 cfg = dict(chain_offset=0, num_warmup=0, num_samples=10, sample_begin=0, sample_capacity=0,
            seed=1, step_size=1e-4, target_accept=0.8, num_leapfrog_steps=L,
            adapt_step_size=False)

@@ -114,8 +114,7 @@ def _run(lp, init, slices, C=8, warm=10, samp=10, L=8, eps=0.02, seed=3, chain_o
     s, rate, info = m.hmc(lp, init, num_samples=samp, num_warmup=warm, step_size=eps,
                           num_leapfrog_steps=L, key=m.random.key(seed), num_chains=C,
                           chain_offset=chain_offset, progress=False, return_info=True,
-                          return_trace=True, num_slices=slices,
-                          slice_kernel=kernel if slices != 1 else "auto")
+                          return_trace=True, num_slices=slices, slice_kernel=kernel)
     return s, info
 
 
@@ -158,6 +157,43 @@ def test_sliced_matches_unsliced(gpu, name, S, kernel):
     for k in a:
         np.testing.assert_allclose(b[k], a[k], rtol=1e-3, atol=1e-4)
     np.testing.assert_allclose(ib.trace["energy"], ia.trace["energy"], rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("name", ["hier_small", "iid", "scalar_mix", "iso100"])
+def test_lanes_one_slice_matches_unsliced(gpu, name):
+    """An unsliced program on the lane-resident kernel (one slice, no
+    exchange; slice_kernel="lanes") against k_hmc: same decisions and step
+    sizes, positions within rtol 1e-3.  (scale_vec and value_pp have more
+    than 256 private parameters: test_lanes_one_slice_selection.)"""
+    if name == "iso100":
+        lp, init = W.iso_normal(W.ns_product(), 100)
+    else:
+        lp, init = MODELS[name](W.ns_product())
+    a, ia = _run(lp, init, 1, C=12)
+    b, ib = _run(lp, init, 1, C=12, kernel="lanes")
+    np.testing.assert_array_equal(ia.trace["accepted"], ib.trace["accepted"])
+    np.testing.assert_array_equal(ia.trace["step_size"], ib.trace["step_size"])
+    for k in a:
+        np.testing.assert_allclose(b[k], a[k], rtol=1e-3, atol=1e-4)
+    np.testing.assert_allclose(ib.trace["energy"], ia.trace["energy"], rtol=1e-4, atol=1e-3)
+
+
+def test_lanes_one_slice_selection(gpu):
+    from mlx_mcmc_amd import _trace
+
+    lp, init = W.iso_normal(W.ns_product(), 100)
+    prog = _trace.compile_model(lp, init)
+    assert prog.num_slices == 1 and prog.slice_kernel == "unsliced"
+    prog.set_slice_kernel("lanes")
+    assert prog.num_slices == 1 and prog.slice_kernel == "lanes"
+    prog.set_slice_kernel("interpreter")
+    assert prog.slice_kernel == "unsliced"
+    from mlx_mcmc_amd import _lib
+
+    big = _trace.compile_model(*model_value_pp(W.ns_product()))   # 500 private parameters
+    with pytest.raises(_lib.EngineError, match="256 private"):
+        big.set_slice_kernel("lanes")
+    assert big.slice_kernel == "unsliced"
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
