@@ -998,6 +998,28 @@ static int auto_slices(const mc_program* p) {
     return 1;
 }
 
+// Plan an unsliced program onto the lane-resident kernel (one slice).
+static int plan_lanes1(mc_program* p) {
+    free_lanes(p->lr);
+    SlicePlan P;
+    SlPartition part;
+    const int rc = plan_slices(p, 1, P, &part);
+    if (rc != MC_OK) return rc;
+    if (plan_lanes(p, P, part, p->lr) != MC_OK) {
+        const std::string why = p->lr.why;
+        free_lanes(p->lr);
+        p->lr.why = why;
+        return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: %s", why.c_str());
+    }
+    const hipError_t e = upload_lanes(p->lr);
+    if (e != hipSuccess) {
+        free_lanes(p->lr);
+        return fail(e == hipErrorOutOfMemory ? MC_ERR_NOMEM : MC_ERR_HIP,
+                    "lane plan upload failed: %s", hipGetErrorString(e));
+    }
+    return MC_OK;
+}
+
 extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
     if (!p) return fail(MC_ERR_INVALID, "program is NULL");
     if (S < 0 || S > 64) return fail(MC_ERR_INVALID, "num_slices must be in [0, 64]");
@@ -1005,7 +1027,13 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
     if (automatic) S = auto_slices(p);
     free_slices(p->sl);
     free_lanes(p->lr);
-    if (S <= 1) return MC_OK;
+    if (S <= 1) {
+        // automatic: the lane-resident kernel with one slice when the program
+        // qualifies (1.4-4.5x k_hmc on D = 2..100 models at 64-1024 chains,
+        // scripts/bench_unsliced.py); an explicit 1 keeps k_hmc
+        if (automatic && p->slice_kernel != 1) (void)plan_lanes1(p);
+        return MC_OK;
+    }
     SlicePlan P;
     SlPartition part;
     int rc = plan_slices(p, S, P, &part);
@@ -1052,6 +1080,7 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
         LP.why = why;
         if (automatic && program_elements(p) < 16384) {  // only worth it on the lanes kernel
             free_slices(p->sl);
+            if (p->slice_kernel != 1) (void)plan_lanes1(p);
             return MC_OK;
         }
     }
@@ -1062,26 +1091,13 @@ extern "C" int mc_program_set_slice_kernel(mc_program* p, int32_t kernel) {
     if (!p) return fail(MC_ERR_INVALID, "program is NULL");
     if (kernel < 0 || kernel > 2) return fail(MC_ERR_INVALID, "slice kernel must be 0, 1 or 2");
     if (p->sl.S < 2) {
-        // an unsliced program: kernel 2 runs it on the lane-resident kernel
-        // with one slice (no exchange); 0 and 1 keep the chain-per-workgroup kernel
+        // an unsliced program: 0 and 2 run it on the lane-resident kernel with
+        // one slice (no exchange) — 0 when it qualifies, 2 or an error; 1 keeps
+        // the chain-per-workgroup kernel (k_hmc)
         free_lanes(p->lr);
-        if (kernel == 2) {
-            SlicePlan P;
-            SlPartition part;
-            int rc = plan_slices(p, 1, P, &part);
-            if (rc != MC_OK) return rc;
-            if (plan_lanes(p, P, part, p->lr) != MC_OK) {
-                const std::string why = p->lr.why;
-                free_lanes(p->lr);
-                p->lr.why = why;
-                return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: %s", why.c_str());
-            }
-            const hipError_t e = upload_lanes(p->lr);
-            if (e != hipSuccess) {
-                free_lanes(p->lr);
-                return fail(e == hipErrorOutOfMemory ? MC_ERR_NOMEM : MC_ERR_HIP,
-                            "lane plan upload failed: %s", hipGetErrorString(e));
-            }
+        if (kernel != 1) {
+            const int rc = plan_lanes1(p);
+            if (rc != MC_OK && kernel == 2) return rc;
         }
         p->slice_kernel = kernel;
         return MC_OK;
@@ -1225,6 +1241,14 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
                 }
             }
         }
+        // constant-shape normalisers (every layout reads them: the sliced
+        // planners copy them from the validated terms)
+        dt.clogs = (dt.op[2].kind == MC_OP_CONST) ? (float)std::log((double)dt.op[2].cval) : 0.0f;
+        dt.clg = 0.0f;
+        if ((dt.dist == MC_DIST_GAMMA && dt.op[1].kind == MC_OP_CONST) ||
+            (dt.dist == MC_DIST_BETA && dt.op[1].kind == MC_OP_CONST &&
+             dt.op[2].kind == MC_OP_CONST))
+            dt.clg = lgamma_norm(dt.dist, dt.op[1].cval, dt.op[2].cval);
         raws.push_back(dt);
         // pass planning: accumulating vector operands with overlapping parameter
         // ranges go to different sweeps
@@ -1269,12 +1293,6 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
         dt.npass = npass;
         dt.pass_masks = masks[0] | (masks[1] << 4) | (masks[2] << 8);
         dt.wave_task = -1;
-        dt.clogs = (dt.op[2].kind == MC_OP_CONST) ? (float)std::log((double)dt.op[2].cval) : 0.0f;
-        dt.clg = 0.0f;
-        if ((dt.dist == MC_DIST_GAMMA && dt.op[1].kind == MC_OP_CONST) ||
-            (dt.dist == MC_DIST_BETA && dt.op[1].kind == MC_OP_CONST &&
-             dt.op[2].kind == MC_OP_CONST))
-            dt.clg = lgamma_norm(dt.dist, dt.op[1].cval, dt.op[2].cval);
         dt.prim_poff = primary >= 0 ? dt.op[primary].poff : 0;
         if (primary >= 0) {
             const int rc = build_segments(dt, dpool, ipool, 64 * wpc);
@@ -1687,9 +1705,21 @@ static bool use_lanes(const mc_program* p, const mc_run_config* cfg) {
 // kernel, or the 32-bit counter would wrap) — not ahead of every launch.
 static std::mutex g_ws_mu;
 static std::unordered_map<const void*, uint32_t> g_ws_epoch;
+// workspaces whose last launch was an exchange kernel (k_hmc_sl / k_hmc_lr):
+// only those hold a status word for mc_workspace_status
+static std::unordered_map<const void*, char> g_ws_status;
 static void ws_forget(const void* ws) {
     std::lock_guard<std::mutex> lk(g_ws_mu);
     g_ws_epoch.erase(ws);
+    g_ws_status.erase(ws);
+}
+static void ws_mark_status(const void* ws) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    g_ws_status[ws] = 1;
+}
+static bool ws_has_status(const void* ws) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    return g_ws_status.count(ws) != 0;
 }
 // Reserve `need` tags on ws: *base = first tag - 1; returns true if the
 // workspace must be cleared first.
@@ -1707,7 +1737,7 @@ extern "C" int mc_workspace_release(const void* ws) {
     return MC_OK;
 }
 
-template <int RS, int NSH, int NW>
+template <int RS, int NSH, int NW, bool X1>
 static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* state,
                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
     int64_t qo, go;
@@ -1718,7 +1748,7 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
     A.cfg = *cfg;
     const LrCtx ctx = lrctx_of(p);
     const size_t lds = (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm);
-    MC_HIP_TRY(allow_lds(k_hmc_lr<RS, NSH, NW>, lds));
+    MC_HIP_TRY(allow_lds(k_hmc_lr<RS, NSH, NW, X1>, lds));
     const int64_t C = cfg->num_chains;
     constexpr int NB = 2 * NW;
     const int64_t groups = (C + NB - 1) / NB;
@@ -1731,9 +1761,10 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
     uint32_t base = 0;
     if (ws_reserve(ws, per_launch * (uint64_t)nlaunch, &base))
         MC_HIP_TRY(hipMemsetAsync(ws, 0, used, st));  // status word and granule lines
+    ws_mark_status(ws);
     for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
         const int64_t ng = std::min(gpl, groups - g0);
-        hipLaunchKernelGGL((k_hmc_lr<RS, NSH, NW>), dim3((unsigned)(ng * p->lr.S)), dim3(64 * NW),
+        hipLaunchKernelGGL((k_hmc_lr<RS, NSH, NW, X1>), dim3((unsigned)(ng * p->lr.S)), dim3(64 * NW),
                            lds, st, ctx, A, g0 * NB, ng, (mc_chain_scalars*)b, (float*)(b + qo),
                            (float*)(b + go), samples, trace_of(tr), xch, status, base);
         MC_HIP_TRY(hipGetLastError());
@@ -1761,6 +1792,7 @@ static int launch_hmc_sl(const mc_program* p, const mc_run_config* cfg, void* st
     int* status = (int*)ws;
     unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
     ws_forget(ws);  // its tags restart at 1: the lane-resident kernel must clear again
+    ws_mark_status(ws);
     for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
         const int64_t ng = std::min(gpl, groups - g0);
         // the exchange tags restart at 1 in every launch: clear the granules
@@ -1778,8 +1810,8 @@ static int launch_hmc_sl(const mc_program* p, const mc_run_config* cfg, void* st
 extern "C" int mc_workspace_status(const mc_program* p, const void* ws, int64_t bytes,
                                    void* stream) {
     if (!p) return fail(MC_ERR_INVALID, "program is NULL");
-    if (!sliced(p) && !lanes1(p)) return MC_OK;
-    if (!ws || bytes < kSlStatusBytes) return fail(MC_ERR_INVALID, "bad workspace");
+    if (!ws || !ws_has_status(ws)) return MC_OK;  // the last launch on ws had no exchange
+    if (bytes < kSlStatusBytes) return fail(MC_ERR_INVALID, "bad workspace");
     int v = 0;
     MC_HIP_TRY(hipMemcpyAsync(&v, ws, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
     MC_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
@@ -1834,10 +1866,11 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
         if (device_cus() <= 0) return fail(MC_ERR_HIP, "no HIP device");
         if (use_lanes(p, cfg)) {
             hipStream_t st = (hipStream_t)stream;
-            const bool n4 = p->lr.Dsh > 3, w4 = lr_nw(p) == 4;
+            const bool n4 = p->lr.Dsh > 3, w4 = lr_nw(p) == 4, x1 = p->lr.S == 1;
 #define MC_LR(RS_, NSH_)                                                                   \
-    return w4 ? launch_hmc_lr<RS_, NSH_, 4>(p, cfg, state, samples, tr, ws, st)            \
-              : launch_hmc_lr<RS_, NSH_, 8>(p, cfg, state, samples, tr, ws, st)
+    return x1 ? launch_hmc_lr<RS_, NSH_, 4, true>(p, cfg, state, samples, tr, ws, st)      \
+         : w4 ? launch_hmc_lr<RS_, NSH_, 4, false>(p, cfg, state, samples, tr, ws, st)     \
+              : launch_hmc_lr<RS_, NSH_, 8, false>(p, cfg, state, samples, tr, ws, st)
             switch (p->lr.rs) {
                 case 1: if (n4) MC_LR(1, 4); else MC_LR(1, 3);
                 case 2: if (n4) MC_LR(2, 4); else MC_LR(2, 3);

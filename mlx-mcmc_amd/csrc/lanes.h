@@ -667,7 +667,9 @@ MC_DEV void wave_sum8(const float (&v)[8], float (&out)[8]) {
 // ---------------------------------------------------------------------------
 // the sampler
 // ---------------------------------------------------------------------------
-template <int RS, int NSH, int NW>
+// X1: a program of one slice (an unsliced program): no exchange — a
+// compile-time flag so the sliced variants keep their register allocation.
+template <int RS, int NSH, int NW, bool X1>
 __global__ void __launch_bounds__(64 * NW)
 k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scalars* scal,
          float* st_q, float* st_g, float* samples, TraceDev tr, unsigned long long* xch,
@@ -941,7 +943,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             ++epoch;
             const int par = epoch & 1;
             // publish: lane x < NPAIR stores pair x (one slice: nothing to exchange)
-            if (S > 1 && j < NPAIR) {
+            if (!X1 && j < NPAIR) {
                 float v = rec[0];
 #pragma unroll
                 for (int x = 1; x < NPAIR; ++x) v = (j == x) ? rec[x] : v;
@@ -961,12 +963,12 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             unsigned long long y0[NPASS];
 #pragma unroll
             for (int ps = 0; ps < NPASS; ++ps)
-                y0[ps] = (S > 1 && poll_lane && 4 * ps + (j >> 4) < NPAIR) ? granule_load(gp + 4 * ps) : 0ull;
+                y0[ps] = (!X1 && poll_lane && 4 * ps + (j >> 4) < NPAIR) ? granule_load(gp + 4 * ps) : 0ull;
             float slp[2] = {0.f, 0.f}, sg_self = 0.0f;
             lr_scalar_terms(P.n_sterms, P.n_sterms_generic, sst, own, sh, j, Dsh, slp, sg_self);
             MC_STAMP(7);
             float tot[4 * NPASS];
-            if (S == 1) {
+            if constexpr (X1) {
 #pragma unroll
                 for (int x = 0; x < 4 * NPASS; ++x) tot[x] = x < NPAIR ? rec[x] : 0.0f;
             } else {

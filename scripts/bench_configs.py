@@ -22,9 +22,9 @@ def main():
     import workloads as W
 
     out = {}
-    # config 2, on the chain-per-workgroup kernel and on the lane-resident one
+    # config 2, automatic (one-slice lane-resident kernel) and on k_hmc (num_slices=1)
     lp, init = W.iso_normal(W.ns_product(), 100)
-    for label, slices, kernel in (("", 0, "auto"), ("_lanes", 1, "lanes")):
+    for label, slices, kernel in (("", 0, "auto"), ("_k_hmc", 1, "auto")):
         t = time.perf_counter()
         s, rate, info = m.hmc(lp, init, num_samples=1000, num_warmup=1000, step_size=0.1,
                               num_leapfrog_steps=10, key=m.random.key(0), num_chains=64,

@@ -84,7 +84,8 @@ def model_hier_small(ns):
 def model_scalar_mix(ns):
     """Hierarchical model whose scalar terms are not all single-parameter
     Normal / HalfNormal priors: z ~ Normal(mu, sigma) couples two shared
-    parameters, tau ~ Gamma(2, 1) (the lane-resident kernel's generic scalar path)."""
+    parameters, tau ~ Gamma(3, 1) (the lane-resident kernel's generic scalar path;
+    a constant shape with a nonzero gammaln normaliser)."""
     rng = np.random.default_rng(6)
     G, N = 12, 1200
     group = (np.arange(N) * G) // N
@@ -92,7 +93,7 @@ def model_scalar_mix(ns):
 
     def lp(p):
         mu, tau, sigma, z, th = p["mu"], p["tau"], p["sigma"], p["z"], p["theta"]
-        out = ns.Normal(0.0, 5.0).log_prob(mu) + ns.Gamma(2.0, 1.0).log_prob(tau)
+        out = ns.Normal(0.0, 5.0).log_prob(mu) + ns.Gamma(3.0, 1.0).log_prob(tau)
         out = out + ns.HalfNormal(2.0).log_prob(sigma) + ns.Normal(mu, sigma).log_prob(z)
         out = out + ns.sum(ns.Normal(mu, tau).log_prob(th))
         return out + ns.sum(ns.Normal(th[group], sigma).log_prob(ns.array(y)))
@@ -101,8 +102,15 @@ def model_scalar_mix(ns):
                 "theta": np.full(G, 0.9, np.float32)}
 
 
+def model_ab_beta(ns):
+    """Only scalar Beta terms with constant shapes (example 03): the
+    normaliser log B(a, b) of every term enters log p."""
+    return W.ab_testing(ns)
+
+
 MODELS = {"iid": model_iid, "scale_vec": model_scale_vec, "value_pp": model_value_pp,
-          "hier_small": model_hier_small, "scalar_mix": model_scalar_mix}
+          "hier_small": model_hier_small, "scalar_mix": model_scalar_mix,
+          "ab_beta": model_ab_beta}
 
 
 KERNELS = ["interpreter", "lanes"]
@@ -159,7 +167,7 @@ def test_sliced_matches_unsliced(gpu, name, S, kernel):
     np.testing.assert_allclose(ib.trace["energy"], ia.trace["energy"], rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("name", ["hier_small", "iid", "scalar_mix", "iso100"])
+@pytest.mark.parametrize("name", ["hier_small", "iid", "scalar_mix", "ab_beta", "iso100"])
 def test_lanes_one_slice_matches_unsliced(gpu, name):
     """An unsliced program on the lane-resident kernel (one slice, no
     exchange; slice_kernel="lanes") against k_hmc: same decisions and step
@@ -182,15 +190,18 @@ def test_lanes_one_slice_selection(gpu):
     from mlx_mcmc_amd import _trace
 
     lp, init = W.iso_normal(W.ns_product(), 100)
-    prog = _trace.compile_model(lp, init)
-    assert prog.num_slices == 1 and prog.slice_kernel == "unsliced"
+    prog = _trace.compile_model(lp, init)          # automatic: one-slice lanes
+    assert prog.num_slices == 1 and prog.slice_kernel == "lanes"
+    prog.set_slice_kernel("interpreter")           # unsliced: k_hmc
+    assert prog.slice_kernel == "unsliced"
     prog.set_slice_kernel("lanes")
     assert prog.num_slices == 1 and prog.slice_kernel == "lanes"
-    prog.set_slice_kernel("interpreter")
+    prog.set_slices(1)                             # an explicit 1: k_hmc
     assert prog.slice_kernel == "unsliced"
     from mlx_mcmc_amd import _lib
 
     big = _trace.compile_model(*model_value_pp(W.ns_product()))   # 500 private parameters
+    assert big.slice_kernel == "unsliced"
     with pytest.raises(_lib.EngineError, match="256 private"):
         big.set_slice_kernel("lanes")
     assert big.slice_kernel == "unsliced"
