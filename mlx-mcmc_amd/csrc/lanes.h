@@ -668,7 +668,7 @@ MC_DEV void wave_sum8(const float (&v)[8], float (&out)[8]) {
 // the sampler
 // ---------------------------------------------------------------------------
 // X1: a program of one slice (an unsliced program): no exchange — a
-// compile-time flag so the sliced variants keep their register allocation.
+// compile-time flag so the sliced variants keep their code and registers.
 template <int RS, int NSH, int NW, bool X1>
 __global__ void __launch_bounds__(64 * NW)
 k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scalars* scal,
@@ -967,45 +967,45 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             float slp[2] = {0.f, 0.f}, sg_self = 0.0f;
             lr_scalar_terms(P.n_sterms, P.n_sterms_generic, sst, own, sh, j, Dsh, slp, sg_self);
             MC_STAMP(7);
+            float vals[NPASS];
+            uint32_t need = 0;
+#pragma unroll
+            for (int ps = 0; ps < NPASS; ++ps) {
+                vals[ps] = 0.0f;
+                if (!X1 && poll_lane && 4 * ps + (j >> 4) < NPAIR) {
+                    if ((uint32_t)(y0[ps] >> 32) == epoch) vals[ps] = __uint_as_float((uint32_t)y0[ps]);
+                    else need |= 1u << ps;
+                }
+            }
+            uint32_t spins = 0;
+            while (__ballot(need != 0)) {
+                if (++spins > kSpinLimit) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                for (int ps = 0; ps < NPASS; ++ps) {
+                    if ((need >> ps) & 1u) {
+                        const unsigned long long y = granule_load(gp + 4 * ps);
+                        if ((uint32_t)(y >> 32) == epoch) {
+                            vals[ps] = __uint_as_float((uint32_t)y);
+                            need &= ~(1u << ps);
+                        }
+                    }
+                }
+            }
+            if (!ok) {
+                __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            MC_STAMP(3);
+            // slice sums: a fixed 16-lane DPP tree per pair, read from the row's lane 0
             float tot[4 * NPASS];
             if constexpr (X1) {
 #pragma unroll
                 for (int x = 0; x < 4 * NPASS; ++x) tot[x] = x < NPAIR ? rec[x] : 0.0f;
             } else {
-                float vals[NPASS];
-                uint32_t need = 0;
-#pragma unroll
-                for (int ps = 0; ps < NPASS; ++ps) {
-                    vals[ps] = 0.0f;
-                    if (poll_lane && 4 * ps + (j >> 4) < NPAIR) {
-                        if ((uint32_t)(y0[ps] >> 32) == epoch) vals[ps] = __uint_as_float((uint32_t)y0[ps]);
-                        else need |= 1u << ps;
-                    }
-                }
-                uint32_t spins = 0;
-                while (__ballot(need != 0)) {
-                    if (++spins > kSpinLimit) {
-                        ok = false;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-                    for (int ps = 0; ps < NPASS; ++ps) {
-                        if ((need >> ps) & 1u) {
-                            const unsigned long long y = granule_load(gp + 4 * ps);
-                            if ((uint32_t)(y >> 32) == epoch) {
-                                vals[ps] = __uint_as_float((uint32_t)y);
-                                need &= ~(1u << ps);
-                            }
-                        }
-                    }
-                }
-                if (!ok) {
-                    __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                MC_STAMP(3);
-                // slice sums: a fixed 16-lane DPP tree per pair, read from the row's lane 0
 #pragma unroll
                 for (int ps = 0; ps < NPASS; ++ps) {
                     float t = vals[ps];
