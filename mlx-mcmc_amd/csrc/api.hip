@@ -1959,12 +1959,27 @@ extern "C" int mc_mh_run(const mc_program* p, const mc_run_config* cfg, double p
     }
 }
 
+// LDS floats per chain group of k_nuts: group scratch, pending words and,
+// with the LDS arena, the trajectory arena
+static int64_t nuts_lds_floats(const mc_program* p, int32_t max_depth, bool lds_arena) {
+    return scratch_of(p) + kNutsLdsWords +
+           (lds_arena ? nuts_arena_vectors(max_depth) * (int64_t)dpad_of(p->D) : 0);
+}
+// The arena goes to LDS when a workgroup's share fits 150 KB (one workgroup
+// per CU: NUTS runs few chains — 64 per GPU in config 5 — so occupancy is not
+// what bounds it; the L2 round trips of a global arena are)
+static constexpr int64_t kNutsLdsBudget = 150 * 1024;
+static bool nuts_use_lds(const mc_program* p, int32_t max_depth) {
+    return cpb_of(p->wpc) * nuts_lds_floats(p, max_depth, true) * 4 <= kNutsLdsBudget;
+}
+
 extern "C" int64_t mc_nuts_workspace_bytes(const mc_program* p, int64_t C, int32_t max_depth) {
     if (!p || C < 0 || max_depth < 0 || max_depth > kMaxTreeDepth) return -1;
+    if (nuts_use_lds(p, max_depth)) return 0;
     return C * nuts_arena_vectors(max_depth) * (int64_t)dpad_of(p->D) * 4;
 }
 
-template <int WPC>
+template <int WPC, bool LDS>
 static int launch_nuts(const mc_program* p, const mc_run_config* cfg, void* state,
                        float* samples, const mc_trace* tr, float* ws, hipStream_t st) {
     int64_t qo, go;
@@ -1974,11 +1989,11 @@ static int launch_nuts(const mc_program* p, const mc_run_config* cfg, void* stat
     A.cfg = *cfg;
     A.dpad = dpad_of(p->D);
     A.scratch_floats = scratch_of(p);
-    A.lds_floats = A.scratch_floats + kNutsLdsWords;
+    A.lds_floats = (int32_t)nuts_lds_floats(p, cfg->max_tree_depth, LDS);
     const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
     const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
-    MC_HIP_TRY(allow_lds(k_nuts<WPC>, lds));
-    hipLaunchKernelGGL(k_nuts<WPC>, dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
+    MC_HIP_TRY(allow_lds(k_nuts<WPC, LDS>, lds));
+    hipLaunchKernelGGL((k_nuts<WPC, LDS>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
                        ctx_of(p), A, (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go),
                        samples, trace_of(tr), ws);
     MC_HIP_TRY(hipGetLastError());
@@ -1994,15 +2009,19 @@ extern "C" int mc_nuts_run(const mc_program* p, const mc_run_config* cfg, void* 
         return fail(MC_ERR_UNSUPPORTED, "max_tree_depth must be in [0, %d]", kMaxTreeDepth);
     if (cfg->num_chains == 0 || cfg->iter_count == 0) return MC_OK;
     const int64_t need = mc_nuts_workspace_bytes(p, cfg->num_chains, cfg->max_tree_depth);
-    if (ws == nullptr || ws_bytes < need)
+    if (need > 0 && (ws == nullptr || ws_bytes < need))
         return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
-    ws_forget(ws);  // another kernel's data: a later sliced launch clears it
+    if (ws) ws_forget(ws);  // another kernel's data: a later sliced launch clears it
     hipStream_t st = (hipStream_t)stream;
     float* w = (float*)ws;
+    const bool lds = nuts_use_lds(p, cfg->max_tree_depth);
     switch (p->wpc) {
-        case 1: return launch_nuts<1>(p, cfg, state, samples, tr, w, st);
-        case 4: return launch_nuts<4>(p, cfg, state, samples, tr, w, st);
-        default: return launch_nuts<8>(p, cfg, state, samples, tr, w, st);
+        case 1: return lds ? launch_nuts<1, true>(p, cfg, state, samples, tr, w, st)
+                           : launch_nuts<1, false>(p, cfg, state, samples, tr, w, st);
+        case 4: return lds ? launch_nuts<4, true>(p, cfg, state, samples, tr, w, st)
+                           : launch_nuts<4, false>(p, cfg, state, samples, tr, w, st);
+        default: return lds ? launch_nuts<8, true>(p, cfg, state, samples, tr, w, st)
+                            : launch_nuts<8, false>(p, cfg, state, samples, tr, w, st);
     }
 }
 

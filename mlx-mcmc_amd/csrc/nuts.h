@@ -66,7 +66,10 @@ MC_DEV bool no_u_turn(const float* qm, const float* qp, const float* rm, const f
 
 MC_DEV int ctz_u32(uint32_t x) { return __builtin_ctz(x); }
 
-template <int WPC>
+// LDS_ARENA: the arena lives in the workgroup's LDS after the group scratch
+// and the pending words (every trajectory vector one LDS round trip away
+// instead of an L2 one); else in the global workspace.
+template <int WPC, bool LDS_ARENA>
 __global__ void __launch_bounds__(WPC >= 4 ? 64 * WPC : 256)
 k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, float* samples,
        TraceDev tr, float* ws) {
@@ -90,7 +93,8 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
     const int D = P.D;
     const int64_t Dp = A.dpad;
     const int MAXJ = cfg.max_tree_depth;
-    float* ar = ws + c * nuts_arena_vectors(MAXJ) * Dp;
+    float* ar = LDS_ARENA ? (base + A.scratch_floats + kNutsLdsWords)
+                          : (ws + c * nuts_arena_vectors(MAXJ) * Dp);
     float* Mq = ar;
     float* Mr = ar + Dp;
     float* Mg = ar + 2 * Dp;

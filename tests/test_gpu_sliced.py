@@ -265,8 +265,9 @@ def test_sliced_posterior(gpu, kernel):
 def test_lanes_launch_split_and_workspace_reuse(gpu):
     """The lane-resident kernel's exchange tags continue across launches on
     one workspace (no clearing between launches): a run split into one launch
-    per iteration equals a single launch, also when another kernel (NUTS)
-    has used the same workspace in between."""
+    per iteration equals a single launch, also when another kernel (the term
+    interpreter, whose tags restart at 1) has used the same workspace in
+    between."""
     import torch
 
     from mlx_mcmc_amd import _engine, _trace
@@ -279,20 +280,21 @@ def test_lanes_launch_split_and_workspace_reuse(gpu):
                seed=11, step_size=0.02, target_accept=0.8, num_leapfrog_steps=6,
                adapt_step_size=True)
 
-    def run(split, nuts_between=False):
+    def run(split, other_between=False):
         cs = _engine.ChainSet(prog, 24, q0, 0.02)
         out = torch.zeros((24, 6, prog.D), dtype=torch.float32, device=cs.device)
         if split:
             for it in range(12):
                 cs.run_hmc(samples=out, iter_begin=it, iter_count=1, **cfg)
-                if nuts_between and it == 5:
+                if other_between and it == 5:
                     other = _engine.ChainSet(prog, 24, q0, 0.02)
-                    other._ws = cs._workspace(cs.lib.mc_nuts_workspace_bytes(
-                        prog.handle, 24, 4))
-                    other.run_nuts(iter_begin=0, iter_count=1, max_tree_depth=4,
-                                   slice_mode=0, **{k: v for k, v in cfg.items()
-                                                    if k != "num_leapfrog_steps"})
-                    other._ws = None
+                    other._ws = cs._ws          # the same workspace
+                    prog.set_slice_kernel("interpreter")
+                    try:
+                        other.run_hmc(iter_begin=0, iter_count=1, **cfg)
+                    finally:
+                        prog.set_slice_kernel("lanes")
+                        other._ws = None
         else:
             cs.run_hmc(samples=out, iter_begin=0, iter_count=12, **cfg)
         torch.cuda.synchronize()
@@ -301,4 +303,4 @@ def test_lanes_launch_split_and_workspace_reuse(gpu):
 
     one = run(False)
     np.testing.assert_array_equal(run(True), one)
-    np.testing.assert_array_equal(run(True, nuts_between=True), one)
+    np.testing.assert_array_equal(run(True, other_between=True), one)
