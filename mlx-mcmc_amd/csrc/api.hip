@@ -1990,7 +1990,14 @@ static int launch_nuts(const mc_program* p, const mc_run_config* cfg, void* stat
     A.dpad = dpad_of(p->D);
     A.scratch_floats = scratch_of(p);
     A.lds_floats = (int32_t)nuts_lds_floats(p, cfg->max_tree_depth, LDS);
-    const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
+    size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
+    // the data pool after the chain groups when it fits as well
+    const size_t dbytes = (p->h_data.size() + 3) / 4 * 16;
+    A.data_lds = 0;
+    if (LDS && lds + dbytes <= (size_t)kNutsLdsBudget) {
+        A.data_lds = (int32_t)p->h_data.size();
+        lds += dbytes;
+    }
     const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
     MC_HIP_TRY(allow_lds(k_nuts<WPC, LDS>, lds));
     hipLaunchKernelGGL((k_nuts<WPC, LDS>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,

@@ -683,6 +683,7 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
 template <int WPC, bool VALUE_ONLY = false>
 MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* g,
                       const Group<WPC>& G, float& lp_acc, const SegScratch& S) {
+    MC_STAMP_DECL
     const bool task = T.wave_task >= 0;
     if (task && (G.tid >> 6) != T.wave_task) return;  // another wave owns it
     const int tid = task ? (G.tid & 63) : G.tid;
@@ -703,6 +704,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                                  ? lgamma_norm(T.dist, um, us)
                                  : T.clg);
 
+    MC_STAMP(20);
     for (int pass = 0; pass < T.npass; ++pass) {
         const uint32_t mask =
             ((T.pass_masks >> (4 * pass)) & 0xFu) & (VALUE_ONLY ? PASS_LP : 0xFu);
@@ -769,6 +771,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                 }
             }
         }
+        MC_STAMP(21);
         if (moments) finish_moments(T, mask, us, ulogs, M, lp_acc, pv, pm, ps);
 
         // broadcast-parameter cotangents: per-wave partials into their slots
@@ -780,6 +783,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
         if ((mask & PASS_LOC) && T.op[1].kind == MC_OP_PSCALAR) flush(T.op[1].slot, pm);
         if ((mask & PASS_SCALE) && T.op[2].kind == MC_OP_PSCALAR) flush(T.op[2].slot, ps);
         if (!VALUE_ONLY && pass + 1 < T.npass) G.sync();  // passes exist because their writes overlap
+        MC_STAMP(22);
     }
 }
 

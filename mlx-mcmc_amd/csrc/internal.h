@@ -81,7 +81,8 @@ struct RunArgs {
     int32_t dpad;          // D rounded up to 16 floats (arena stride unit)
     int32_t lds_floats;    // LDS floats per chain group
     int32_t scratch_floats;  // of which the evaluator's scratch (arena follows)
-    int32_t pad;
+    int32_t data_lds;      // k_nuts: data-pool floats staged in LDS after the
+                           // chain groups (0: the pool is read from global memory)
 };
 
 struct TraceDev {

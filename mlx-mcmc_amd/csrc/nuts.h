@@ -79,6 +79,17 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
     const mc_run_config& cfg = A.cfg;
     const int lc = threadIdx.x / T;
     const int64_t c = (int64_t)blockIdx.x * CPB + lc;
+    // the (read-only) data pool staged in LDS once per workgroup: the tape's
+    // per-element operand loads become LDS reads (before any chain returns)
+    DevCtx Pd = P;
+    if constexpr (LDS_ARENA) {
+        if (A.data_lds > 0) {
+            float* dl = smem + (int64_t)CPB * A.lds_floats;
+            for (int i = threadIdx.x; i < A.data_lds; i += blockDim.x) dl[i] = P.data[i];
+            __syncthreads();
+            Pd.data = dl;
+        }
+    }
     if (c >= cfg.num_chains) return;
 
     Group<WPC> G;
@@ -106,6 +117,7 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
     float* sq = st_q + c * D;  // current sample (theta0 of the next iteration)
     float* sg = st_g + c * D;
 
+    MC_STAMP_INIT
     mc_chain_scalars sc = scal[c];
     float lp = sc.logp;
     double eps = sc.step_size;
@@ -114,6 +126,7 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
     int64_t n_grad = 0;
 
     for (int64_t it = cfg.iter_begin; it < it_end; ++it) {
+        MC_STAMP_DECL
         if (it == cfg.num_warmup) {  // nuts.py:318-319, 328-330
             if (cfg.adapt_step_size) eps = sc.step_size_bar;
             sc.warmup_accept = sc.n_accept;
@@ -180,6 +193,7 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
         int leaves = 0;
         int divergent = 0;
         G.sync();
+        MC_STAMP(14);
 
         while (s && j < MAXJ) {
             const mc_u32x4 rd = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_DEPTH,
@@ -206,7 +220,9 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
                     Eg[jj] = 0.0f;  // the evaluator accumulates into a zeroed gradient
                 }
                 G.sync();
-                const float lpl = eval_lp_grad<WPC>(P, Eq, Eg, G, S, true);
+                MC_STAMP(8);
+                const float lpl = eval_lp_grad<WPC>(Pd, Eq, Eg, G, S, true);
+                MC_STAMP(9);
                 float kl = 0.0f;
                 for (int jj = G.tid; jj < D; jj += T) {
                     const float pj = Er[jj] + h * Eg[jj];
@@ -221,6 +237,7 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
                 alpha_sum += (a < 1.0) ? a : 1.0;
                 n_alpha += 1;
                 if (!s_leaf) divergent += 1;
+                MC_STAMP(10);
 
                 // park the leaf as a candidate and, if it opens a subtree of
                 // level >= 1, as that subtree's first leaf
@@ -243,6 +260,7 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
                 }
                 if (G.tid == 0) pool_lp[f] = lpl;
                 G.sync();
+                MC_STAMP(11);
                 if (!s_leaf) {
                     s_sub = false;
                     break;
@@ -288,6 +306,7 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
                         break;
                     }
                 }
+                MC_STAMP(12);
                 if (!s_sub) break;
                 if (parked) continue;
                 // l reached j: the depth-j subtree is complete
@@ -312,6 +331,7 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
             s = s_sub && no_u_turn<WPC>(Mq, Pq, Mr, Pr, D, G);
             j += 1;
             G.sync();
+            MC_STAMP(13);
         }
 
         const double alpha = alpha_sum / (n_alpha > 1 ? (double)n_alpha : 1.0);
@@ -354,7 +374,9 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
             }
         }
         G.sync();
+        MC_STAMP(15);
     }
+    MC_STAMP_FLUSH
 
     if (G.tid == 0) {
         sc.logp = lp;
