@@ -132,10 +132,11 @@ int32_t mc_program_waves_per_chain(const mc_program* prog);
  * fp32 summation order and do not depend on how chains are split over
  * launches or GPUs.  num_slices: 0 = automatic (the default chosen by
  * mc_program_create: 16 for >= 65536 elements, 8 for >= 16384, 4 for >= 2048
- * when the lane-resident kernel takes the layout, else off),
- * 1 = off, 2..64 = that many (MC_ERR_UNSUPPORTED if the program does not
- * qualify).  NUTS, mc_logp_grad and mc_state_init always use the
- * chain-per-workgroup kernels.                                              */
+ * when the lane-resident kernel takes the layout, else unsliced — and then
+ * planned as ONE slice of the lane-resident kernel when it qualifies),
+ * 1 = off (the chain-per-workgroup kernel k_hmc), 2..64 = that many
+ * (MC_ERR_UNSUPPORTED if the program does not qualify).  NUTS, MH,
+ * mc_logp_grad and mc_state_init always use the chain-per-workgroup kernels. */
 int mc_program_set_slices(mc_program* prog, int32_t num_slices);
 int32_t mc_program_num_slices(const mc_program* prog);
 /* Which kernel runs a sliced HMC program.  kernel: 0 = automatic (the
@@ -146,7 +147,10 @@ int32_t mc_program_num_slices(const mc_program* prog);
  * does not qualify; mc_last_error says why).  mc_program_slice_kernel returns
  * the kernel a launch with L > 0 will use: 0 unsliced, 1 interpreter, 2
  * lane-resident.  Both compute the same sampler; they differ in fp32
- * summation order only.  mc_program_set_slices resets the choice's layout. */
+ * summation order only.  On an unsliced program, 2 plans it as one slice of
+ * the lane-resident kernel (no exchange; an error if it does not qualify), 0
+ * does so when it qualifies and 1 keeps k_hmc.  mc_program_set_slices resets
+ * the choice's layout.                                                      */
 int mc_program_set_slice_kernel(mc_program* prog, int32_t kernel);
 int32_t mc_program_slice_kernel(const mc_program* prog);
 

@@ -40,6 +40,23 @@ def ess_batch(x) -> np.ndarray:
     return np.where(var == 0, float(n), ess)
 
 
+def mcse_batch(x, n_batches: int = 20):
+    """x: [C, S, D] draws -> (MCSE of the pooled mean, MCSE of the pooled
+    variance) per parameter by non-overlapping batch means (n_batches per
+    chain): robust to the antithetic HMC draws for which the reference's
+    autocorrelation rule (compute_ess) gives ESS <= 0.  Test infrastructure
+    for SURVEY 8(d)'s parity rule."""
+    x = np.asarray(x, dtype=np.float64)
+    C, S, D = x.shape
+    b = S // n_batches
+    xb = x[:, :b * n_batches].reshape(C, n_batches, b, D)
+    mean = x.reshape(-1, D).mean(0)
+    m1 = xb.mean(2).reshape(-1, D)                       # batch means
+    m2 = ((xb - mean) ** 2).mean(2).reshape(-1, D)       # batch second moments
+    nb = C * n_batches
+    return m1.std(0, ddof=1) / np.sqrt(nb), m2.std(0, ddof=1) / np.sqrt(nb)
+
+
 def split_rhat(x) -> float:
     """x: [C, S] draws of one scalar -> split R-hat (BDA3 11.4)."""
     x = np.asarray(x, dtype=np.float64)

@@ -186,6 +186,24 @@ def test_lanes_one_slice_matches_unsliced(gpu, name):
     np.testing.assert_allclose(ib.trace["energy"], ia.trace["energy"], rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("C", [1, 3, 17, 100])
+def test_lanes_one_slice_chain_counts(gpu, C):
+    """The automatic one-slice kernel on part-filled and single-chain blocks
+    (dead waves of a workgroup must not store) against k_hmc; L = 0 runs fall
+    back to k_hmc on the same program."""
+    m = _m()
+    lp, init = model_hier_small(W.ns_product())
+    a, ia = _run(lp, init, 1, C=C)
+    b, ib = _run(lp, init, 0, C=C)
+    np.testing.assert_array_equal(ia.trace["accepted"], ib.trace["accepted"])
+    for k in a:
+        np.testing.assert_allclose(b[k], a[k], rtol=1e-3, atol=1e-4)
+    s0, _ = m.hmc(lp, init, num_samples=3, num_warmup=3, num_leapfrog_steps=0,
+                  key=m.random.key(1), num_chains=C, progress=False)
+    for k in s0:
+        assert np.all(np.isfinite(s0[k]))
+
+
 def test_lanes_one_slice_selection(gpu):
     from mlx_mcmc_amd import _trace
 

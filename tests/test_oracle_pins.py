@@ -326,6 +326,28 @@ def test_ess_batch_matches_reference_loop():
 
 
 # ---- split R-hat (BDA3 11.4; the reference has none: README.md:214) ---------------
+def test_mcse_batch_known_answers():
+    """Batch-means MCSE (the posterior-parity tests' error bar): iid draws give
+    sd / sqrt(n) for the mean and sqrt(Var[(x - m)^2] / n) for the variance;
+    an AR(1) series with rho = 0.9 inflates the mean's by sqrt((1 + rho) / (1 - rho))."""
+    from oracle.diag import mcse_batch
+
+    rng = np.random.default_rng(5)
+    x = rng.normal(2.0, 3.0, size=(8, 20000, 1))
+    m, v = mcse_batch(x)
+    n = x.size
+    assert abs(m[0] / (3.0 / np.sqrt(n)) - 1) < 0.15
+    assert abs(v[0] / (np.sqrt(2.0) * 9.0 / np.sqrt(n)) - 1) < 0.15
+    e = rng.normal(size=(8, 20000))
+    ar = np.empty_like(e)
+    ar[:, 0] = e[:, 0]
+    for t in range(1, e.shape[1]):
+        ar[:, t] = 0.9 * ar[:, t - 1] + e[:, t]
+    m_ar, _ = mcse_batch(ar[..., None])
+    sd = np.sqrt(1.0 / (1 - 0.81))
+    assert abs(m_ar[0] / (sd / np.sqrt(ar.size) * np.sqrt(1.9 / 0.1)) - 1) < 0.2
+
+
 def test_split_rhat_known_answers():
     from oracle.diag import split_rhat
 
