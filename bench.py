@@ -54,6 +54,10 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=15,
                     help="processes of the aggregate CPU baseline (0: skip)")
     ap.add_argument("--no-ess", action="store_true")
+    ap.add_argument("--iters-per-launch", type=int, default=50,
+                    help="HMC iterations per sampler launch (hmc() launches its persistent "
+                         "kernel in chunks of 500, or once per phase without progress "
+                         "output); 1 = one launch per step")
     ap.add_argument("--slices", type=int, default=0,
                     help="data slices per chain (0: the engine's automatic choice)")
     ap.add_argument("--slice-kernel", default="auto", choices=["auto", "interpreter", "lanes"],
@@ -176,30 +180,42 @@ def main():
                sample_capacity=K, seed=args.seed, step_size=args.step_size,
                target_accept=0.8, num_leapfrog_steps=L, adapt_step_size=True)
 
+    # launches of B iterations (the last one shorter), in the warmup too, so
+    # that a kernel-trace profile's average duration is the timed launches'
+    B = max(1, args.iters_per_launch)
+
+    def launches(first, count):
+        return [(first + i, min(B, count - i)) for i in range(0, count, B)]
+
     # ---- untimed warmup (step-size adaptation) -------------------------------
-    # one launch per iteration, like the timed region, so that a kernel-trace
-    # profile's average k_hmc duration is the timed launches' duration
-    for it in range(Wm):
-        chains.run_hmc(samples=samples, iter_begin=it, iter_count=1, **cfg)
+    for it0, n in launches(0, Wm):
+        chains.run_hmc(samples=samples, iter_begin=it0, iter_count=n, **cfg)
     torch.cuda.synchronize()
 
-    # ---- timed region: K steps, one launch each --------------------------------
+    # ---- timed region: K steps in launches of B ---------------------------------
     stream = torch.cuda.current_stream()
+    timed = launches(Wm, K)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(K)]
+          for _ in timed]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(K):
-        ev[k][0].record(stream)
-        chains.run_hmc(samples=samples, iter_begin=Wm + k, iter_count=1, **cfg)
-        ev[k][1].record(stream)
+    for (it0, n), (e0, e1) in zip(timed, ev):
+        e0.record(stream)
+        chains.run_hmc(samples=samples, iter_begin=it0, iter_count=n, **cfg)
+        e1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if K else float("nan")
+    # per-iteration kernel time from the full launches (HIP events on the
+    # launch stream)
+    full = [a.elapsed_time(b) for (a, b), (_, n) in zip(ev, timed) if n == B] or \
+           [a.elapsed_time(b) / n for (a, b), (_, n) in zip(ev, timed)]
+    launch_ms = float(np.mean(full)) if K else float("nan")
+    iters_per_launch = B if any(n == B for _, n in timed) else 1
+    kern_ms = launch_ms / iters_per_launch
     elapsed = max_over_ranks(elapsed, device=dev)
 
     sc = chains.scalars()
@@ -228,13 +244,17 @@ def main():
         total_chains = C * world
         steps_total = total_chains * L * K
         value = steps_total / elapsed
-        flops_per_launch = C * L * W.hierarchical_flops_per_step(G, N)
-        achieved = flops_per_launch / (kern_ms * 1e-3) / 1e12
+        flops_per_launch = C * L * W.hierarchical_flops_per_step(G, N) * iters_per_launch
+        achieved = flops_per_launch / (launch_ms * 1e-3) / 1e12
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get(args.shape, {}).get("hbm_bytes_per_launch")
+                rec = json.load(open(pmc)).get(args.shape, {})
+                traffic = rec.get("hbm_bytes_per_launch")
+                # per launch of this run's size (the profile's launches may differ)
+                if traffic is not None:
+                    traffic *= iters_per_launch / rec.get("iters_per_launch", 1)
             except Exception:
                 traffic = None
         out = {
@@ -262,12 +282,15 @@ def main():
                 "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
                 "kernel": kernel_label(prog, C),
                 "kernel_ms": kern_ms,
+                "launch_ms": launch_ms,
+                "iters_per_launch": iters_per_launch,
                 "flops_per_launch": flops_per_launch,
                 "note": ("fp32 VALU bound (SURVEY 8d; vector FP32 peak = f32-MFMA peak 157.3 TF); "
-                         "F = 5N + 13D flops per chain-leapfrog-step, C*L per launch; kernel_ms = "
-                         "HIP events around each launch (the sampler kernel and, when sliced, "
-                         "its exchange-buffer memset); traffic = (2*FETCH_SIZE + WRITE_SIZE) per "
-                         "launch from profiles/pmc_traffic.json"),
+                         "F = 5N + 13D flops per chain-leapfrog-step, C*L per iteration, "
+                         "iters_per_launch iterations per launch; launch_ms = HIP events around "
+                         "each full launch on its stream, kernel_ms = launch_ms per iteration; "
+                         "traffic = (2*FETCH_SIZE + WRITE_SIZE) per launch from "
+                         "profiles/pmc_traffic.json (its launch size in that file)"),
             },
             "accept_rate": accept, "step_size": eps,
             # the data every chain reads per step (8N bytes: y and the

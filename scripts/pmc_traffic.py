@@ -26,6 +26,7 @@ def per_dispatch(d, counter, match):
 
 def main():
     fdir, wdir, shape = sys.argv[1], sys.argv[2], sys.argv[3]
+    ipl = int(sys.argv[4]) if len(sys.argv) > 4 else 1  # bench.py --iters-per-launch
     f = {}
     for kern in ("k_hmc_lr", "k_hmc_sl", "k_hmc"):  # the sampler kernel bench.py ran
         f = per_dispatch(fdir, "FETCH_SIZE", kern)
@@ -39,6 +40,7 @@ def main():
     data[shape] = {
         "kernel": kern,
         "dispatches": [len(f), len(w)],
+        "iters_per_launch": ipl,
         "fetch_kb_per_launch": fk,
         "write_kb_per_launch": wk,
         "hbm_bytes_per_launch": (2.0 * fk + wk) * 1024.0,
