@@ -1677,7 +1677,9 @@ static int64_t sl_groups_per_launch(const mc_program* p, int64_t C) {
 static constexpr int64_t kSlStatusBytes = 256;
 // waves per workgroup of the lane-resident kernel: 8 (16 chains, two waves per
 // SIMD) for up to 16 slices... 4 (8 chains, one wave per SIMD) for <= 8 slices
-static int lr_nw(const mc_program* p) { return p->lr.S <= 8 ? 4 : 8; }
+// one slice: one wave per workgroup (no exchange, so no block structure to
+// keep; a lone wave per CU does not share the scalar unit or LDS with others)
+static int lr_nw(const mc_program* p) { return p->lr.S == 1 ? 1 : (p->lr.S <= 8 ? 4 : 8); }
 static int64_t lr_groups_per_launch(const mc_program* p, int64_t C) {
     const int nb = 2 * lr_nw(p);
     const int64_t groups = (C + nb - 1) / nb;
@@ -1868,7 +1870,7 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
             hipStream_t st = (hipStream_t)stream;
             const bool n4 = p->lr.Dsh > 3, w4 = lr_nw(p) == 4, x1 = p->lr.S == 1;
 #define MC_LR(RS_, NSH_)                                                                   \
-    return x1 ? launch_hmc_lr<RS_, NSH_, 4, true>(p, cfg, state, samples, tr, ws, st)      \
+    return x1 ? launch_hmc_lr<RS_, NSH_, 1, true>(p, cfg, state, samples, tr, ws, st)      \
          : w4 ? launch_hmc_lr<RS_, NSH_, 4, false>(p, cfg, state, samples, tr, ws, st)     \
               : launch_hmc_lr<RS_, NSH_, 8, false>(p, cfg, state, samples, tr, ws, st)
             switch (p->lr.rs) {
