@@ -3,17 +3,23 @@
 Workload (BASELINE.json configs[2], SURVEY §8d "Large"): hierarchical Normal,
 D = 1000 parameters (theta[997], mu, tau, sigma), N = 100,000 observations,
 HMC with L = 20 leapfrog steps, 256 chains per GPU (configs[3] at N = 8: 2048
-chains, 256/GPU; ESS and R-hat reduced over RCCL as [2, D] moment blocks).  One *step* = one HMC iteration
-of every chain on the GPU = one launch of the persistent kernel k_hmc
-(L leapfrog steps, fused gradient tape, accept, sample store).
+chains, 256/GPU; ESS and R-hat reduced over RCCL as [2, D] moment blocks).
+One *step* = one HMC iteration of every chain (L leapfrog steps, fused
+gradient tape, accept, sample store) inside the persistent sampler kernel,
+which is launched in chunks of --iters-per-launch iterations (default 50).
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
-Warmup W = untimed warmup iterations of the sampler (step-size adaptation);
-K timed sampling iterations, each its own launch, bracketed by barrier +
-synchronize; value = sum over ranks of chain-leapfrog-steps / max-over-ranks
-wall time.  Rank 0 prints one JSON line.
+Warmup W = untimed warmup iterations of the sampler (the reference's step-size
+rule, Q4); K timed sampling iterations bracketed by barrier + synchronize;
+value = sum over ranks of chain-leapfrog-steps / max-over-ranks wall time.
+The initial step size defaults to the one the reference's warmup rule reaches
+on this model after the SURVEY's W = 500 (mean over 256 chains,
+profiles/r1/v9_bench.json), so short driver runs (W = 5) sample with moving
+chains instead of the blow-up regime of eps = 0.01.  Rank 0 prints one JSON
+line; a cross-workgroup exchange timeout ends the run with a non-zero status
+and no result line.
 """
 from __future__ import annotations
 
@@ -30,6 +36,9 @@ sys.path.insert(0, ROOT)
 METRIC = "leapfrog-steps/sec (all chains) + ESS/sec, 1000-dim Gaussian @1/2/4/8 GPUs"
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = f32-MFMA peak
 HBM_PEAK_GBS = 8000.0
+# mean step size over 256 chains after the reference's warmup rule (hmc.py:157-170)
+# ran W = 500 iterations from eps0 = 0.01 on the Large model (profiles/r1/v9_bench.json)
+CONVERGED_EPS = 6.1458e-4
 
 
 def _ensure_pkg():
@@ -46,13 +55,18 @@ def parse():
     ap.add_argument("--shape", default="large", choices=["small", "medium", "large"])
     ap.add_argument("--chains", type=int, default=256, help="chains per GPU")
     ap.add_argument("--leapfrog", type=int, default=20)
-    ap.add_argument("--step-size", type=float, default=0.01)
+    ap.add_argument("--step-size", type=float, default=CONVERGED_EPS,
+                    help="initial step size (default: the reference warmup rule's converged "
+                         "value on the Large model after W = 500, profiles/r1/v9_bench.json)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-oracle baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-procs", type=int, default=15,
-                    help="processes of the aggregate CPU baseline (0: skip)")
+    ap.add_argument("--cpu-procs", type=int, default=-1,
+                    help="processes of the aggregate CPU baseline (-1: min(15, cpu count): "
+                         "the GPU box's CPU share is 16 and its process guard allows 16 "
+                         "processes with the GPU device open, which torch's import in each "
+                         "worker counts as, this one included; 0: skip)")
     ap.add_argument("--no-ess", action="store_true")
     ap.add_argument("--iters-per-launch", type=int, default=50,
                     help="HMC iterations per sampler launch (hmc() launches its persistent "
@@ -67,7 +81,27 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(G, N, L, step_size, budget_s, chain=0):
+def cpu_model() -> str:
+    """lscpu's model name of the host."""
+    import subprocess
+
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_single(G, N, L, step_size, budget_s, chain=0):
     """Time the CPU oracle (reference cost structure) on the same model, 1 chain, 1 thread."""
     import torch
 
@@ -95,10 +129,7 @@ def cpu_baseline(G, N, L, step_size, budget_s, chain=0):
             q = qp
         iters += 1
     dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "leapfrog-steps/s", "cores": 1, "kind": "port",
-            "sample": (f"oracle/samplers.py HMC restatement (2 gradients per leapfrog step, "
-                       f"torch-CPU autograd), 1 chain, 1 thread, {iters} iterations x L={L} "
-                       f"on the same D={G + 3}, N={N} model, {dt:.1f} s")}
+    return {"value": steps / dt, "iterations": iters, "seconds": dt}
 
 
 def _cpu_worker(a):
@@ -107,8 +138,7 @@ def _cpu_worker(a):
     import torch
 
     torch.set_num_threads(1)
-    r = cpu_baseline(G, N, L, step_size, budget_s, chain=seed)
-    return r["value"]
+    return cpu_single(G, N, L, step_size, budget_s, chain=seed)["value"]
 
 
 def cpu_aggregate(G, N, L, step_size, budget_s, nproc):
@@ -136,6 +166,35 @@ def cpu_aggregate(G, N, L, step_size, budget_s, nproc):
     return float(sum(vals))
 
 
+def cpu_baseline(G, N, L, step_size, budget_s, nproc, gpu_value):
+    """The `cpu_baseline` object: the oracle's HMC (reference cost structure:
+    two gradients per leapfrog step, a Python iteration loop) on nproc
+    single-thread processes (the baseline the >= 10x target
+    is quoted against), plus one process alone (8d (i))."""
+    one = cpu_single(G, N, L, step_size, budget_s)
+    ncpu = os.cpu_count()
+    out = {"unit": "leapfrog-steps/s", "kind": "port", "cpu_model": cpu_model(),
+           "os_cpu_count": ncpu,
+           "single_thread": {"value": one["value"], "cores": 1,
+                             "gpu_over_cpu": gpu_value / one["value"],
+                             "sample": (f"1 chain, 1 thread, {one['iterations']} iterations x "
+                                        f"L={L}, {one['seconds']:.1f} s")}}
+    if nproc > 0:
+        agg = cpu_aggregate(G, N, L, step_size, budget_s / 2, nproc)
+        out.update(value=agg, cores=nproc, gpu_over_cpu=gpu_value / agg,
+                   sample=(f"oracle/samplers.py HMC restatement (torch-CPU autograd, 2 gradients "
+                           f"per leapfrog step) on the same D={G + 3}, N={N} model at "
+                           f"eps={step_size:.3g}, L={L}: {nproc} spawned single-thread "
+                           f"processes, one chain each, {budget_s / 2:.1f} s each "
+                           f"(SURVEY 8d (ii); the GPU box's CPU share is 16 of os.cpu_count()="
+                           f"{ncpu}, and its process guard caps processes with the GPU device "
+                           f"open at 16, this one included)"))
+    else:
+        out.update(value=one["value"], cores=1, gpu_over_cpu=gpu_value / one["value"],
+                   sample=out["single_thread"]["sample"])
+    return out
+
+
 def kernel_label(prog, C):
     """The sampler kernel a launch runs (rocprof names it the same way)."""
     kind = prog.slice_kernel
@@ -144,6 +203,18 @@ def kernel_label(prog, C):
     if kind == "interpreter":
         return f"k_hmc_sl<{16 if C > 8 else 8}> (S={prog.num_slices} slices)"
     return f"k_hmc<{prog.waves_per_chain}>"
+
+
+def check(chains, where):
+    """A sliced launch whose cross-workgroup exchange timed out skipped work:
+    report it and exit non-zero rather than publish a number for it."""
+    from mlx_mcmc_amd import _lib
+
+    try:
+        chains.check_status()
+    except _lib.EngineError as e:
+        print(f"bench.py: sampler failed in the {where}: {e}", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 def main():
@@ -191,6 +262,7 @@ def main():
     for it0, n in launches(0, Wm):
         chains.run_hmc(samples=samples, iter_begin=it0, iter_count=n, **cfg)
     torch.cuda.synchronize()
+    check(chains, "warmup")
 
     # ---- timed region: K steps in launches of B ---------------------------------
     stream = torch.cuda.current_stream()
@@ -209,6 +281,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    check(chains, "timed region")
     # per-iteration kernel time from the full launches (HIP events on the
     # launch stream)
     full = [a.elapsed_time(b) for (a, b), (_, n) in zip(ev, timed) if n == B] or \
@@ -220,6 +293,8 @@ def main():
 
     sc = chains.scalars()
     accept = float(np.mean(sc["n_accept"] / np.maximum(sc["n_total"], 1)))
+    frozen = int(np.sum(sc["n_accept"] == 0)) if K else 0     # chains that never moved
+    frozen = int(max_over_ranks(float(frozen), device=dev))
     eps = float(np.mean(sc["step_size"]))
 
     # ---- diagnostics on the device (not timed) ----------------------------------
@@ -278,14 +353,15 @@ def main():
                 "waves_per_chain": prog.waves_per_chain, "slices": prog.num_slices,
             },
             "roofline": {
-                "bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
+                "bound": "valu_fp32", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
                 "kernel": kernel_label(prog, C),
                 "kernel_ms": kern_ms,
                 "launch_ms": launch_ms,
                 "iters_per_launch": iters_per_launch,
                 "flops_per_launch": flops_per_launch,
-                "note": ("fp32 VALU bound (SURVEY 8d; vector FP32 peak = f32-MFMA peak 157.3 TF); "
+                "note": ("FP32 VALU bound (SURVEY 8d: no dense contraction, no MFMA; vector FP32 "
+                         "peak 157.3 TF); "
                          "F = 5N + 13D flops per chain-leapfrog-step, C*L per iteration, "
                          "iters_per_launch iterations per launch; launch_ms = HIP events around "
                          "each full launch on its stream, kernel_ms = launch_ms per iteration; "
@@ -299,25 +375,30 @@ def main():
         }
         if gather_ms is not None:
             out["gather_ms"] = gather_ms
+        out["frozen_chains"] = frozen
         if diag is not None:
             ess_sum = diag["ess_sum"]                         # per element, all chains
-            out["ess_per_sec"] = {"min": float(ess_sum.min()) / elapsed,
-                                  "median": float(np.median(ess_sum)) / elapsed,
-                                  "unit": "effective samples/s (sum over chains)",
-                                  "draws": K}
-            out["rhat"] = {"max": float(np.nanmax(diag["rhat"])),
-                           "median": float(np.nanmedian(diag["rhat"])), "split": True}
+            rh = diag["rhat"]
+            if frozen or diag["n_constant"]:
+                # the reference rule scores a constant series as ESS = n: an
+                # ESS/s from chains that never moved would be fiction
+                out["ess_per_sec"] = None
+                out["rhat"] = None
+                out["ess_null_reason"] = (f"{frozen} chains accepted no proposal and "
+                                          f"{diag['n_constant']} series have zero variance "
+                                          f"over the {K} timed draws")
+            else:
+                out["ess_per_sec"] = {"min": float(ess_sum.min()) / elapsed,
+                                      "median": float(np.median(ess_sum)) / elapsed,
+                                      "unit": "effective samples/s (sum over chains)",
+                                      "draws": K}
+                out["rhat"] = ({"max": float(np.nanmax(rh)), "median": float(np.nanmedian(rh)),
+                                "split": True} if np.isfinite(rh).any() else None)
             out["diagnostics_ms"] = diag_ms
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(G, N, L, max(eps, 1e-4), args.cpu_seconds)
-            out["cpu_baseline"]["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
-            if args.cpu_procs > 0:
-                agg = cpu_aggregate(G, N, L, max(eps, 1e-4), args.cpu_seconds / 2, args.cpu_procs)
-                out["cpu_baseline"]["aggregate"] = {
-                    "value": agg, "processes": args.cpu_procs, "unit": "leapfrog-steps/s",
-                    "gpu_over_cpu": value / agg,
-                    "sample": f"{args.cpu_procs} spawned single-thread oracle processes, one "
-                              f"chain each, {args.cpu_seconds / 2:.1f} s each (SURVEY 8d (ii))"}
+            nproc = args.cpu_procs if args.cpu_procs >= 0 else min(15, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(G, N, L, max(eps, 1e-4), args.cpu_seconds, nproc,
+                                               value)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

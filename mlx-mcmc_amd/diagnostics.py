@@ -92,7 +92,8 @@ def chain_diagnostics(samples, max_lag: int = MAX_LAG, group=None) -> Dict[str, 
     """ESS and split R-hat per element of a [C, S, D] buffer.
 
     Returns ``ess`` [C, D] (this rank's chains), ``ess_sum`` [D] (summed over
-    every chain of every rank) and ``rhat`` [D] (NaN unless S >= 4).  With an
+    every chain of every rank), ``rhat`` [D] (NaN unless S >= 4) and
+    ``n_constant`` (series of zero variance over all ranks).  With an
     initialised process group (pass ``group=False`` to stay local) the chain
     sums are all-reduced over the ranks' shards.
     """
@@ -105,12 +106,16 @@ def chain_diagnostics(samples, max_lag: int = MAX_LAG, group=None) -> Dict[str, 
     st = series_stats(x, max_lag)
     red = torch.empty((2, D), dtype=torch.float64, device=x.device)
     _lib.check(lib.mc_stats_reduce(C, S, D, _lib.ptr(st), None, 0, _lib.ptr(red), stream))
-    m_total = torch.tensor([2 * C], dtype=torch.float64, device=x.device)
+    # [split chains, constant series]: a constant series scores ESS = n by
+    # the reference rule, so callers need to know how many there are
+    counts = torch.stack([torch.tensor(2.0 * C, dtype=torch.float64, device=x.device),
+                          (st[_lib.MC_ST_M2] == 0).sum().to(torch.float64)])
     _all_reduce(red, group)
-    _all_reduce(m_total, group)
+    _all_reduce(counts, group)
     ess_sum = red[1].clone()
     rhat = torch.full((D,), float("nan"), dtype=torch.float64, device=x.device)
-    m = int(m_total.item())
+    m_total, n_const = (int(v) for v in counts.tolist())
+    m = m_total
     if S >= 4 and m >= 2:
         center = red[0].contiguous()
         spread = torch.empty((2, D), dtype=torch.float64, device=x.device)
@@ -119,7 +124,8 @@ def chain_diagnostics(samples, max_lag: int = MAX_LAG, group=None) -> Dict[str, 
         _all_reduce(spread, group)
         _lib.check(lib.mc_rhat(D, m, S, _lib.ptr(spread), _lib.ptr(rhat), stream))
     return {"ess": st[_lib.MC_ST_ESS].view(C, D).cpu().numpy(),
-            "ess_sum": ess_sum.cpu().numpy(), "rhat": rhat.cpu().numpy()}
+            "ess_sum": ess_sum.cpu().numpy(), "rhat": rhat.cpu().numpy(),
+            "n_constant": n_const}
 
 
 # ------------------------------------------------------------ summary -----

@@ -133,3 +133,19 @@ def test_gpu_nuts_matches_trace_fixture(gpu):
     same = next((i for i in range(len(d)) if d[i] != n["depth"][i] or lv[i] != n["leaves"][i]),
                 len(d))
     assert same >= 10
+
+
+def test_large_trace_fixture_is_mixed():
+    """tests/golden/hmc_large_trace.npz (scripts/gen_golden_large.py): the
+    oracle's trace at the bench shape mixes accepts and rejects and its
+    chains move (the GPU test in test_gpu_large_parity.py relies on it)."""
+    fx = np.load(os.path.join(GOLD, "hmc_large_trace.npz"), allow_pickle=False)
+    acc = fx["accepted"].astype(bool)
+    assert 0.2 < acc.mean() < 0.95
+    assert acc[:, :12].any() and not acc[:, :12].all()
+    assert np.all(np.ptp(fx["samples"][:, :, 3:], axis=1).max(axis=1) > 0)
+    # log U is the shared Philox stream's accept draw (oracle/philox.py)
+    from oracle import philox as R
+
+    c = int(fx["chains"][2])
+    assert fx["log_u"][2][5] == R.logf_ref(R.uniform(0, c, 5, R.TAG_ACCEPT))
