@@ -252,6 +252,13 @@ int64_t mc_hmc_workspace_bytes(const mc_program* prog, int64_t num_chains);
  * that frees or repurposes a workspace between sliced HMC launches calls
  * mc_workspace_release(ws) first.                                           */
 int mc_workspace_release(const void* workspace_dev);
+
+/* Test hook for the exchange kernels' timeout path (no reference counterpart):
+ * while on != 0, the last workgroup of every sliced HMC launch exits without
+ * publishing, so the other slices of its chain block time out; the launch's
+ * chains of that block keep their state, mc_workspace_status then reports
+ * MC_ERR_TIMEOUT and the next launch on the workspace starts clean.       */
+int mc_debug_exchange_fault(int on);
 /* After a sliced mc_hmc_run: MC_OK, or MC_ERR_TIMEOUT if an exchange timed
  * out (the launch then left its chains' state unchanged or partial).
  * Synchronises the stream.  Always MC_OK for an unsliced program.         */

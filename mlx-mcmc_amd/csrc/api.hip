@@ -8,7 +8,10 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
+#include <tuple>
+#include <type_traits>
 #include <numeric>
 #include <unordered_map>
 #include <string>
@@ -1660,6 +1663,46 @@ static int device_cus() {
     }
     return cached[dev];
 }
+// Exchange kernels (k_hmc_sl, k_hmc_lr with S >= 2) spin on records of the
+// other workgroups of their chain block, so every workgroup of a launch must
+// be resident at once.  They are launched cooperatively (the runtime checks
+// the grid against what the device can hold and runs it only when all of it
+// fits, also beside other work on the device) after an occupancy query of
+// the same kernel, block size and LDS: a launch that cannot be co-resident
+// fails fast with MC_ERR_UNSUPPORTED instead of spinning into MC_ERR_TIMEOUT.
+// MC_COOPERATIVE=0 in the environment selects plain launches (A/B timing).
+static bool coop_enabled() {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = std::getenv("MC_COOPERATIVE");
+        on = (e && e[0] == '0') ? 0 : 1;
+    }
+    return on == 1;
+}
+template <typename... KA, typename... A>
+static hipError_t launch_exchange(void (*k)(KA...), int64_t grid, int block, size_t lds,
+                                  hipStream_t st, A&&... a) {
+    std::tuple<std::decay_t<KA>...> t(std::forward<A>(a)...);
+    void* ptrs[sizeof...(KA)];
+    std::apply([&](auto&... x) {
+        int i = 0;
+        ((ptrs[i++] = (void*)&x), ...);
+    }, t);
+    if (coop_enabled())
+        return hipLaunchCooperativeKernel((const void*)k, dim3((unsigned)grid), dim3(block), ptrs,
+                                          (unsigned)lds, st);
+    return hipLaunchKernel((const void*)k, dim3((unsigned)grid), dim3(block), ptrs, lds, st);
+}
+// workgroups of kernel k (block threads, lds bytes) the device holds at once
+template <typename K>
+static int64_t resident_capacity(K k, int block, size_t lds) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(k), block,
+                                                     lds) != hipSuccess)
+        return -1;
+    return (int64_t)n * device_cus();
+}
+static int g_exchange_fault = 0;  // mc_debug_exchange_fault
 static bool sliced(const mc_program* p) { return p->sl.S >= 2 && p->sl.d_terms != nullptr; }
 // an unsliced program planned onto the lane-resident kernel (one slice)
 static bool lanes1(const mc_program* p) { return p->sl.S < 2 && p->lr.ok && p->lr.S == 1; }
@@ -1706,7 +1749,11 @@ static bool use_lanes(const mc_program* p, const mc_run_config* cfg) {
 // the library sees a workspace (or after it is released, reused by another
 // kernel, or the 32-bit counter would wrap) — not ahead of every launch.
 static std::mutex g_ws_mu;
-static std::unordered_map<const void*, uint32_t> g_ws_epoch;
+struct WsTags {
+    uint32_t epoch;    // last tag handed out
+    uint64_t cleared;  // bytes of the workspace cleared when its tags started
+};
+static std::unordered_map<const void*, WsTags> g_ws_epoch;
 // workspaces whose last launch was an exchange kernel (k_hmc_sl / k_hmc_lr):
 // only those hold a status word for mc_workspace_status
 static std::unordered_map<const void*, char> g_ws_status;
@@ -1723,19 +1770,29 @@ static bool ws_has_status(const void* ws) {
     std::lock_guard<std::mutex> lk(g_ws_mu);
     return g_ws_status.count(ws) != 0;
 }
-// Reserve `need` tags on ws: *base = first tag - 1; returns true if the
-// workspace must be cleared first.
-static bool ws_reserve(const void* ws, uint64_t need, uint32_t* base) {
+// Reserve `need` tags on ws, whose launch uses `bytes` of it: *base = first
+// tag - 1; returns true if the workspace must be cleared first — the first
+// time, when the tags would wrap, or when the launch uses more of it than was
+// cleared (a larger layout after mc_program_set_slices / set_slice_kernel
+// would otherwise read stale words beyond the cleared range).
+static bool ws_reserve(const void* ws, uint64_t need, uint64_t bytes, uint32_t* base) {
     std::lock_guard<std::mutex> lk(g_ws_mu);
     auto it = g_ws_epoch.find(ws);
-    const bool clear = it == g_ws_epoch.end() || (uint64_t)it->second + need >= 0xFFFFFFF0ull;
-    *base = clear ? 0u : it->second;
-    g_ws_epoch[ws] = (uint32_t)(*base + need);
+    const bool clear = it == g_ws_epoch.end() || (uint64_t)it->second.epoch + need >= 0xFFFFFFF0ull ||
+                       bytes > it->second.cleared;
+    *base = clear ? 0u : it->second.epoch;
+    const uint64_t cleared = clear ? bytes : it->second.cleared;
+    g_ws_epoch[ws] = WsTags{(uint32_t)(*base + need), cleared};
     return clear;
 }
 
 extern "C" int mc_workspace_release(const void* ws) {
     if (ws) ws_forget(ws);
+    return MC_OK;
+}
+
+extern "C" int mc_debug_exchange_fault(int on) {
+    g_exchange_fault = on ? 1 : 0;
     return MC_OK;
 }
 
@@ -1760,16 +1817,38 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
     unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
     const uint64_t per_launch = (uint64_t)cfg->iter_count * cfg->num_leapfrog_steps + 1;
     const int64_t nlaunch = (groups + gpl - 1) / gpl;
+    if (!X1) {
+        const int64_t cap = resident_capacity(k_hmc_lr<RS, NSH, NW, X1>, 64 * NW, lds);
+        if (cap < std::min(gpl, groups) * p->lr.S)
+            return fail(MC_ERR_UNSUPPORTED,
+                        "lane-resident HMC: %lld workgroups must be co-resident, the device holds "
+                        "%lld of this kernel", (long long)(std::min(gpl, groups) * p->lr.S),
+                        (long long)cap);
+        A.fault = g_exchange_fault;
+    }
     uint32_t base = 0;
-    if (ws_reserve(ws, per_launch * (uint64_t)nlaunch, &base))
+    if (ws_reserve(ws, per_launch * (uint64_t)nlaunch, (uint64_t)used, &base))
         MC_HIP_TRY(hipMemsetAsync(ws, 0, used, st));  // status word and granule lines
     ws_mark_status(ws);
     for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
         const int64_t ng = std::min(gpl, groups - g0);
-        hipLaunchKernelGGL((k_hmc_lr<RS, NSH, NW, X1>), dim3((unsigned)(ng * p->lr.S)), dim3(64 * NW),
-                           lds, st, ctx, A, g0 * NB, ng, (mc_chain_scalars*)b, (float*)(b + qo),
-                           (float*)(b + go), samples, trace_of(tr), xch, status, base);
-        MC_HIP_TRY(hipGetLastError());
+        const int64_t grid = ng * p->lr.S;
+        if (X1) {
+            hipLaunchKernelGGL((k_hmc_lr<RS, NSH, NW, X1>), dim3((unsigned)grid), dim3(64 * NW),
+                               lds, st, ctx, A, g0 * NB, ng, (mc_chain_scalars*)b,
+                               (float*)(b + qo), (float*)(b + go), samples, trace_of(tr), xch,
+                               status, base);
+            MC_HIP_TRY(hipGetLastError());
+        } else {
+            const hipError_t e = launch_exchange(
+                k_hmc_lr<RS, NSH, NW, X1>, grid, 64 * NW, lds, st, ctx, A, g0 * NB, ng,
+                (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples, trace_of(tr),
+                xch, status, base);
+            if (e == hipErrorCooperativeLaunchTooLarge)
+                return fail(MC_ERR_UNSUPPORTED, "lane-resident HMC: grid of %lld workgroups is "
+                            "too large to be co-resident", (long long)grid);
+            MC_HIP_TRY(e);
+        }
         base += (uint32_t)per_launch;
     }
     return MC_OK;
@@ -1793,6 +1872,12 @@ static int launch_hmc_sl(const mc_program* p, const mc_run_config* cfg, void* st
     const int64_t used = sl_workspace_bytes(p, C);
     int* status = (int*)ws;
     unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
+    const int64_t cap = resident_capacity(k_hmc_sl<NB>, kSlLanes * NB / 2, lds);
+    if (cap < std::min(gpl, groups) * p->sl.S)
+        return fail(MC_ERR_UNSUPPORTED,
+                    "sliced HMC: %lld workgroups must be co-resident, the device holds %lld of "
+                    "this kernel", (long long)(std::min(gpl, groups) * p->sl.S), (long long)cap);
+    A.fault = g_exchange_fault;
     ws_forget(ws);  // its tags restart at 1: the lane-resident kernel must clear again
     ws_mark_status(ws);
     for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
@@ -1801,10 +1886,15 @@ static int launch_hmc_sl(const mc_program* p, const mc_run_config* cfg, void* st
         // (and, first, the status word) ahead of it
         MC_HIP_TRY(hipMemsetAsync(g0 == 0 ? ws : (void*)xch, 0,
                                   g0 == 0 ? used : used - kSlStatusBytes, st));
-        hipLaunchKernelGGL(k_hmc_sl<NB>, dim3((unsigned)(ng * p->sl.S)), dim3(kSlLanes * NB / 2), lds, st, ctx,
-                           A, g0 * NB, ng, (mc_chain_scalars*)b, (float*)(b + qo),
-                           (float*)(b + go), samples, trace_of(tr), xch, status);
-        MC_HIP_TRY(hipGetLastError());
+        const int64_t grid = ng * p->sl.S;
+        const hipError_t e = launch_exchange(k_hmc_sl<NB>, grid, kSlLanes * NB / 2, lds, st, ctx,
+                                             A, g0 * NB, ng, (mc_chain_scalars*)b,
+                                             (float*)(b + qo), (float*)(b + go), samples,
+                                             trace_of(tr), xch, status);
+        if (e == hipErrorCooperativeLaunchTooLarge)
+            return fail(MC_ERR_UNSUPPORTED, "sliced HMC: grid of %lld workgroups is too large "
+                        "to be co-resident", (long long)grid);
+        MC_HIP_TRY(e);
     }
     return MC_OK;
 }
@@ -1840,6 +1930,7 @@ static int launch_hmc(const mc_program* p, const mc_run_config* cfg, void* state
     mc_state_offsets(p, cfg->num_chains, &qo, &go);
     char* b = (char*)state;
     RunArgs A;
+    std::memset(&A, 0, sizeof(A));
     A.cfg = *cfg;
     A.dpad = dpad_of(p->D);
     A.lds_floats = (int32_t)hmc_lds_floats(p, LDS);
@@ -1922,6 +2013,7 @@ static int launch_mh(const mc_program* p, const mc_run_config* cfg, float scale,
     mc_state_offsets(p, cfg->num_chains, &qo, &go);
     char* b = (char*)state;
     RunArgs A;
+    std::memset(&A, 0, sizeof(A));
     A.cfg = *cfg;
     A.dpad = dpad_of(p->D);
     A.lds_floats = (int32_t)mh_lds_floats(p, LDS);
@@ -1988,6 +2080,7 @@ static int launch_nuts(const mc_program* p, const mc_run_config* cfg, void* stat
     mc_state_offsets(p, cfg->num_chains, &qo, &go);
     char* b = (char*)state;
     RunArgs A;
+    std::memset(&A, 0, sizeof(A));
     A.cfg = *cfg;
     A.dpad = dpad_of(p->D);
     A.scratch_floats = scratch_of(p);

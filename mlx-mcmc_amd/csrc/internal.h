@@ -83,6 +83,9 @@ struct RunArgs {
     int32_t scratch_floats;  // of which the evaluator's scratch (arena follows)
     int32_t data_lds;      // k_nuts: data-pool floats staged in LDS after the
                            // chain groups (0: the pool is read from global memory)
+    int32_t fault;         // exchange kernels, test hook (mc_debug_exchange_fault):
+                           // the grid's last workgroup exits at once, so the others
+                           // of its chain block time out
 };
 
 struct TraceDev {

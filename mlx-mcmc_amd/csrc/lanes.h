@@ -680,6 +680,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     constexpr int NPAIR = 2 * (NSH + 3), NPASS = (NPAIR + 3) / 4;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const mc_run_config& cfg = A.cfg;
+    if (!X1 && A.fault && blockIdx.x == gridDim.x - 1) return;  // test hook: never publishes
     const int tid = threadIdx.x;
     const int wave = tid >> 6, j = tid & 63;
     const int S = P.S, D = P.D, Dsh = P.Dsh;

@@ -5,6 +5,10 @@ CPU restatements the device diagnostics (csrc/diag.h) are checked against:
   compute_ess   examples/06_nuts_comparison.py:22-41, verbatim semantics
                 (oracle.samplers.compute_ess); ``ess_batch`` is the same rule
                 vectorised over columns.
+  compute_ess_02  the variant of examples/02_hmc_comparison.py:111-128 that
+                produced the published example-02 ESS (PROGRESS.md:78-80): it
+                stops at the first rho < 0.05 only from lag 2 on, and has no
+                constant-series guard.
   split_rhat    Gelman et al., Bayesian Data Analysis 3rd ed., eq. 11.4 on
                 split chains (first and last floor(S/2) draws).  The
                 reference has no R-hat (roadmap only, README.md:214), so this
@@ -18,6 +22,20 @@ from __future__ import annotations
 import numpy as np
 
 from .samplers import compute_ess  # noqa: F401  (re-exported)
+
+
+def compute_ess_02(samples) -> float:
+    """examples/02_hmc_comparison.py:111-128 (restated)."""
+    x = np.asarray(samples, np.float64)
+    n = len(x)
+    mean = np.mean(x)
+    c0 = np.mean((x - mean) ** 2)
+    acf = []
+    for lag in range(1, min(n // 2, 100)):
+        acf.append(np.mean((x[:-lag] - mean) * (x[lag:] - mean)) / c0)
+        if len(acf) > 1 and acf[-1] < 0.05:
+            break
+    return n / (1 + 2 * np.sum(acf))
 
 
 def ess_batch(x) -> np.ndarray:

@@ -15,13 +15,20 @@ infrastructure, run here on the CPU and committed.
       -(H_prop - H_init), f32 log U of the accept draw, step size, H_init;
       the 15 stored draws [S, D].
   tests/golden/posterior_large.json
-      Posterior moments at the same shape: 16 chains (0..15, seed 0), eps0 =
-      3e-3, W = 300 with the reference's rule, S = 2000; per parameter the
+      Posterior moments at the same shape: 16 chains (0..15, seed 0) at a
+      fixed eps = 2e-3 (accept ~0.9), W = 200, S = 2000; per parameter the
       pooled mean / variance and their batch-means MCSE (oracle/diag.py) —
       north_star's "posterior moments within 1 % of reference" at the
       1000-parameter / 100 K-observation model.
+  tests/golden/posterior_large_adapt.json
+      The same 16 chains with the reference's warmup rule on (eps0 = 3e-3,
+      W = 300, S = 2000): per chain the final step size and the sampling
+      accept rate (the rule leaves chains 0 and 13 at eps = 5.4e-3, past
+      stability, where they never accept again — SURVEY Q4), and the pooled
+      moments of all 16 chains (informational: frozen chains are no
+      posterior draws).
 
-    python scripts/gen_golden_large.py [trace|posterior|all]
+    python scripts/gen_golden_large.py [trace|posterior|adapt|all]
 """
 import json
 import os
@@ -35,8 +42,10 @@ GOLD = os.path.join(ROOT, "tests", "golden")
 TRACE = dict(num_samples=15, num_warmup=15, step_size=3e-3, num_leapfrog_steps=20,
              adapt_step_size=True, target_accept=0.8)
 TRACE_CHAINS = (0, 1, 77, 255)
-POST = dict(num_samples=2000, num_warmup=300, step_size=3e-3, num_leapfrog_steps=20,
-            adapt_step_size=True, target_accept=0.8)
+POST = dict(num_samples=2000, num_warmup=200, step_size=2e-3, num_leapfrog_steps=20,
+            adapt_step_size=False, target_accept=0.8)
+ADAPT = dict(num_samples=2000, num_warmup=300, step_size=3e-3, num_leapfrog_steps=20,
+             adapt_step_size=True, target_accept=0.8)
 POST_CHAINS = 16
 
 
@@ -52,7 +61,7 @@ def _run(job):
 
     kind, chain = job
     lp, init = W.hierarchical(W.ns_oracle(), *W.SHAPES["large"])
-    cfg = TRACE if kind == "trace" else POST
+    cfg = {"trace": TRACE, "posterior": POST, "adapt": ADAPT}[kind]
     r = S.hmc(lp, init, seed=0, chain=chain, record=(kind == "trace"), **cfg)
     out = {"samples": r.samples, "step_size": r.step_size, "accept_rate": r.accept_rate}
     if kind == "trace":
@@ -83,18 +92,19 @@ def trace(pool):
     print("wrote", path, "accept fraction per chain", acc.mean(1))
 
 
-def posterior(pool):
+def posterior(pool, kind="posterior"):
     import numpy as np
 
     from oracle.diag import ess_batch, mcse_batch
 
-    res = pool.map(_run, [("posterior", c) for c in range(POST_CHAINS)])
+    cfg = POST if kind == "posterior" else ADAPT
+    res = pool.map(_run, [(kind, c) for c in range(POST_CHAINS)])
     res = sorted(res, key=lambda t: t[1])
     x = np.stack([o["samples"] for _, _, o in res]).astype(np.float64)   # [C, S, D]
     pooled = x.reshape(-1, x.shape[-1])
     mcse_m, mcse_v = mcse_batch(x)
     ess = np.sum([ess_batch(xc) for xc in x], axis=0)
-    out = {"hmc": dict(POST, chains=POST_CHAINS, seed=0,
+    out = {"hmc": dict(cfg, chains=POST_CHAINS, seed=0,
                        model="hierarchical large (G=997, N=100000), workloads.hierarchical; "
                              "layout order mu, tau, sigma, theta[0..996]",
                        final_step_size=[float(o["step_size"]) for _, _, o in res],
@@ -102,7 +112,8 @@ def posterior(pool):
            "hmc_moments": {"mean": pooled.mean(0).tolist(), "var": pooled.var(0).tolist(),
                            "ess_reference_rule": ess.tolist(), "mcse_mean": mcse_m.tolist(),
                            "mcse_var": mcse_v.tolist()}}
-    path = os.path.join(GOLD, "posterior_large.json")
+    path = os.path.join(GOLD, "posterior_large.json" if kind == "posterior"
+                        else "posterior_large_adapt.json")
     with open(path, "w") as f:
         json.dump(out, f)
     print("wrote", path, "final eps", out["hmc"]["final_step_size"],
@@ -116,6 +127,8 @@ def main():
             trace(pool)
         if what in ("posterior", "all"):
             posterior(pool)
+        if what in ("adapt", "all"):
+            posterior(pool, "adapt")
 
 
 if __name__ == "__main__":

@@ -97,6 +97,8 @@ def test_validation_errors_before_device_work():
                                3, ctypes.byref(h))
     assert rc == _lib.MC_ERR_INVALID and b"out of range" in lib.mc_last_error()
     assert lib.mc_abi_version() == 1
+    # host-side switch of the exchange kernels' timeout test hook
+    assert lib.mc_debug_exchange_fault(0) == 0
     assert lib.mc_rng_fill(0, 0, 0, 0, 0, 0, 1, 9, None, None) == _lib.MC_ERR_INVALID
 
 

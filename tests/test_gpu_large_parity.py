@@ -22,7 +22,7 @@ interpreter, and the unsliced k_hmc — and for the fixture's chains:
 
 TIE: H is a float32 sum of ~100 K terms of magnitude ~1.4e5 (ulp 2^-6); the
 GPU sums per slice / per lane, the oracle (torch) in its own order, so each
-H may differ by a few ulp of |H|.  TIE = 8 ulp(|H_init|) (0.125 at this
+H may differ by a few ulp of |H|.  TIE = 8 ulp(|H_init|) (tests/_near_tie.py) (0.125 at this
 shape) bounds |ratio_gpu - ratio_ref| (asserted, so the bound is checked,
 not assumed; measured on MI355X: at most 3 ulp, and chain 77 diverges at
 iteration 16 where |log U - ratio| = 0.0093, below one ulp).
@@ -34,12 +34,11 @@ import numpy as np
 import pytest
 
 import workloads as W
+from _near_tie import compare_trace
 
 pytestmark = pytest.mark.gpu
 
 FIXTURE = os.path.join(os.path.dirname(__file__), "golden", "hmc_large_trace.npz")
-TIE_ULPS = 8
-BLOWUP = 1e3     # |log ratio| beyond which the proposal is a diverged trajectory
 
 
 def _fixture():
@@ -47,42 +46,6 @@ def _fixture():
     out = {k: fx[k] for k in fx.files}
     out["config"] = json.loads(str(out["config"]))
     return out
-
-
-def tie_bound(energy):
-    return TIE_ULPS * np.spacing(np.abs(np.float32(energy))).astype(np.float64)
-
-
-def compare_trace(gpu, ref, W_, label):
-    """Decisions / ratios / step sizes of one chain; returns the number of
-    iterations that agree (up to a proven near-tie, or all)."""
-    n = len(ref["accepted"])
-    worst = 0.0
-    for i in range(n):
-        tie = tie_bound(ref["energy"][i])
-        rg, rr = float(gpu["ratio"][i]), float(ref["ratio"][i])
-        if not np.isfinite(rr) or rr < -BLOWUP:
-            # a diverged trajectory (the rule raised eps past stability):
-            # chaotic in its last digits, but both sides must see it
-            assert not np.isfinite(rg) or rg < -BLOWUP, \
-                f"{label} it {i}: oracle trajectory diverged ({rr}), GPU ratio {rg}"
-        else:
-            assert abs(rg - rr) <= tie, \
-                f"{label} it {i}: ratio {rg} vs oracle {rr} (tie {tie})"
-            worst = max(worst, abs(rg - rr))
-        assert abs(float(gpu["energy"][i]) - float(ref["energy"][i])) <= tie, \
-            f"{label} it {i}: H_init {gpu['energy'][i]} vs oracle {ref['energy'][i]}"
-        assert float(gpu["step_size"][i]) == float(ref["step_size"][i]), \
-            f"{label} it {i}: step size {gpu['step_size'][i]} vs {ref['step_size'][i]}"
-        if bool(gpu["accepted"][i]) != bool(ref["accepted"][i]):
-            gap = abs(float(ref["log_u"][i]) - float(ref["ratio"][i]))
-            assert gap <= tie, (f"{label} it {i}: decisions differ but |log U - ratio| = "
-                                f"{gap} > {tie}: not a near-tie")
-            print(f"{label}: {i} of {n} iterations agree, near-tie at {i} (gap {gap:.4f}), "
-                  f"max |ratio diff| {worst:.4f}")
-            return i
-    print(f"{label}: all {n} iterations agree, max |ratio diff| {worst:.4f}")
-    return n
 
 
 @pytest.mark.parametrize("kernel", ["lanes", "interpreter", "unsliced"])
@@ -108,7 +71,7 @@ def test_large_hmc_trace_matches_oracle(gpu, kernel):
         ref = {k: fx[k][j] for k in ("accepted", "ratio", "log_u", "step_size", "energy")}
         gpu_c = {"accepted": tr["accepted"][c], "ratio": tr["accept_stat"][c],
                  "step_size": tr["step_size"][c], "energy": tr["energy"][c]}
-        same = compare_trace(gpu_c, ref, Wm, f"{kernel} chain {c}")
+        same = compare_trace(gpu_c, ref, f"{kernel} chain {c}", verbose=True)
         seen_acc += int(np.sum(ref["accepted"][:same]))
         seen_rej += int(same - np.sum(ref["accepted"][:same]))
         ns = max(0, same - Wm)                 # stored draws before any divergence

@@ -260,19 +260,31 @@ def test_sliced_large_matches_unsliced(gpu, kernel):
     chains move (eps0 = 3e-3, the reference's rule acting at i = 11..14; at
     eps = 0.01 every trajectory diverges and every proposal is rejected, which
     would compare nothing): decisions, step sizes and energies agree, and the
-    decisions are a mix.  The oracle comparison at this shape is
+    decisions are a mix.  The two kernels sum the log density in different
+    orders, so a decision may flip at a proven near-tie (tests/_near_tie.py);
+    draws are compared up to it.  The oracle comparison at this shape is
     tests/test_gpu_large_parity.py."""
+    from _near_tie import compare_trace, log_u
+
     G, N = W.SHAPES["large"]
     lp, init = W.hierarchical(W.ns_product(), G, N)
     a, ia = _run(lp, init, 1, C=16, warm=15, samp=15, L=20, eps=3e-3)
     b, ib = _run(lp, init, 0, C=16, warm=15, samp=15, L=20, eps=3e-3, kernel=kernel)
     acc = ia.trace["accepted"].astype(bool)
     assert 0 < acc.mean() < 1, "the regime must mix accepts and rejects"
-    np.testing.assert_array_equal(ia.trace["accepted"], ib.trace["accepted"])
-    np.testing.assert_array_equal(ia.trace["step_size"], ib.trace["step_size"])
-    np.testing.assert_allclose(ib.trace["energy"], ia.trace["energy"], rtol=1e-6)
-    for k in a:
-        np.testing.assert_allclose(b[k], a[k], rtol=1e-4, atol=1e-5)
+    full = 0
+    for c in range(16):
+        ref = {"accepted": ia.trace["accepted"][c], "ratio": ia.trace["accept_stat"][c],
+               "energy": ia.trace["energy"][c], "step_size": ia.trace["step_size"][c],
+               "log_u": log_u(3, c, 30)}
+        got = {"accepted": ib.trace["accepted"][c], "ratio": ib.trace["accept_stat"][c],
+               "energy": ib.trace["energy"][c], "step_size": ib.trace["step_size"][c]}
+        same = compare_trace(got, ref, f"{kernel} chain {c}")
+        full += same == 30
+        ns = max(0, same - 15)
+        for k in a:
+            np.testing.assert_allclose(b[k][c, :ns], a[k][c, :ns], rtol=1e-4, atol=1e-5)
+    assert full >= 12, "most chains agree over the whole run"
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -331,3 +343,56 @@ def test_lanes_launch_split_and_workspace_reuse(gpu):
     one = run(False)
     np.testing.assert_array_equal(run(True), one)
     np.testing.assert_array_equal(run(True, other_between=True), one)
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_exchange_timeout_reported_and_state_kept(gpu, kernel):
+    """The exchange kernels' timeout path (include/mcmc355.h,
+    mc_workspace_status / mc_debug_exchange_fault): with the grid's last
+    workgroup never publishing, the other slices of its chain block time out.
+    mc_workspace_status then reports MC_ERR_TIMEOUT; the chains of the
+    stranded block keep their state (positions and counters as before the
+    launch), every other chain equals an undisturbed run; the next launch on
+    the same workspace runs clean."""
+    import torch
+
+    from mlx_mcmc_amd import _engine, _lib, _trace
+
+    lp, init = model_hier_small(W.ns_product())
+    prog = _trace.compile_model(lp, init, slices=4, slice_kernel=kernel)
+    q0 = prog.layout.flatten(init)
+    cfg = dict(chain_offset=0, num_warmup=4, num_samples=0, sample_begin=0, sample_capacity=0,
+               seed=5, step_size=0.02, target_accept=0.8, num_leapfrog_steps=6,
+               adapt_step_size=True)
+    lib = _lib.load()
+
+    ref = _engine.ChainSet(prog, 40, q0, 0.02)
+    ref.run_hmc(iter_begin=0, iter_count=4, **cfg)
+    torch.cuda.synchronize()
+    ref.check_status()
+
+    cs = _engine.ChainSet(prog, 40, q0, 0.02)
+    cs.run_hmc(iter_begin=0, iter_count=2, **cfg)
+    torch.cuda.synchronize()
+    cs.check_status()
+    before_q = cs.positions().cpu().numpy().copy()
+    before_n = cs.scalars()["n_total"].copy()
+    lib.mc_debug_exchange_fault(1)
+    try:
+        cs.run_hmc(iter_begin=2, iter_count=2, **cfg)
+        torch.cuda.synchronize()
+        with pytest.raises(_lib.EngineError, match="timed out"):
+            cs.check_status()
+    finally:
+        lib.mc_debug_exchange_fault(0)
+    after_q = cs.positions().cpu().numpy()
+    after_n = cs.scalars()["n_total"]
+    ref_q = ref.positions().cpu().numpy()
+    kept = np.all(after_q == before_q, axis=1) & (after_n == before_n)
+    done = np.all(after_q == ref_q, axis=1) & (after_n == before_n + 2)
+    assert np.all(kept | done), "every chain is either untouched or finished"
+    assert kept.any() and done.any()
+    # the next launch on the same workspace starts clean
+    cs.run_hmc(iter_begin=2, iter_count=1, **cfg)
+    torch.cuda.synchronize()
+    cs.check_status()
