@@ -22,6 +22,7 @@
 #include "hmc.h"
 #include "internal.h"
 #include "lanes.h"
+#include "lanes_fast.h"
 #include "mh.h"
 #include "nuts.h"
 #include "philox.h"
@@ -79,6 +80,7 @@ struct LanePlan {
     int S = 0, Dsh = 0, nitems = 0;  // slice geometry (S = 1: an unsliced program, no exchange)
     int32_t shl[kLrMaxShared] = {0, 0, 0, 0};  // shared parameters by ordinal
     int32_t n_generic = 0;  // scalar terms that are not "own" priors
+    int fast = 0;        // fast form: only swept / direct terms and own priors (k_hmc_lf)
     std::string why;     // why it does not qualify
     std::vector<LrTerm> terms;
     std::vector<float> data;
@@ -786,6 +788,7 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
     L.gidx.assign((size_t)S * kLrMaxSlots * 64, -1);
     L.sdata_floats = 0;
     std::vector<int> lane_of(p->D, -1), slot_of_p(p->D, -1);
+    bool any_rest = false;
     for (int s = 0; s < S; ++s) {
         // ---- parameters -> (lane, slot) ----
         const std::vector<int>& pv = part.priv[s];
@@ -920,6 +923,11 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
             else if (sw && (int)swept.size() < kLrSweep) swept.push_back(lt);
             else rest.push_back(lt);
         }
+        // fast form (lanes_fast.h): one swept term with data value and private
+        // loc at most, one direct term at most, nothing else
+        if (!rest.empty() || swept.size() > 1 || direct.size() > 1 ||
+            (!swept.empty() && swept[0].sig != LS_DATA_PP_SH && swept[0].sig != LS_DATA_PP_C))
+            any_rest = true;
         for (const LrTerm& lt : swept) L.terms[(size_t)s * nT + nact++] = lt;
         for (const LrTerm& lt : direct) L.terms[(size_t)s * nT + nact++] = lt;
         for (const LrTerm& lt : rest) L.terms[(size_t)s * nT + nact++] = lt;
@@ -962,6 +970,7 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         kSlLdsBudget)
         return no("slice data exceed the LDS budget");
     if (L.data.empty()) L.data.assign(4, 0.0f);
+    L.fast = (!any_rest && L.n_generic == 0) ? 1 : 0;
     L.ok = 1;
     return MC_OK;
 }
@@ -1796,9 +1805,22 @@ extern "C" int mc_debug_exchange_fault(int on) {
     return MC_OK;
 }
 
+// the fast-form kernel (lanes_fast.h) for programs that qualify, unless
+// MC_LANES_FAST=0 in the environment (A/B timing against k_hmc_lr)
+static bool lanes_fast_enabled() {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = std::getenv("MC_LANES_FAST");
+        on = (e && e[0] == '0') ? 0 : 1;
+    }
+    return on == 1;
+}
+
 template <int RS, int NSH, int NW, bool X1>
 static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* state,
                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
+    const bool fast = p->lr.fast && lanes_fast_enabled();
+    auto kern = fast ? k_hmc_lf<RS, NSH, NW, X1> : k_hmc_lr<RS, NSH, NW, X1>;
     int64_t qo, go;
     mc_state_offsets(p, cfg->num_chains, &qo, &go);
     char* b = (char*)state;
@@ -1807,7 +1829,7 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
     A.cfg = *cfg;
     const LrCtx ctx = lrctx_of(p);
     const size_t lds = (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm);
-    MC_HIP_TRY(allow_lds(k_hmc_lr<RS, NSH, NW, X1>, lds));
+    MC_HIP_TRY(allow_lds(kern, lds));
     const int64_t C = cfg->num_chains;
     constexpr int NB = 2 * NW;
     const int64_t groups = (C + NB - 1) / NB;
@@ -1818,7 +1840,7 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
     const uint64_t per_launch = (uint64_t)cfg->iter_count * cfg->num_leapfrog_steps + 1;
     const int64_t nlaunch = (groups + gpl - 1) / gpl;
     if (!X1) {
-        const int64_t cap = resident_capacity(k_hmc_lr<RS, NSH, NW, X1>, 64 * NW, lds);
+        const int64_t cap = resident_capacity(kern, 64 * NW, lds);
         if (cap < std::min(gpl, groups) * p->lr.S)
             return fail(MC_ERR_UNSUPPORTED,
                         "lane-resident HMC: %lld workgroups must be co-resident, the device holds "
@@ -1834,14 +1856,13 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
         const int64_t ng = std::min(gpl, groups - g0);
         const int64_t grid = ng * p->lr.S;
         if (X1) {
-            hipLaunchKernelGGL((k_hmc_lr<RS, NSH, NW, X1>), dim3((unsigned)grid), dim3(64 * NW),
-                               lds, st, ctx, A, g0 * NB, ng, (mc_chain_scalars*)b,
-                               (float*)(b + qo), (float*)(b + go), samples, trace_of(tr), xch,
-                               status, base);
+            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), lds, st, ctx, A,
+                               g0 * NB, ng, (mc_chain_scalars*)b, (float*)(b + qo),
+                               (float*)(b + go), samples, trace_of(tr), xch, status, base);
             MC_HIP_TRY(hipGetLastError());
         } else {
             const hipError_t e = launch_exchange(
-                k_hmc_lr<RS, NSH, NW, X1>, grid, 64 * NW, lds, st, ctx, A, g0 * NB, ng,
+                kern, grid, 64 * NW, lds, st, ctx, A, g0 * NB, ng,
                 (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples, trace_of(tr),
                 xch, status, base);
             if (e == hipErrorCooperativeLaunchTooLarge)

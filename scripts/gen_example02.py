@@ -11,12 +11,13 @@ helper :111-128).  Those numbers come from one draw of MLX's RNG, which is
 not available here; the oracle restates the sampler (oracle/samplers.py)
 with the shared Philox stream, so a run here is a different realisation of
 the same random process.  This script runs it for seed 42 (MCMC.run's key),
-chains 0..7, and records per chain the same five statistics:
+chains 0..63 (64 realisations, ~5 minutes on 8 cores), and records per chain
+the same five statistics:
 
     tests/golden/example02_hmc.json
 
 tests/test_oracle_pins.py checks the fixture against the published numbers
-(tolerances stated there); tests/test_gpu_samplers.py runs the same 8 chains
+(tolerances stated there); tests/test_gpu_samplers.py runs the same 64 chains
 through MCMC.run / hmc() on the GPU and checks them against the fixture.
 
     python scripts/gen_example02.py
@@ -32,7 +33,7 @@ sys.path.insert(0, ROOT)
 CFG = dict(num_samples=5000, num_warmup=1000, step_size=0.1, num_leapfrog_steps=10,
            adapt_step_size=True, target_accept=0.8)
 SEED = 42
-CHAINS = 8
+CHAINS = 64
 
 
 def _run(chain):

@@ -215,3 +215,50 @@ def test_distribution_sampling(gpu):
     assert np.isclose(h.mean(), 2.0 * np.sqrt(2 / np.pi), rtol=0.1)
     assert np.isclose(h.std(), 2.0 * np.sqrt(1 - 2 / np.pi), rtol=0.1)
     assert m.HalfNormal(5.0).sample(m.random.key(0), shape=(1000,)).min() >= 0
+
+
+def test_example02_realisations_match_oracle(gpu):
+    """Example 02's HMC run (examples/02_hmc_comparison.py:86-100: MCMC.run
+    method='hmc', step_size 0.1, L = 10, W = 1000, S = 5000, seed 42) on 64
+    chains through the product API against the oracle's 64 realisations
+    (tests/golden/example02_hmc.json): a chain whose 6000 accept decisions all
+    agree ends with a bit-identical step size, so at least 56 of 64 must; those
+    carry the oracle's statistics (acceptance exactly, ESS and |mean - truth|
+    to float rounding), and the GPU's realisations bracket the reference's
+    published numbers by the same rule as the oracle's
+    (test_oracle_pins.example02_bracket)."""
+    import json
+    import os
+
+    from test_oracle_pins import example02_bracket
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "example02_hmc.json")) as f:
+        fx = json.load(f)
+    cfg = fx["config"]
+    lp, init = W.simple_normal(W.ns_product())
+    s, rate, info = m.hmc(lp, init, num_samples=cfg["num_samples"],
+                          num_warmup=cfg["num_warmup"], step_size=cfg["step_size"],
+                          num_leapfrog_steps=cfg["num_leapfrog_steps"],
+                          adapt_step_size=cfg["adapt_step_size"],
+                          target_accept=cfg["target_accept"], key=m.random.key(cfg["seed"]),
+                          num_chains=64, progress=False, return_info=True)
+    from oracle.diag import compute_ess_02
+
+    mu = np.asarray(s["mu"], np.float64)
+    sg = np.asarray(s["sigma"], np.float64)
+    mine = []
+    same = 0
+    for c, o in enumerate(fx["chains"]):
+        r = {"accept_rate": float(info.accept_rate[c]), "step_size": float(info.step_size[c]),
+             "ess_mu": compute_ess_02(mu[c]), "ess_sigma": compute_ess_02(sg[c]),
+             "err_mu": abs(mu[c].mean() - 5.0), "err_sigma": abs(sg[c].mean() - 2.0)}
+        mine.append(r)
+        if r["step_size"] == o["step_size"]:
+            same += 1
+            assert r["accept_rate"] == o["accept_rate"]
+            assert r["err_mu"] == pytest.approx(o["err_mu"], abs=1e-4)
+            assert r["err_sigma"] == pytest.approx(o["err_sigma"], abs=1e-4)
+            assert r["ess_mu"] == pytest.approx(o["ess_mu"], rel=1e-2)
+            assert r["ess_sigma"] == pytest.approx(o["ess_sigma"], rel=1e-2)
+    assert same >= 56, f"only {same} of 64 realisations kept the oracle's decisions"
+    example02_bracket(mine, fx["published"])
