@@ -41,6 +41,8 @@ MC_DEV constexpr int lf_row(int P) { return (P & 3) == 1 ? 2 : ((P & 3) == 2 ? 1
 MC_DEV constexpr int lf_shlane(int k, int c) {
     return 16 * lf_row(2 * (k + 1) + c) + (2 * (k + 1) + c) / 4;
 }
+// Uniform (per chain) value `v` of shared parameter k, chain c.
+MC_DEV float lf_sh(float v, int k, int c) { return rl(v, lf_shlane(k, c)); }
 
 // Reduce-scatter of 8 per-lane values over the wave: returns two registers;
 // row r of register n holds (in all 16 lanes) the wave total of value

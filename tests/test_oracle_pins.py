@@ -444,8 +444,10 @@ def example02_bracket(chains, pub):
     assert np.mean(acc >= 0.999) >= 0.8 and acc.max() >= pub["accept_rate"]
     assert np.quantile(em, 0.1) <= pub["err_mu"] <= np.quantile(em, 0.9)
     assert np.quantile(es, 0.1) <= pub["err_sigma"] <= np.quantile(es, 0.9)
-    assert nm.min() <= pub["ess_mu"] <= nm.max()
-    assert ns_.min() <= pub["ess_sigma"] <= ns_.max()
+    # a realisation frozen by the rule (a constant series) has no ESS by the
+    # example's helper (0 / 0): NaN, left out
+    assert np.nanmin(nm) <= pub["ess_mu"] <= np.nanmax(nm)
+    assert np.nanmin(ns_) <= pub["ess_sigma"] <= np.nanmax(ns_)
     reach = (acc >= 0.999) & (nm >= pub["ess_mu"] / 2) & (ns_ >= pub["ess_sigma"] / 2)
     assert reach.any()
 
