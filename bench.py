@@ -199,7 +199,8 @@ def kernel_label(prog, C):
     """The sampler kernel a launch runs (rocprof names it the same way)."""
     kind = prog.slice_kernel
     if kind == "lanes":
-        return f"k_hmc_lr (S={prog.num_slices} slices, lane-resident)"
+        name = "k_hmc_lf" if prog.lanes_fast else "k_hmc_lr"
+        return f"{name} (S={prog.num_slices} slices, lane-resident)"
     if kind == "interpreter":
         return f"k_hmc_sl<{16 if C > 8 else 8}> (S={prog.num_slices} slices)"
     return f"k_hmc<{prog.waves_per_chain}>"
@@ -400,6 +401,14 @@ def main():
             out["cpu_baseline"] = cpu_baseline(G, N, L, max(eps, 1e-4), args.cpu_seconds, nproc,
                                                value)
         print(json.dumps(out), flush=True)
+    # release the device objects (program, chain state, workspace) before the
+    # interpreter's exit handlers run, so nothing calls into HIP after a
+    # profiler's teardown
+    del chains, prog, samples, diag
+    torch.cuda.synchronize()
+    if os.environ.get("MC_DUMP_MAPS"):  # diagnostic: map exit-time crash addresses
+        with open(os.environ["MC_DUMP_MAPS"], "w") as f:
+            f.write(open("/proc/self/maps").read())
     if world > 1:
         dist.destroy_process_group()
 

@@ -153,6 +153,12 @@ int32_t mc_program_num_slices(const mc_program* prog);
  * the choice's layout.                                                      */
 int mc_program_set_slice_kernel(mc_program* prog, int32_t kernel);
 int32_t mc_program_slice_kernel(const mc_program* prog);
+/* 1 when a lane-resident launch of this program runs the fast-form kernel
+ * k_hmc_lf (every slice term a swept N(theta[g], scale) term over data or a
+ * direct theta ~ N(loc, scale) term, every scalar term the own prior of a
+ * broadcast parameter; MC_LANES_FAST=0 in the environment turns it off),
+ * 0 when it runs k_hmc_lr or no lane-resident kernel, -1 on a null program. */
+int32_t mc_program_lanes_fast(const mc_program* prog);
 
 /* Batched tape evaluation: for every point p, logp[p] = log density at
  * q[p, :] and grad[p, :] = its gradient (replaces hmc.py:53-67 mx.grad).   */

@@ -503,6 +503,11 @@ class Program:
         k = _lib.load().mc_program_slice_kernel(self.handle)
         return {0: "unsliced", 1: "interpreter", 2: "lanes"}[k]
 
+    @property
+    def lanes_fast(self) -> bool:
+        """True when a lane-resident launch runs the fast-form kernel k_hmc_lf."""
+        return _lib.load().mc_program_lanes_fast(self.handle) == 1
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and h.value:

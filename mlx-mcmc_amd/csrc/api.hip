@@ -1127,6 +1127,13 @@ extern "C" int32_t mc_program_slice_kernel(const mc_program* p) {
     return 2;
 }
 
+static bool lanes_fast_enabled();
+extern "C" int32_t mc_program_lanes_fast(const mc_program* p) {
+    if (!p) return -1;
+    const int32_t k = mc_program_slice_kernel(p);
+    return (k == 2 && p->lr.fast && lanes_fast_enabled()) ? 1 : 0;
+}
+
 extern "C" int32_t mc_program_num_slices(const mc_program* p) { return p ? p->sl.S : -1; }
 
 extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t n_params,

@@ -28,7 +28,7 @@ def main():
     fdir, wdir, shape = sys.argv[1], sys.argv[2], sys.argv[3]
     ipl = int(sys.argv[4]) if len(sys.argv) > 4 else 1  # bench.py --iters-per-launch
     f = {}
-    for kern in ("k_hmc_lr", "k_hmc_sl", "k_hmc"):  # the sampler kernel bench.py ran
+    for kern in ("k_hmc_lf", "k_hmc_lr", "k_hmc_sl", "k_hmc"):  # the sampler kernel bench.py ran
         f = per_dispatch(fdir, "FETCH_SIZE", kern)
         if f:
             break
