@@ -81,6 +81,8 @@ struct LanePlan {
     int32_t shl[kLrMaxShared] = {0, 0, 0, 0};  // shared parameters by ordinal
     int32_t n_generic = 0;  // scalar terms that are not "own" priors
     int fast = 0;        // fast form: only swept / direct terms and own priors (k_hmc_lf)
+    int form = -1;       // the fast form's LF_* bits when every slice has the same terms
+                         // and distinct shared roles (compile-time k_hmc_lf), else -1
     std::string why;     // why it does not qualify
     std::vector<LrTerm> terms;
     std::vector<float> data;
@@ -752,6 +754,40 @@ static LrCtx lrctx_of(const mc_program* p) {
 // the least loaded lane with a free slot, and tile each term's elements per
 // (slot, lane).  Returns MC_ERR_UNSUPPORTED (with L.why) when the program does
 // not qualify; the term interpreter (k_hmc_sl) then runs it.
+// The compile-time form of a fast-form plan (lanes_fast.h LF_* bits): every
+// slice holds the same swept / direct terms with the same shared operands,
+// the shared roles (swept scale, direct loc, direct scale) are distinct
+// parameters and every shared parameter has one; -1 otherwise, or when the
+// form has no compiled kernel (k_hmc_lf<..., -1> reads it at run time).
+static int lanes_form(const LanePlan& L, int nT) {
+    int form = -2, o_sw = -1, o_dm = -1, o_ds = -1;
+    for (int s = 0; s < L.S; ++s) {
+        const int nsw = (int)(L.blocks[4 * s + 3] & 255), ndir = (int)((L.blocks[4 * s + 3] >> 8) & 255);
+        const LrTerm* t = &L.terms[(size_t)s * nT];
+        int f = 0, a = -1, b = -1, c = -1;
+        if (nsw > 0) {
+            f |= LF_SW;
+            if (t[0].kind[2] == SK_SHARED) f |= LF_SWS, a = t[0].jsh[2];
+        }
+        if (ndir > 0) {
+            const LrTerm& u = t[nsw];
+            f |= LF_DIR;
+            if (u.kind[1] == SK_SHARED) f |= LF_DM, b = u.jsh[1];
+            if (u.kind[2] == SK_SHARED) f |= LF_DS, c = u.jsh[2];
+        }
+        if (form == -2) {
+            form = f, o_sw = a, o_dm = b, o_ds = c;
+        } else if (f != form || a != o_sw || b != o_dm || c != o_ds) {
+            return -1;
+        }
+    }
+    if (form < 0) return -1;
+    const int roles = lf_nroles(form);
+    if (roles != L.Dsh) return -1;
+    if ((o_sw >= 0 && (o_sw == o_dm || o_sw == o_ds)) || (o_dm >= 0 && o_dm == o_ds)) return -1;
+    return (form == (LF_SW | LF_SWS | LF_DIR | LF_DM | LF_DS) || form == LF_DIR) ? form : -1;
+}
+
 static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartition& part,
                       LanePlan& L) {
     const std::vector<DevTerm>& raw = p->raw;
@@ -971,6 +1007,7 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         return no("slice data exceed the LDS budget");
     if (L.data.empty()) L.data.assign(4, 0.0f);
     L.fast = (!any_rest && L.n_generic == 0) ? 1 : 0;
+    L.form = L.fast ? lanes_form(L, nT) : -1;
     L.ok = 1;
     return MC_OK;
 }
@@ -1827,7 +1864,16 @@ template <int RS, int NSH, int NW, bool X1>
 static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* state,
                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
     const bool fast = p->lr.fast && lanes_fast_enabled();
-    auto kern = fast ? k_hmc_lf<RS, NSH, NW, X1> : k_hmc_lr<RS, NSH, NW, X1>;
+    auto kern = fast ? k_hmc_lf<RS, NSH, NW, X1, -1> : k_hmc_lr<RS, NSH, NW, X1>;
+    static const bool forms = [] {  // MC_LANES_FORM=0: run-time forms only (A/B timing)
+        const char* e = std::getenv("MC_LANES_FORM");
+        return !(e && e[0] == '0');
+    }();
+    if constexpr (NSH == 3) {  // the compile-time forms (one instantiation each)
+        constexpr int HIER = LF_SW | LF_SWS | LF_DIR | LF_DM | LF_DS;
+        if (fast && forms && p->lr.form == HIER) kern = k_hmc_lf<RS, lf_nroles(HIER), NW, X1, HIER>;
+        if (fast && forms && p->lr.form == LF_DIR) kern = k_hmc_lf<RS, lf_nroles(LF_DIR), NW, X1, LF_DIR>;
+    }
     int64_t qo, go;
     mc_state_offsets(p, cfg->num_chains, &qo, &go);
     char* b = (char*)state;

@@ -12,11 +12,20 @@
 // configs[2]/[3] and the isotropic / diagonal Gaussians of configs[1]/[4] are
 // of this form.
 //
+// FORM (template): -1 reads the form from the terms at run time; FORM >= 0
+// fixes it at compile time (bits LF_*; the planner sets LanePlan::form when
+// every slice has the same terms and the shared roles are distinct
+// parameters).  A compile-time form keys the record's cotangent items by
+// *role* (swept scale, direct loc, direct scale) instead of by shared
+// ordinal: no selects between them, and the lane that holds a role's total
+// after the exchange holds that role's parameter.
+//
 // What differs from k_hmc_lr:
 //   * the terms' fields, the lanes holding their shared operands and the
-//     runs' data pointers are read once per launch (k_hmc_lr re-reads them
-//     from constant memory at every step and indexes its cotangent partials
-//     by a runtime ordinal, which the compiler keeps in scratch);
+//     runs' data pointers are read once per launch;
+//   * both chains' per-step arithmetic runs packed (v_pk_*_f32: the same
+//     IEEE operations per chain, two chains per instruction), the per-launch
+//     uniform values pinned in VGPRs (no SGPR spills reloaded per step);
 //   * the moment sweep keeps even and odd elements in separate packed
 //     accumulators (two dependency chains each; a dependent v_pk_add_f32
 //     advances every 10 cycles, scripts/micro/pk_probe.hip);
@@ -24,8 +33,11 @@
 //     permlane16 swaps + one 16-lane DPP row sum) so that pair P's total is
 //     in row perm[P % 4] of register P / 4 — no readlanes, no publish select;
 //     the poll uses the same pair -> row map, so after the slice sums the
-//     lane that holds shared parameter (k, c) finds its cotangent total in
-//     its own register (lane 16 perm[P % 4] + P / 4, P = 2 (k + 1) + c);
+//     lane that holds shared slot (k, c) finds its cotangent total in its own
+//     register (lane 16 perm[P % 4] + P / 4, P = 2 (k + 1) + c);
+//   * the shared parameters' own priors enter slice 0's log-p record (one
+//     add in the lane that holds the parameter, instead of a per-step
+//     readlane sum over the shared parameters after the exchange);
 //   * the kinetic-energy items K0 / K1 travel only on the first / last step.
 // Results equal k_hmc_lr's up to fp32 summation order; runs are
 // bit-reproducible and independent of how chains are split over launches.
@@ -34,15 +46,42 @@
 
 namespace mc {
 
+// compile-time term forms (FORM bits)
+constexpr int LF_SW = 1;    // a swept term
+constexpr int LF_SWS = 2;   //   its scale a shared parameter (else constant)
+constexpr int LF_DIR = 4;   // a direct term
+constexpr int LF_DM = 8;    //   its loc a shared parameter (else constant)
+constexpr int LF_DS = 16;   //   its scale a shared parameter (else constant)
+// the shared slots of a compile-time form: swept scale, direct loc, direct
+// scale, in that order, for the roles present
+constexpr int lf_slot_sws(int F) { return (void)F, 0; }
+constexpr int lf_slot_dm(int F) { return (F & LF_SWS) ? 1 : 0; }
+constexpr int lf_slot_ds(int F) { return lf_slot_dm(F) + ((F & LF_DM) ? 1 : 0); }
+constexpr int lf_nroles(int F) { return lf_slot_ds(F) + ((F & LF_DS) ? 1 : 0); }
+
 // pair P -> the row (16-lane group) that holds its total after the
 // reduce-scatter / the slice sums: rows hold values 4n + {0, 2, 1, 3}
 MC_DEV constexpr int lf_row(int P) { return (P & 3) == 1 ? 2 : ((P & 3) == 2 ? 1 : (P & 3)); }
-// the lane that holds shared parameter k of chain c
+// the lane that holds shared slot k of chain c
 MC_DEV constexpr int lf_shlane(int k, int c) {
     return 16 * lf_row(2 * (k + 1) + c) + (2 * (k + 1) + c) / 4;
 }
-// Uniform (per chain) value `v` of shared parameter k, chain c.
+// Uniform (per chain) value `v` of shared slot k, chain c.
 MC_DEV float lf_sh(float v, int k, int c) { return rl(v, lf_shlane(k, c)); }
+// Both chains' values of shared slot k.
+MC_DEV f2 lf_sh2(float v, int k) { return (f2){rl(v, lf_shlane(k, 0)), rl(v, lf_shlane(k, 1))}; }
+
+// Keep a wave-uniform value in a VGPR: the kernel holds more uniform values
+// than there are SGPRs, and a spilled SGPR costs a v_readlane at every use.
+MC_DEV float vpin(float x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+MC_DEV f2 vpin(f2 x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+MC_DEV f2 bc2(float x) { return (f2){x, x}; }
 
 // Reduce-scatter of 8 per-lane values over the wave: returns two registers;
 // row r of register n holds (in all 16 lanes) the wave total of value
@@ -107,7 +146,7 @@ MC_DEV void lf_moments(const float* xv, int len, int lmin4, f2 th, f2& s1, f2& s
 // The fast-form terms of a slice, read once per launch: at most one swept
 // term (y ~ N(theta[g], scale): value data, loc private, scale shared or
 // constant) and one direct term (theta ~ N(loc, scale), loc / scale shared or
-// constant).  Shared operands are addressed by the lanes that hold them.
+// constant).  Shared operands are named by their shared ordinals.
 struct LfTerms {
     bool sw, dir;
     // swept term
@@ -146,12 +185,15 @@ MC_DEV LfTerms lf_terms(const MC_CONST LrTerm* tt, int nsweep, int ndirect) {
     return F;
 }
 
-template <int RS, int NSH, int NW, bool X1>
+// NSH: shared slots of the record (FORM >= 0: lf_nroles(FORM)).
+template <int RS, int NSH, int NW, bool X1, int FORM>
 __global__ void __launch_bounds__(64 * NW)
 k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scalars* scal,
          float* st_q, float* st_g, float* samples, TraceDev tr, unsigned long long* xch,
          int* status, uint32_t ebase) {
     static_assert(NSH <= kLrMaxShared, "shared parameters");
+    constexpr bool CF = FORM >= 0;      // the form is fixed at compile time
+    static_assert(!CF || lf_nroles(FORM) == NSH, "record slots of a compile-time form");
     constexpr int NB = 2 * NW;          // chains per block: wave w owns chains 2w, 2w + 1
     constexpr int NV = 2 * (NSH + 1);   // per-step pairs: lp and the shared cotangents
     constexpr int NPAIR = NV + 4;       // + K0 (first step) and K1 (last step)
@@ -186,22 +228,6 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         live[c] = cbase + b0 + c < C;
         cc[c] = min(cbase + b0 + c, C - 1);
     }
-    // this lane's shared parameter: (xk, xc) with lf_shlane(xk, xc) == j
-    int xk = -1, xc = 0;
-#pragma unroll
-    for (int k = 0; k < kLrMaxShared; ++k)
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-            if (k < Dsh && lf_shlane(k, c) == j) {
-                xk = k;
-                xc = c;
-            }
-    const bool xon = xk >= 0;
-    int xg = P.shl[0];
-#pragma unroll
-    for (int k = 1; k < kLrMaxShared; ++k) xg = (xk == k) ? P.shl[k] : xg;
-    const int64_t xch_id = xc ? cc[1] : cc[0];
-    const bool xlive = xon && (xc ? live[1] : live[0]);
 
     float* sd = smem;
     const int64_t* blk = P.blocks + 4 * (int64_t)slice;
@@ -215,17 +241,59 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     for (int i = tid; i < P.n_sterms * (int)(sizeof(LrSterm) / 16); i += 64 * NW)
         ((float4*)sst)[i] = ((const float4*)P.sterms)[i];
 
-    LrPriv<RS> R;
+    const MC_CONST LrTerm* tt = cptr(P.terms) + (int64_t)slice * P.n_terms;
+    const LfTerms F = lf_terms(tt, nsweep, ndirect);
+    // the form, folded to constants when FORM >= 0
+    const bool SW = CF ? (FORM & LF_SW) != 0 : F.sw;
+    const bool SWS = CF ? (FORM & LF_SWS) != 0 : F.sw_shs;
+    const bool DIR = CF ? (FORM & LF_DIR) != 0 : F.dir;
+    const bool DM = CF ? (FORM & LF_DM) != 0 : F.d_shm;
+    const bool DS = CF ? (FORM & LF_DS) != 0 : F.d_shs;
+    // the shared slot of each role: its role index (compile-time form) or its
+    // shared ordinal (run-time form)
+    const int ksw = CF ? lf_slot_sws(FORM) : max(F.sw_ks, 0);
+    const int kdm = CF ? lf_slot_dm(FORM) : max(F.d_km, 0);
+    const int kds = CF ? lf_slot_ds(FORM) : max(F.d_ks, 0);
+    const int nsl = CF ? NSH : Dsh;  // shared slots
+    // shared ordinal of slot k
+    auto ord_of = [&](int k) {
+        int o = F.d_ks;  // selects, not an indexed read of F (scratch)
+        o = (DM && k == kdm) ? F.d_km : o;
+        o = (SWS && k == ksw) ? F.sw_ks : o;
+        return CF ? o : k;
+    };
+    // this lane's shared slot: (xk, xc) with lf_shlane(xk, xc) == j
+    int xk = -1, xc = 0;
+#pragma unroll
+    for (int k = 0; k < kLrMaxShared; ++k)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+            if (k < nsl && lf_shlane(k, c) == j) {
+                xk = k;
+                xc = c;
+            }
+    const bool xon = xk >= 0;
+    const int xo = xon ? ord_of(xk) : 0;  // its shared ordinal
+    int xg = P.shl[0];
+#pragma unroll
+    for (int k = 1; k < kLrMaxShared; ++k) xg = (xo == k) ? P.shl[k] : xg;
+    const int64_t xch_id = xc ? cc[1] : cc[0];
+    const bool xlive = xon && (xc ? live[1] : live[0]);
+
+    LrPriv<RS> R0;  // (loaded as in k_hmc_lr, then packed per slot)
     int gk[RS];
+    f2 q[RS], p[RS], g[RS];
 #pragma unroll
     for (int r = 0; r < RS; ++r) {
         gk[r] = P.gidx[((int64_t)slice * kLrMaxSlots + r) * 64 + j];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            R.q[r][c] = gk[r] >= 0 ? st_q[cc[c] * D + gk[r]] : 0.0f;
-            R.g[r][c] = gk[r] >= 0 ? st_g[cc[c] * D + gk[r]] : 0.0f;
-            R.p[r][c] = 0.0f;
+            R0.q[r][c] = gk[r] >= 0 ? st_q[cc[c] * D + gk[r]] : 0.0f;
+            R0.g[r][c] = gk[r] >= 0 ? st_g[cc[c] * D + gk[r]] : 0.0f;
         }
+        q[r] = (f2){R0.q[r][0], R0.q[r][1]};
+        g[r] = (f2){R0.g[r][0], R0.g[r][1]};
+        p[r] = (f2){0.f, 0.f};
     }
     LrShared sh;
     sh.q = xon ? st_q[xch_id * D + xg] : 1.0f;
@@ -234,7 +302,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     sh.is = sh.iv = 1.0f;
     sh.lg = 0.0f;
     double eps[2];
-    float lp[2];
+    f2 lp;
     int nacc[2], ntot[2], wacc[2], wtot[2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -248,41 +316,49 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     MC_STAMP_INIT
     __syncthreads();  // the slice block is in LDS
 
-    const MC_CONST LrTerm* tt = cptr(P.terms) + (int64_t)slice * P.n_terms;
-    // the lane's own prior: lr_own_prior keys it by ordinal k = lane / 2
-    const LrOwn own = lr_own_prior(P.n_sterms, sst, xon ? 2 * xk + xc : 64, Dsh);
-    const LfTerms F = lf_terms(tt, nsweep, ndirect);
+    // the lane's own prior (lr_own_prior keys it by ordinal); it enters
+    // slice 0's log-p record through this lane
+    const LrOwn own = lr_own_prior(P.n_sterms, sst, xon ? 2 * xo + xc : 64, Dsh);
+    const bool own_lp0 = own.on && slice == 0 && xc == 0;
+    const bool own_lp1 = own.on && slice == 0 && xc == 1;
+    const float o_m = vpin(own.m), o_cinv2 = vpin(own.cinv2), o_c0l = vpin(own.c0l),
+                o_wn = vpin(own.wn);
     // per slot: the swept term's run (data pointer, length, full float4
     // groups of every lane) and the direct term's presence
     const float* xv[RS];
     int len[RS], lmin4[RS];
-    float cnt[RS];
+    f2 cnt[RS];
     bool pdir[RS];
 #pragma unroll
     for (int r = 0; r < RS; ++r) {
         len[r] = 0;
         lmin4[r] = 0;
         xv[r] = sd;
-        if (F.sw && r < tt[0].nslot) {
+        if (SW && r < tt[0].nslot) {
             len[r] = ((const int32_t*)sd)[tt[0].len_off + r * 64 + j];
             lmin4[r] = tt[0].lmin4[r];
             xv[r] = sd + tt[0].doff[0] + tt[0].toff[r] + 4 * j;
         }
-        cnt[r] = (float)len[r];
-        pdir[r] = F.dir && r < tt[nsweep].nslot &&
+        cnt[r] = bc2((float)len[r]);
+        pdir[r] = DIR && r < tt[nsweep].nslot &&
                   ((const int32_t*)sd)[tt[nsweep].len_off + r * 64 + j] > 0;
     }
-    // the lanes that hold the shared operands, per chain
-    const int sw_l0 = lf_shlane(max(F.sw_ks, 0), 0), sw_l1 = lf_shlane(max(F.sw_ks, 0), 1);
-    const int dm_l0 = lf_shlane(max(F.d_km, 0), 0), dm_l1 = lf_shlane(max(F.d_km, 0), 1);
-    const int ds_l0 = lf_shlane(max(F.d_ks, 0), 0), ds_l1 = lf_shlane(max(F.d_ks, 0), 1);
+    // the terms' constants, pinned in VGPRs
+    const f2 sw_w = vpin(bc2(F.sw_w)), sw_c0 = vpin(bc2(F.sw_c0));
+    const f2 sw_cinv = vpin(bc2(F.sw_cinv)), sw_cinv2 = vpin(bc2(F.sw_cinv2)),
+             sw_clogs = vpin(bc2(F.sw_clogs));
+    const f2 d_w = vpin(bc2(F.d_w)), d_c0 = vpin(bc2(F.d_c0)), d_m = vpin(bc2(F.d_m));
+    const f2 d_cinv = vpin(bc2(F.d_cinv)), d_cinv2 = vpin(bc2(F.d_cinv2)),
+             d_clogs = vpin(bc2(F.d_clogs));
+    const f2 half = bc2(0.5f), one = bc2(1.0f);
+    const float lp_const = vpin(P.lp_const);
     // the swept terms' moment sums at the current point, both chains
     auto sweep = [&](f2 (&s1)[RS], f2 (&s2)[RS]) {
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             s1[r] = (f2){0.f, 0.f};
             s2[r] = (f2){0.f, 0.f};
-            if (len[r] > 0) lf_moments(xv[r], len[r], lmin4[r], (f2){R.q[r][0], R.q[r][1]}, s1[r], s2[r]);
+            if (len[r] > 0) lf_moments(xv[r], len[r], lmin4[r], q[r], s1[r], s2[r]);
         }
     };
 
@@ -300,11 +376,22 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     const bool poll_lane = col < S;
     // publishing: lanes 16 r + n (n < NRS * 2) hold pair 8 (n / 2) + 4 (n % 2) + perm[r]
     const int pub_pair = (col < 2 * NRS) ? 8 * (col >> 1) + 4 * (col & 1) + lf_row(row) : -1;
+    const bool pub_rec = pub_pair >= 0 && pub_pair < NV;
+    // poll passes by kind: record pairs every step, K0 / K1 pairs on the first / last
+    uint32_t need_v = 0, need_k0 = 0, need_k1 = 0;
+#pragma unroll
+    for (int ps = 0; ps < NPASS; ++ps) {
+        const int pr = 4 * ps + lf_row(row);
+        if (X1 || !poll_lane || pr >= NPAIR) continue;
+        if (pr < NV) need_v |= 1u << ps;
+        else if (pr < NV + 2) need_k0 |= 1u << ps;
+        else need_k1 |= 1u << ps;
+    }
     const int64_t it_end = cfg.iter_begin + cfg.iter_count;
     for (int64_t it = cfg.iter_begin; it < it_end && ok; ++it) {
         MC_STAMP_DECL
         const bool warm = it < cfg.num_warmup;
-        float h[2], e[2];
+        float hs[2], es[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             if (it == cfg.num_warmup) {  // hmc.py:175-180
@@ -313,62 +400,56 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 nacc[c] = 0;
                 ntot[c] = 0;
             }
-            h[c] = (float)(0.5 * eps[c]);
-            e[c] = (float)eps[c];
+            hs[c] = (float)(0.5 * eps[c]);
+            es[c] = (float)eps[c];
         }
-        const float xh = xc ? h[1] : h[0], xe = xc ? e[1] : e[0];
+        const f2 h = vpin((f2){hs[0], hs[1]}), e = vpin((f2){es[0], es[1]});
+        const float xh = vpin(xc ? hs[1] : hs[0]), xe = vpin(xc ? es[1] : es[0]);
         // momentum: parameter g takes normal g % 4 of Philox block g / 4
-        auto normal_of = [&](int g, int64_t chain) {
+        auto normal_of = [&](int gi, int64_t chain) {
             const mc_u32x4 rr = mc_draw(cfg.seed, (uint32_t)(cfg.chain_offset + chain),
-                                        (uint32_t)it, MC_RNG_TAG_MOMENTUM, 0, (uint32_t)(g >> 2));
+                                        (uint32_t)it, MC_RNG_TAG_MOMENTUM, 0, (uint32_t)(gi >> 2));
             float z0, z1;
-            if ((g & 3) < 2) mc_box_muller(rr.x, rr.y, &z0, &z1);
+            if ((gi & 3) < 2) mc_box_muller(rr.x, rr.y, &z0, &z1);
             else mc_box_muller(rr.z, rr.w, &z0, &z1);
-            return (g & 1) ? z1 : z0;
+            return (gi & 1) ? z1 : z0;
         };
-        float k0p[2] = {0.f, 0.f};
+        f2 k0p = {0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
-            if (gk[r] < 0) continue;
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const float z = normal_of(gk[r], cc[c]);
-                R.p[r][c] = z;
-                k0p[c] += z * z;
-            }
+            if (gk[r] < 0) continue;  // (an empty slot's p stays 0: its g is always 0)
+            const f2 z = {normal_of(gk[r], cc[0]), normal_of(gk[r], cc[1])};
+            p[r] = z;
+            k0p += z * z;
         }
         sh.p = xon ? normal_of(xg, xch_id) : 0.0f;
         const float K0w[2] = {wave_sum(k0p[0]), wave_sum(k0p[1])};
-        float k0s[2] = {0.f, 0.f};  // the shared parameters' part, in parameter order
+        float k0s[2] = {0.f, 0.f};  // the shared parameters' part, in slot order
         {
             const float p2 = sh.p * sh.p;
-            for (int k = 0; k < Dsh; ++k) {
+            for (int k = 0; k < nsl; ++k) {
                 k0s[0] += lf_sh(p2, k, 0);
                 k0s[1] += lf_sh(p2, k, 1);
             }
         }
-        float q0[RS][2], g0[RS][2];
+        f2 q0[RS], g0[RS];
 #pragma unroll
-        for (int r = 0; r < RS; ++r)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                q0[r][c] = R.q[r][c];
-                g0[r][c] = R.g[r][c];
-            }
+        for (int r = 0; r < RS; ++r) {
+            q0[r] = q[r];
+            g0[r] = g[r];
+        }
         const float q0s = sh.q, g0s = sh.g;
-        float lpn[2] = {lp[0], lp[1]}, K0[2] = {0.f, 0.f}, K1[2] = {0.f, 0.f};
+        f2 lpn = lp;
+        float K0[2] = {0.f, 0.f}, K1[2] = {0.f, 0.f};
         MC_STAMP(5);
         auto drift_private = [&](bool second_half) {
 #pragma unroll
-            for (int c = 0; c < 2; ++c) {
-#pragma unroll
-                for (int r = 0; r < RS; ++r) {
-                    float pj = R.p[r][c];
-                    if (second_half) pj = pj + h[c] * R.g[r][c];  // end of the previous step
-                    pj = pj + h[c] * R.g[r][c];
-                    R.p[r][c] = pj;
-                    R.q[r][c] = R.q[r][c] + e[c] * pj;
-                }
+            for (int r = 0; r < RS; ++r) {
+                f2 pj = p[r];
+                if (second_half) pj = pj + h * g[r];  // end of the previous step
+                pj = pj + h * g[r];
+                p[r] = pj;
+                q[r] = q[r] + e * pj;
             }
         };
         auto drift_shared = [&](bool second_half) {
@@ -388,61 +469,62 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         for (int l = 0; l < L; ++l) {
             MC_STAMP(0);
             // finish the swept term from its moment sums, evaluate the direct
-            // term (k_hmc_lr's lr_finish; same arithmetic, scalar per chain):
+            // term (k_hmc_lr's lr_finish; same arithmetic, both chains packed):
             // log p partial, complete private gradients, cotangent partials of
             // the swept scale (cs), the direct loc (cm) and scale (cd)
-            float lpp[2] = {0.f, 0.f}, cs[2] = {0.f, 0.f}, cm[2] = {0.f, 0.f}, cd[2] = {0.f, 0.f};
+            f2 lpp = {0.f, 0.f}, cs = {0.f, 0.f}, cm = {0.f, 0.f}, cd = {0.f, 0.f};
 #pragma unroll
-            for (int r = 0; r < RS; ++r) R.g[r][0] = R.g[r][1] = 0.0f;
-            if (F.sw) {
-                float is[2], iv[2], lg[2];
-                is[0] = F.sw_shs ? rl(sh.is, sw_l0) : F.sw_cinv;
-                is[1] = F.sw_shs ? rl(sh.is, sw_l1) : F.sw_cinv;
-                iv[0] = F.sw_shs ? rl(sh.iv, sw_l0) : F.sw_cinv2;
-                iv[1] = F.sw_shs ? rl(sh.iv, sw_l1) : F.sw_cinv2;
-                lg[0] = F.sw_shs ? rl(sh.lg, sw_l0) : F.sw_clogs;
-                lg[1] = F.sw_shs ? rl(sh.lg, sw_l1) : F.sw_clogs;
+            for (int r = 0; r < RS; ++r) g[r] = (f2){0.f, 0.f};
+            if (SW) {
+                const f2 is = SWS ? lf_sh2(sh.is, ksw) : sw_cinv;
+                const f2 iv = SWS ? lf_sh2(sh.iv, ksw) : sw_cinv2;
+                const f2 lg = SWS ? lf_sh2(sh.lg, ksw) : sw_clogs;
+                const f2 c0lg = sw_c0 - lg;
 #pragma unroll
                 for (int r = 0; r < RS; ++r) {
-                    if (cnt[r] == 0.0f) continue;
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const float s1 = M1[r][c], s2 = M2[r][c];
-                        const float lpt = cnt[r] * (F.sw_c0 - lg[c]) - (0.5f * s2) * iv[c];
-                        lpp[c] += F.sw_w * lpt;
-                        R.g[r][c] += F.sw_w * (s1 * iv[c]);
-                        cs[c] += F.sw_w * ((s2 * iv[c] - cnt[r]) * is[c]);
-                    }
+                    if (len[r] == 0) continue;
+                    const f2 lpt = cnt[r] * c0lg - (half * M2[r]) * iv;
+                    lpp += sw_w * lpt;
+                    g[r] += sw_w * (M1[r] * iv);
+                    cs += sw_w * ((M2[r] * iv - cnt[r]) * is);
                 }
             }
-            if (F.dir) {
-                float um[2], is[2], iv[2], lg[2];
-                um[0] = F.d_shm ? rl(sh.q, dm_l0) : F.d_m;
-                um[1] = F.d_shm ? rl(sh.q, dm_l1) : F.d_m;
-                is[0] = F.d_shs ? rl(sh.is, ds_l0) : F.d_cinv;
-                is[1] = F.d_shs ? rl(sh.is, ds_l1) : F.d_cinv;
-                iv[0] = F.d_shs ? rl(sh.iv, ds_l0) : F.d_cinv2;
-                iv[1] = F.d_shs ? rl(sh.iv, ds_l1) : F.d_cinv2;
-                lg[0] = F.d_shs ? rl(sh.lg, ds_l0) : F.d_clogs;
-                lg[1] = F.d_shs ? rl(sh.lg, ds_l1) : F.d_clogs;
+            if (DIR) {
+                const f2 um = DM ? lf_sh2(sh.q, kdm) : d_m;
+                const f2 is = DS ? lf_sh2(sh.is, kds) : d_cinv;
+                const f2 iv = DS ? lf_sh2(sh.iv, kds) : d_cinv2;
+                const f2 lg = DS ? lf_sh2(sh.lg, kds) : d_clogs;
+                const f2 c0lg = one * (d_c0 - lg);
 #pragma unroll
                 for (int r = 0; r < RS; ++r) {
                     if (!pdir[r]) continue;
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const float d = R.q[r][c] - um[c];
-                        const float s2 = d * d;
-                        const float lpt = 1.0f * (F.d_c0 - lg[c]) - (0.5f * s2) * iv[c];
-                        lpp[c] += F.d_w * lpt;
-                        const float u = F.d_w * (d * iv[c]);
-                        R.g[r][c] += -u;
-                        cm[c] += u;
-                        cd[c] += F.d_w * ((s2 * iv[c] - 1.0f) * is[c]);
-                    }
+                    const f2 d = q[r] - um;
+                    const f2 s2 = d * d;
+                    const f2 lpt = c0lg - (half * s2) * iv;
+                    lpp += d_w * lpt;
+                    const f2 u = d_w * (d * iv);
+                    g[r] += -u;
+                    cm += u;
+                    cd += d_w * ((s2 * iv - one) * is);
                 }
             }
+            // the own prior of this lane's shared parameter (moment form with
+            // the constant scale's reciprocals, as the sliced terms); its log p
+            // enters slice 0's record
+            float g_own = 0.0f;
+            {
+                const float v = sh.q;
+                const float d = own.hn ? v : v - o_m;
+                const float d2 = d * d;
+                const bool out = own.hn && !(v >= 0.0f);
+                const float lpe = out ? -__builtin_inff() : o_c0l - (0.5f * d2) * o_cinv2;
+                const float lp_own = o_wn * lpe;
+                g_own = (out || !own.on) ? 0.0f : o_wn * -(d * o_cinv2);
+                if (own_lp0) lpp[0] += lp_own;
+                if (own_lp1) lpp[1] += lp_own;
+            }
             MC_STAMP(1);
-            // wave totals, reduce-scattered: pair P = 2 item + chain
+            // wave totals, reduce-scattered: pair P = 2 slot + chain
             float xr[2 * NRS];
             {
                 float v[8 * NRS];
@@ -450,34 +532,47 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 for (int x = 0; x < 8 * NRS; ++x) v[x] = 0.0f;
                 v[0] = lpp[0];
                 v[1] = lpp[1];
+                if constexpr (CF) {
+                    if (FORM & LF_SWS) {
+                        v[2 + 2 * lf_slot_sws(FORM)] = cs[0];
+                        v[3 + 2 * lf_slot_sws(FORM)] = cs[1];
+                    }
+                    if (FORM & LF_DM) {
+                        v[2 + 2 * lf_slot_dm(FORM)] = cm[0];
+                        v[3 + 2 * lf_slot_dm(FORM)] = cm[1];
+                    }
+                    if (FORM & LF_DS) {
+                        v[2 + 2 * lf_slot_ds(FORM)] = cd[0];
+                        v[3 + 2 * lf_slot_ds(FORM)] = cd[1];
+                    }
+                } else {
 #pragma unroll
-                for (int k = 0; k < NSH; ++k)
+                    for (int k = 0; k < NSH; ++k)
 #pragma unroll
-                    for (int c = 0; c < 2; ++c)
-                        v[2 + 2 * k + c] = ((F.sw_ks == k ? cs[c] : 0.0f) +
-                                            (F.d_km == k ? cm[c] : 0.0f)) +
-                                           (F.d_ks == k ? cd[c] : 0.0f);
+                        for (int c = 0; c < 2; ++c)
+                            v[2 + 2 * k + c] = ((F.sw_ks == k ? cs[c] : 0.0f) +
+                                                (F.d_km == k ? cm[c] : 0.0f)) +
+                                               (F.d_ks == k ? cd[c] : 0.0f);
+                }
 #pragma unroll
-                for (int q = 0; q < NRS; ++q) {
+                for (int qq = 0; qq < NRS; ++qq) {
                     float vv[8], xx[2];
 #pragma unroll
-                    for (int x = 0; x < 8; ++x) vv[x] = v[8 * q + x];
+                    for (int x = 0; x < 8; ++x) vv[x] = v[8 * qq + x];
                     lf_rs8(vv, xx);
-                    xr[2 * q] = xx[0];
-                    xr[2 * q + 1] = xx[1];
+                    xr[2 * qq] = xx[0];
+                    xr[2 * qq + 1] = xx[1];
                 }
             }
-            // the kinetic partials of the first / last step (uniform)
+            // the kinetic partials of the last step (uniform)
             float k1w[2] = {0.f, 0.f};
             if (l == L - 1) {
-                float k1p[2] = {0.f, 0.f};
+                f2 k1p = {0.f, 0.f};
 #pragma unroll
-                for (int c = 0; c < 2; ++c)
-#pragma unroll
-                    for (int r = 0; r < RS; ++r) {
-                        const float pj = R.p[r][c] + h[c] * R.g[r][c];
-                        k1p[c] += pj * pj;
-                    }
+                for (int r = 0; r < RS; ++r) {
+                    const f2 pj = p[r] + h * g[r];
+                    k1p += pj * pj;
+                }
                 k1w[0] = wave_sum(k1p[0]);
                 k1w[1] = wave_sum(k1p[1]);
             }
@@ -488,7 +583,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 // first / last step (lanes 2, 3 of rows 0 / 1)
                 int pp = -1;
                 float pv = 0.0f;
-                if (pub_pair >= 0 && pub_pair < NV) {
+                if (pub_rec) {
                     pp = pub_pair;
                     pv = xr[0];
 #pragma unroll
@@ -516,45 +611,22 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 sweep(M1, M2);
             }
             // poll: pass ps reads pair 4 ps + perm[row] of slice col
-            float vals[NPASS];
-            uint32_t need = 0;
-            unsigned long long y0[NPASS];
             const bool kstep = (l == 0) || (l == L - 1);
+            uint32_t need = need_v | (l == 0 ? need_k0 : 0u) | (l == L - 1 ? need_k1 : 0u);
+            float vals[NPASS];
+            unsigned long long* gp = gline[par] + col * 16 + lf_row(row);
 #pragma unroll
             for (int ps = 0; ps < NPASS; ++ps) {
-                const int pr = 4 * ps + lf_row(row);
-                const bool want = !X1 && poll_lane && pr < NPAIR && (pr < NV || kstep) &&
-                                  (pr < NV || (pr < NV + 2 ? l == 0 : l == L - 1));
-                y0[ps] = want ? granule_load(gline[par] + col * 16 + pr) : 0ull;
                 vals[ps] = 0.0f;
-                if (want) need |= 1u << ps;
-            }
-            // the own priors of the shared parameters (lanes holding one)
-            float lp_own = 0.0f, g_own = 0.0f;
-            if (own.on) {
-                const float v = sh.q;
-                const float d = own.hn ? v : v - own.m;
-                const float d2 = d * d;
-                const bool out = own.hn && !(v >= 0.0f);
-                const float lpe = out ? -__builtin_inff() : own.c0l - (0.5f * d2) * own.cinv2;
-                lp_own = own.wn * lpe;
-                g_own = out ? 0.0f : own.wn * -(d * own.cinv2);
-            }
-            float slp[2] = {0.f, 0.f};
-            for (int k = 0; k < Dsh; ++k) {
-                slp[0] += lf_sh(lp_own, k, 0);
-                slp[1] += lf_sh(lp_own, k, 1);
-            }
-            MC_STAMP(7);
-#pragma unroll
-            for (int ps = 0; ps < NPASS; ++ps) {
                 if ((need >> ps) & 1u) {
-                    if ((uint32_t)(y0[ps] >> 32) == epoch) {
-                        vals[ps] = __uint_as_float((uint32_t)y0[ps]);
+                    const unsigned long long y = granule_load(gp + 4 * ps);
+                    if ((uint32_t)(y >> 32) == epoch) {
+                        vals[ps] = __uint_as_float((uint32_t)y);
                         need &= ~(1u << ps);
                     }
                 }
             }
+            MC_STAMP(7);
             uint32_t spins = 0;
             while (__ballot(need != 0)) {
                 if (++spins > kSpinLimit) {
@@ -565,8 +637,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
 #pragma unroll
                 for (int ps = 0; ps < NPASS; ++ps) {
                     if ((need >> ps) & 1u) {
-                        const int pr = 4 * ps + lf_row(row);
-                        const unsigned long long y = granule_load(gline[par] + col * 16 + pr);
+                        const unsigned long long y = granule_load(gp + 4 * ps);
                         if ((uint32_t)(y >> 32) == epoch) {
                             vals[ps] = __uint_as_float((uint32_t)y);
                             need &= ~(1u << ps);
@@ -598,18 +669,18 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     tot[ps] = t;
                 }
             }
-            // totals: the slice sum plus the own priors' sum
-            lpn[0] = (rl(tot[0], 0) + slp[0]) + P.lp_const;
-            lpn[1] = (rl(tot[0], 16 * lf_row(1)) + slp[1]) + P.lp_const;
+            // totals: the slice sum (the own priors are in slice 0's record)
+            lpn[0] = rl(tot[0], 0) + lp_const;
+            lpn[1] = rl(tot[0], 16 * lf_row(1)) + lp_const;
             {
                 float gx = 0.0f;
 #pragma unroll
                 for (int ps = 0; ps < NPASS_V; ++ps)
-                    if (j % 16 == ps) gx = tot[ps];  // lane 16 row + P / 4 holds pair P
+                    if (col == ps) gx = tot[ps];  // lane 16 row + P / 4 holds pair P
                 sh.g = xon ? gx + g_own : 0.0f;
             }
             if (l == 0) {
-                const int p0 = NV, p1 = NV + 1;
+                constexpr int p0 = NV, p1 = NV + 1;
                 if constexpr (X1) {
                     K0[0] = K0w[0];
                     K0[1] = K0w[1];
@@ -619,7 +690,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 }
             }
             if (l == L - 1) {
-                const int p0 = NV + 2, p1 = NV + 3;
+                constexpr int p0 = NV + 2, p1 = NV + 3;
                 if constexpr (X1) {
                     K1[0] = k1w[0];
                     K1[1] = k1w[1];
@@ -637,7 +708,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         {
             const float p1 = sh.p + xh * sh.g;
             const float p2 = p1 * p1;
-            for (int k = 0; k < Dsh; ++k) {
+            for (int k = 0; k < nsl; ++k) {
                 k1s[0] += lf_sh(p2, k, 0);
                 k1s[1] += lf_sh(p2, k, 1);
             }
@@ -660,15 +731,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 const double rate = (double)nacc[c] / (double)ntot[c];
                 eps[c] = (rate < cfg.target_accept) ? eps_used * 0.95 : eps_used * 1.05;
             }
-            if (accepted) {
-                lp[c] = lpn[c];
-            } else {
-#pragma unroll
-                for (int r = 0; r < RS; ++r) {
-                    R.q[r][c] = q0[r][c];
-                    R.g[r][c] = g0[r][c];
-                }
-            }
+            if (accepted) lp[c] = lpn[c];
             if (slice == 0 && j == 0 && live[c]) {
                 const int64_t ti = it - tr.iter_begin;
                 if (ti >= 0 && ti < tr.capacity) {
@@ -681,6 +744,11 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     if (tr.n_leapfrog) tr.n_leapfrog[o] = L;
                 }
             }
+        }
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            q[r] = (f2){acc[0] ? q[r][0] : q0[r][0], acc[1] ? q[r][1] : q0[r][1]};
+            g[r] = (f2){acc[0] ? g[r][0] : g0[r][0], acc[1] ? g[r][1] : g0[r][1]};
         }
         if (!(xc ? acc[1] : acc[0])) {
             sh.q = q0s;
@@ -695,7 +763,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     float* out = samples + (cc[c] * cfg.sample_capacity + s) * (int64_t)D;
 #pragma unroll
                     for (int r = 0; r < RS; ++r)
-                        if (gk[r] >= 0) out[gk[r]] = R.q[r][c];
+                        if (gk[r] >= 0) out[gk[r]] = q[r][c];
                 }
                 if (slice == 0 && xlive)
                     samples[(xch_id * cfg.sample_capacity + s) * (int64_t)D + xg] = sh.q;
@@ -713,8 +781,8 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             if (gk[r] >= 0) {
-                st_q[cc[c] * D + gk[r]] = R.q[r][c];
-                st_g[cc[c] * D + gk[r]] = R.g[r][c];
+                st_q[cc[c] * D + gk[r]] = q[r][c];
+                st_g[cc[c] * D + gk[r]] = g[r][c];
             }
         }
         if (slice == 0 && j == 0) {
