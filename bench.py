@@ -78,7 +78,14 @@ def parse():
                     help="kernel of the sliced program (csrc/lanes.h or csrc/sliced.h)")
     ap.add_argument("--gather", action="store_true",
                     help="also gather every rank's samples to rank 0 over RCCL (untimed)")
-    return ap.parse_args()
+    ap.add_argument("--workload", default="hmc", choices=["hmc", "nuts"],
+                    help="hmc: the headline (BASELINE configs[2]/[3]); nuts: BASELINE "
+                         "configs[4] (NUTS depth 10 + dual averaging, 100-dim kappa = 1000 "
+                         "Gaussian, 64 chains per GPU; a measurement line, not the headline)")
+    args = ap.parse_args()
+    if args.workload == "nuts" and not any(a.startswith("--chains") for a in sys.argv[1:]):
+        args.chains = 64
+    return args
 
 
 def cpu_model() -> str:
@@ -218,8 +225,143 @@ def check(chains, where):
         sys.exit(3)
 
 
+NUTS_D = 100
+# SURVEY 8d unit for NUTS: one leaf (leapfrog step + gradient + Hamiltonian);
+# algorithmic FP32 flops per leaf of the D-dim diagonal Gaussian: kicks and
+# drift 6D, kinetic energy 2D, the Normal tape with a per-element scale 7D
+# (d, d^2, 0.5 d^2, / var, c0 - log s, -, d / var), U-turn dot products at the
+# merges <= 4D amortised
+NUTS_FLOPS_PER_LEAF = 19 * NUTS_D
+
+
+def nuts_cpu_baseline(budget_s):
+    """The oracle's NUTS (reference cost structure: two gradients per leaf,
+    recursive build_tree) on the same model, one chain, one thread: leaves/s."""
+    import torch
+
+    import workloads as W
+    from oracle import samplers as S
+
+    torch.set_num_threads(1)
+    lp, init = W.illcond_normal(W.ns_oracle(), NUTS_D)
+    leaves, t0, runs = 0, time.perf_counter(), 0
+    while time.perf_counter() - t0 < budget_s:
+        r = S.nuts(lp, init, num_samples=20, num_warmup=20, step_size=0.1, max_tree_depth=10,
+                   seed=runs)
+        leaves += int(sum(r.trace["leaves"]))
+        runs += 1
+    dt = time.perf_counter() - t0
+    return {"value": leaves / dt, "unit": "leaf-steps/s", "cores": 1, "kind": "port",
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": (f"oracle/samplers.py NUTS restatement (torch-CPU autograd, 2 gradients per "
+                       f"leaf), 1 chain, 1 thread: {runs} runs of 20 warmup + 20 sampling "
+                       f"iterations (depth <= 10) on the same D={NUTS_D} model, {leaves} leaves "
+                       f"in {dt:.1f} s")}
+
+
+def main_nuts(args):
+    """BASELINE configs[4]: NUTS (depth 10, dual averaging) on the 100-dim
+    kappa = 1000 Gaussian; value = leaves (leapfrog steps) of all chains per
+    second over the timed sampling iterations."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    _ensure_pkg()
+    import workloads as W
+    from mlx_mcmc_amd import _engine, _trace
+    from mlx_mcmc_amd.distributed import max_over_ranks, shard
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    C, K, Wm, B = args.chains, args.steps, args.warmup, max(1, args.iters_per_launch)
+    lp_fn, init = W.illcond_normal(W.ns_product(), NUTS_D)
+    prog = _trace.compile_model(lp_fn, init)
+    chains = _engine.ChainSet(prog, C, prog.layout.flatten(init), 0.1, device=dev)
+    samples = torch.empty((C, max(K, 1), NUTS_D), dtype=torch.float32, device=dev)
+    chain_offset, _ = shard(C * world, world, rank)
+    cfg = dict(chain_offset=chain_offset, num_warmup=Wm, num_samples=K, sample_begin=0,
+               sample_capacity=K, seed=args.seed, step_size=0.1, target_accept=0.8,
+               max_tree_depth=10, adapt_step_size=True, slice_mode=0)
+
+    def launches(first, count):
+        return [(first + i, min(B, count - i)) for i in range(0, count, B)]
+
+    for it0, n in launches(0, Wm):
+        chains.run_nuts(samples=samples, iter_begin=it0, iter_count=n, **cfg)
+    torch.cuda.synchronize()
+    g0 = chains.scalars()["n_grad"].astype(np.int64)
+    stream = torch.cuda.current_stream()
+    timed = launches(Wm, K)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in timed]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for (it0, n), (e0, e1) in zip(timed, ev):
+        e0.record(stream)
+        chains.run_nuts(samples=samples, iter_begin=it0, iter_count=n, **cfg)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    sc = chains.scalars()
+    leaves = int(np.sum(sc["n_grad"].astype(np.int64) - g0))
+    full = [a.elapsed_time(b) for (a, b), (_, n) in zip(ev, timed) if n == B] or \
+           [a.elapsed_time(b) for (a, b), _ in zip(ev, timed)]
+    launch_ms = float(np.mean(full)) if K else float("nan")
+    launch_ms_total = float(sum(a.elapsed_time(b) for a, b in ev))
+    elapsed = max_over_ranks(elapsed, device=dev)
+    leaves_all = int(max_over_ranks(float(leaves), device=dev)) * world if world > 1 else leaves
+    if rank == 0:
+        value = leaves_all / elapsed
+        # per launch: the timed leaves spread over the launches by their time
+        leaves_per_launch = leaves * (launch_ms / launch_ms_total) if launch_ms_total else 0.0
+        achieved = leaves_per_launch * NUTS_FLOPS_PER_LEAF / (launch_ms * 1e-3) / 1e12
+        out = {
+            "metric": "leapfrog-steps/sec (all chains), NUTS 100-dim kappa=1000 Gaussian",
+            "value": value, "unit": "leaf-steps/s", "n_gpus": world, "steps": K,
+            "warmup": Wm, "ms_per_step": elapsed * 1e3 / max(K, 1), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (fixed kappa = 1000 diagonal scales, SURVEY §8d config 5)",
+            "config": {"workload": (f"NUTS depth 10 + dual averaging (BASELINE configs[4]): "
+                                    f"D={NUTS_D}, kappa=1000, {C} chains per GPU"),
+                       "num_params": NUTS_D, "max_tree_depth": 10, "chains_per_gpu": C,
+                       "total_chains": C * world, "parallelism": f"chains sharded {C}/GPU"},
+            "roofline": {
+                "bound": "valu_fp32", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
+                "kernel": f"k_nuts<{prog.waves_per_chain}>", "launch_ms": launch_ms,
+                "iters_per_launch": B, "flops_per_leaf": NUTS_FLOPS_PER_LEAF,
+                "note": (f"latency bound: {C} chains = {C * prog.waves_per_chain} waves on "
+                         "1024 SIMDs; F = 19 D flops per leaf (SURVEY 8d unit: one leaf)")},
+            "leaves": leaves, "mean_tree_depth": float(np.mean(sc["depth_sum"] / np.maximum(
+                sc["n_total"], 1))),
+            "accept_stat_mean": float(np.mean(sc["alpha_sum"]) / max(Wm + K, 1)),
+            "step_size": float(np.mean(sc["step_size"])),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb = nuts_cpu_baseline(min(args.cpu_seconds, 15.0))
+            cb["gpu_over_cpu"] = value / cb["value"]
+            out["cpu_baseline"] = cb
+        print(json.dumps(out), flush=True)
+    del chains, prog, samples
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.workload == "nuts":
+        return main_nuts(args)
     import numpy as np
     import torch
     import torch.distributed as dist

@@ -131,14 +131,24 @@ MC_DEV void lf_moments(const float* xv, int len, int lmin4, f2 th, f2& s1, f2& s
             elem(a[q].w, 1);
         }
     }
-    for (; u4 < lmin4; ++u4) {
+    // the lane's remaining full groups (a lane-varying count), then its last
+    // partial group: elements in the accumulators of their parity, no
+    // per-element accumulator select
+    const int len4 = len >> 2;
+    for (; u4 < len4; ++u4) {
         const float4 a = *(const float4*)(xv + u4 * 256);
         elem(a.x, 0);
         elem(a.y, 1);
         elem(a.z, 0);
         elem(a.w, 1);
     }
-    for (int u = 4 * u4; u < len; ++u) elem(xv[(u >> 2) * 256 + (u & 3)], u & 1);
+    const int rem = len & 3;
+    if (rem) {
+        const float4 a = *(const float4*)(xv + u4 * 256);
+        elem(a.x, 0);
+        if (rem > 1) elem(a.y, 1);
+        if (rem > 2) elem(a.z, 0);
+    }
     s1 = a1[0] + a1[1];
     s2 = a2[0] + a2[1];
 }
@@ -374,6 +384,10 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         gline[par] = xch + (((int64_t)par * n_groups + grp) * (NB / 2) + wave) * S * 16;
     const int row = j >> 4, col = j & 15;
     const bool poll_lane = col < S;
+    // the poll address of pass 0 (pass ps: + 4 ps), per epoch parity
+    unsigned long long* gp[2];
+#pragma unroll
+    for (int par = 0; par < 2; ++par) gp[par] = gline[par] + min(col, S - 1) * 16 + lf_row(row);
     // publishing: lanes 16 r + n (n < NRS * 2) hold pair 8 (n / 2) + 4 (n % 2) + perm[r]
     const int pub_pair = (col < 2 * NRS) ? 8 * (col >> 1) + 4 * (col & 1) + lf_row(row) : -1;
     const bool pub_rec = pub_pair >= 0 && pub_pair < NV;
@@ -614,18 +628,24 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             const bool kstep = (l == 0) || (l == L - 1);
             uint32_t need = need_v | (l == 0 ? need_k0 : 0u) | (l == L - 1 ? need_k1 : 0u);
             float vals[NPASS];
-            unsigned long long* gp = gline[par] + col * 16 + lf_row(row);
 #pragma unroll
-            for (int ps = 0; ps < NPASS; ++ps) {
-                vals[ps] = 0.0f;
-                if ((need >> ps) & 1u) {
-                    const unsigned long long y = granule_load(gp + 4 * ps);
-                    if ((uint32_t)(y >> 32) == epoch) {
-                        vals[ps] = __uint_as_float((uint32_t)y);
+            for (int ps = 0; ps < NPASS; ++ps) vals[ps] = 0.0f;
+            // every pass's granules loaded at once (one round trip; lanes that
+            // need none read an in-bounds line and ignore it), then checked
+            auto poll = [&]() {
+                unsigned long long y[NPASS];
+#pragma unroll
+                for (int ps = 0; ps < NPASS; ++ps)
+                    y[ps] = (ps < NPASS_V || kstep) ? granule_load(gp[par] + 4 * ps) : 0ull;
+#pragma unroll
+                for (int ps = 0; ps < NPASS; ++ps) {
+                    if (((need >> ps) & 1u) && (uint32_t)(y[ps] >> 32) == epoch) {
+                        vals[ps] = __uint_as_float((uint32_t)y[ps]);
                         need &= ~(1u << ps);
                     }
                 }
-            }
+            };
+            if (!X1) poll();
             MC_STAMP(7);
             uint32_t spins = 0;
             while (__ballot(need != 0)) {
@@ -634,16 +654,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-                for (int ps = 0; ps < NPASS; ++ps) {
-                    if ((need >> ps) & 1u) {
-                        const unsigned long long y = granule_load(gp + 4 * ps);
-                        if ((uint32_t)(y >> 32) == epoch) {
-                            vals[ps] = __uint_as_float((uint32_t)y);
-                            need &= ~(1u << ps);
-                        }
-                    }
-                }
+                poll();
             }
             if (!ok) {
                 __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
