@@ -107,6 +107,17 @@ MC_DEV void lf_rs8(const float (&v)[8], float (&x)[2]) {
     }
 }
 
+// (xy.y, xy.y) - th in one v_pk_add_f32: the backend copies the odd register
+// of a pair to an even one before broadcasting it (one v_mov per element
+// pair); op_sel on the pair reads it in place.
+MC_DEV f2 lf_hi_minus(f2 xy, f2 th) {
+    f2 d;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]"
+        : "=v"(d)
+        : "v"(xy), "v"(th));
+    return d;
+}
+
 // Moment sums of one lane's run (value = data x, loc = the lane's private
 // parameter th) for both chains, packed FP32: d = x - th, s1 += d,
 // s2 = fma(d, d, s2), with the even and odd elements in separate packed
@@ -118,17 +129,29 @@ MC_DEV void lf_moments(const float* xv, int len, int lmin4, f2 th, f2& s1, f2& s
         a1[hh] += d;
         a2[hh] = pk_fma(d, d, a2[hh]);
     };
+    // a register pair's elements broadcast by swizzle (op_sel on the pair,
+    // no copy of the odd register)
+    auto pair = [&](f2 xy) {
+        const f2 d0 = xy.xx - th;
+        a1[0] += d0;
+        a2[0] = pk_fma(d0, d0, a2[0]);
+        const f2 d1 = lf_hi_minus(xy, th);
+        a1[1] += d1;
+        a2[1] = pk_fma(d1, d1, a2[1]);
+    };
     int u4 = 0;
     for (; u4 + 4 <= lmin4; u4 += 4) {
-        float4 a[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a[q] = *(const float4*)(xv + (u4 + q) * 256);
+        f2 a[4][2];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            elem(a[q].x, 0);
-            elem(a[q].y, 1);
-            elem(a[q].z, 0);
-            elem(a[q].w, 1);
+            const float4 v = *(const float4*)(xv + (u4 + q) * 256);
+            a[q][0] = (f2){v.x, v.y};
+            a[q][1] = (f2){v.z, v.w};
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            pair(a[q][0]);
+            pair(a[q][1]);
         }
     }
     // the lane's remaining full groups (a lane-varying count), then its last
