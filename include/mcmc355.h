@@ -159,6 +159,12 @@ int32_t mc_program_slice_kernel(const mc_program* prog);
  * broadcast parameter; MC_LANES_FAST=0 in the environment turns it off),
  * 0 when it runs k_hmc_lr or no lane-resident kernel, -1 on a null program. */
 int32_t mc_program_lanes_fast(const mc_program* prog);
+/* 1 when mc_nuts_run with this max_tree_depth runs the lane-resident NUTS
+ * kernel k_nuts_lr (a program planned as one lane-resident slice; its arena
+ * fits LDS; MC_NUTS_LANES=0 in the environment turns it off), 0 when it runs
+ * k_nuts, -1 on a null program.  Both take the reference's decisions; they
+ * differ in fp32 summation order only.                                      */
+int32_t mc_program_nuts_lanes(const mc_program* prog, int32_t max_tree_depth);
 
 /* Batched tape evaluation: for every point p, logp[p] = log density at
  * q[p, :] and grad[p, :] = its gradient (replaces hmc.py:53-67 mx.grad).   */

@@ -503,6 +503,11 @@ class Program:
         k = _lib.load().mc_program_slice_kernel(self.handle)
         return {0: "unsliced", 1: "interpreter", 2: "lanes"}[k]
 
+    def nuts_kernel(self, max_tree_depth: int = 10) -> str:
+        """"lanes" (k_nuts_lr) or "tape" (k_nuts): what mc_nuts_run will run."""
+        k = _lib.load().mc_program_nuts_lanes(self.handle, int(max_tree_depth))
+        return "lanes" if k == 1 else "tape"
+
     @property
     def lanes_fast(self) -> bool:
         """True when a lane-resident launch runs the fast-form kernel k_hmc_lf."""

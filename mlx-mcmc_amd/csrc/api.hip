@@ -23,6 +23,7 @@
 #include "internal.h"
 #include "lanes.h"
 #include "lanes_fast.h"
+#include "nuts_lanes.h"
 #include "mh.h"
 #include "nuts.h"
 #include "philox.h"
@@ -895,6 +896,12 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
                 else if (a == SK_PP && b == SK_DATA && c == SK_SHARED) lt.sig = LS_PP_DATA_SH;
                 else if (a == SK_DATA && b == SK_SHARED && c == SK_SHARED) lt.sig = LS_DATA_SH_SH;
             }
+            // Normal with a per-element data scale, one of value / loc private
+            // (theta ~ N(m, s_i), y_i ~ N(theta_g, s_i)): lanes.h lr_dscale_term
+            if (rt.dist == MC_DIST_NORMAL && lt.kind[2] == SK_DATA && lt.pp >= 0 && lt.pp <= 1 &&
+                lt.kind[lt.pp] == SK_PP && lt.kind[1 - lt.pp] != SK_PP &&
+                lt.kind[1 - lt.pp] != SK_NONE)
+                lt.sig = LS_DSCALE;
             // element lists per (slot, lane), in element order
             std::vector<std::vector<int64_t>> lists((size_t)kLrMaxSlots * 64);
             int nslot = 1;
@@ -945,6 +952,26 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
                                 dp[src + li[u]];
                     }
                 lt.doff[a] = (int32_t)(base - blk0);
+            }
+            if (lt.sig == LS_DSCALE) {
+                // the scale tile becomes 1/s^2 and the private operand's (free)
+                // tile holds f32 log s, per element, as the constant-scale
+                // terms' cinv2 / clogs
+                const int64_t sb = blk0 + lt.doff[2];
+                while (L.data.size() % 4) L.data.push_back(0.0f);
+                const int64_t base = (int64_t)L.data.size();
+                L.data.resize(base + tot, 0.0f);
+                for (int r = 0; r < nslot; ++r)
+                    for (int l = 0; l < 64; ++l) {
+                        const size_t nl = lists[(size_t)r * 64 + l].size();
+                        for (size_t u = 0; u < nl; ++u) {
+                            const int64_t o = lt.toff[r] + (u >> 2) * 256 + 4 * l + (u & 3);
+                            const float sc = L.data[sb + o];
+                            L.data[base + o] = (float)std::log((double)sc);
+                            L.data[sb + o] = 1.0f / (sc * sc);
+                        }
+                    }
+                lt.doff[lt.pp] = (int32_t)(base - blk0);
             }
             const int64_t lo = (int64_t)L.data.size();
             L.data.resize(lo + lens.size());
@@ -2176,6 +2203,49 @@ static int launch_nuts(const mc_program* p, const mc_run_config* cfg, void* stat
     return MC_OK;
 }
 
+// The lane-resident NUTS kernel (nuts_lanes.h) for programs planned as one
+// lane-resident slice (the layout k_hmc_lr runs with X1), unless
+// MC_NUTS_LANES=0 in the environment (A/B timing against k_nuts) or the
+// arena does not fit the LDS budget.
+static bool nuts_lanes_enabled() {
+    static int on = -1;
+    if (on < 0) {
+        const char* e = std::getenv("MC_NUTS_LANES");
+        on = (e && e[0] == '0') ? 0 : 1;
+    }
+    return on == 1;
+}
+static size_t nuts_lr_lds_bytes(const mc_program* p, int max_depth) {
+    return (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm) +
+           (size_t)nuts_lr_arena_floats(p->lr.rs, max_depth) * 4;
+}
+static bool use_nuts_lanes(const mc_program* p, int max_depth) {
+    return nuts_lanes_enabled() && p->sl.S < 2 && p->lr.ok && p->lr.S == 1 &&
+           p->slice_kernel != 1 && nuts_lr_lds_bytes(p, max_depth) <= (size_t)kSlLdsBudget;
+}
+extern "C" int32_t mc_program_nuts_lanes(const mc_program* p, int32_t max_tree_depth) {
+    if (!p) return -1;
+    return use_nuts_lanes(p, max_tree_depth) ? 1 : 0;
+}
+
+template <int RS, int NSH>
+static int launch_nuts_lr(const mc_program* p, const mc_run_config* cfg, void* state,
+                          float* samples, const mc_trace* tr, hipStream_t st) {
+    int64_t qo, go;
+    mc_state_offsets(p, cfg->num_chains, &qo, &go);
+    char* b = (char*)state;
+    RunArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.cfg = *cfg;
+    const size_t lds = nuts_lr_lds_bytes(p, cfg->max_tree_depth);
+    MC_HIP_TRY(allow_lds(k_nuts_lr<RS, NSH>, lds));
+    hipLaunchKernelGGL((k_nuts_lr<RS, NSH>), dim3((unsigned)cfg->num_chains), dim3(64), lds, st,
+                       lrctx_of(p), A, (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go),
+                       samples, trace_of(tr));
+    MC_HIP_TRY(hipGetLastError());
+    return MC_OK;
+}
+
 extern "C" int mc_nuts_run(const mc_program* p, const mc_run_config* cfg, void* state,
                            float* samples, const mc_trace* tr, void* ws, int64_t ws_bytes,
                            void* stream) {
@@ -2189,6 +2259,17 @@ extern "C" int mc_nuts_run(const mc_program* p, const mc_run_config* cfg, void* 
         return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
     if (ws) ws_forget(ws);  // another kernel's data: a later sliced launch clears it
     hipStream_t st = (hipStream_t)stream;
+    if (use_nuts_lanes(p, cfg->max_tree_depth)) {
+        const bool n4 = p->lr.Dsh > 3;
+        switch (p->lr.rs) {
+            case 1: return n4 ? launch_nuts_lr<1, 4>(p, cfg, state, samples, tr, st)
+                              : launch_nuts_lr<1, 3>(p, cfg, state, samples, tr, st);
+            case 2: return n4 ? launch_nuts_lr<2, 4>(p, cfg, state, samples, tr, st)
+                              : launch_nuts_lr<2, 3>(p, cfg, state, samples, tr, st);
+            default: return n4 ? launch_nuts_lr<4, 4>(p, cfg, state, samples, tr, st)
+                               : launch_nuts_lr<4, 3>(p, cfg, state, samples, tr, st);
+        }
+    }
     float* w = (float*)ws;
     const bool lds = nuts_use_lds(p, cfg->max_tree_depth);
     switch (p->wpc) {

@@ -68,6 +68,8 @@ enum : int32_t {
     LS_PP_C_C = 4,       // theta ~ Normal(const, const)
     LS_PP_DATA_SH = 5,   // theta ~ Normal(m_data, tau)
     LS_DATA_SH_SH = 6,   // y ~ Normal(mu, sigma)              chunked likelihood
+    LS_DSCALE = 7,       // theta ~ Normal(m, s_i), y_i ~ Normal(theta_g, s_i): a per-element
+                         // data scale (tiles of 1/s^2 and log s), one of value / loc private
 };
 
 // A scalar term (constants and shared parameters only), compact for LDS.
@@ -396,6 +398,57 @@ MC_DEV void lr_finish(const MC_CONST LrTerm* tt, int nsweep, int ndirect, LrPriv
     }
 }
 
+// A Normal term with a per-element data scale (LS_DSCALE): the planner
+// stored 1/s^2 in the scale's tile and f32 log s in the private operand's
+// tile; the other of value / loc is a constant, a shared parameter or data.
+// Per element, both chains packed: d = value - loc,
+// lp = (c0 - log s) - (0.5 d^2) / s^2, d lp / d value = -d / s^2.
+template <int RS>
+MC_DEV void lr_dscale_term(const MC_CONST LrTerm* T, const float* sd, int j, LrPriv<RS>& R,
+                           const LrShared& sh, float (&lpp)[2],
+                           float (&gshp)[kLrMaxShared][2]) {
+    const int ppo = T->pp;  // 0: value private (loc the other), 1: loc private
+    const int oth = 1 - ppo;
+    const int ko = T->kind[oth], jo = T->jsh[oth];
+    const int nslot = T->nslot;
+    const f2 w = f2s(T->weight), c0 = f2s(T->c0), half = f2s(0.5f);
+    const int32_t* lens = (const int32_t*)sd + T->len_off;
+    const f2 uo = ko == SK_SHARED ? (f2){rl(sh.q, 2 * jo), rl(sh.q, 2 * jo + 1)}
+                                  : f2s(T->cval[oth]);
+    f2 lp = {0.f, 0.f}, po = {0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+        if (r >= nslot) break;
+        const int len = lens[r * 64 + j];
+        if (len <= 0) continue;
+        const int toff = T->toff[r] + 4 * j;
+        const float* xo = sd + T->doff[oth] + toff;
+        const float* xl = sd + T->doff[ppo] + toff;
+        const float* xi = sd + T->doff[2] + toff;
+        const f2 th = {R.q[r][0], R.q[r][1]};
+        f2 gp = {0.f, 0.f};
+        for (int u = 0; u < len; ++u) {
+            const int o = (u >> 2) * 256 + (u & 3);
+            const f2 other = ko == SK_DATA ? f2s(xo[o]) : uo;
+            const f2 d = ppo == 0 ? th - other : other - th;
+            const f2 iv = f2s(xi[o]);
+            const f2 lpt = (c0 - f2s(xl[o])) - (half * (d * d)) * iv;
+            lp += w * lpt;
+            const f2 t = w * (d * iv);
+            gp += ppo == 0 ? -t : t;
+            po += ppo == 0 ? t : -t;
+        }
+        R.g[r][0] += gp[0];
+        R.g[r][1] += gp[1];
+    }
+    lpp[0] += lp[0];
+    lpp[1] += lp[1];
+    if (ko == SK_SHARED) {
+        add4(gshp, jo, 0, po[0]);
+        add4(gshp, jo, 1, po[1]);
+    }
+}
+
 // Log p partial of this slice at the current point; private gradients
 // (complete) into R.g, this lane's shared-cotangent partials into gshp.
 template <int RS>
@@ -422,6 +475,9 @@ MC_DEV void lr_eval(const MC_CONST LrTerm* tt, int t0, int nact, const float* sd
                 continue;
             case LS_DATA_SH_SH:
                 lr_normal_term<RS, SK_DATA, SK_SHARED, SK_SHARED>(T, sd, j, R, sh, lpp, gshp);
+                continue;
+            case LS_DSCALE:
+                lr_dscale_term<RS>(T, sd, j, R, sh, lpp, gshp);
                 continue;
             default:
                 break;

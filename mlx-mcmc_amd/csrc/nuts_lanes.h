@@ -1,0 +1,524 @@
+// nuts_lanes.h — lane-resident NUTS (k_nuts_lr): the iterative slice-NUTS of
+// k_nuts (nuts.h; reference nuts.py:16-358, same draws, same decisions rule
+// by rule) on the one-slice lane-resident layout of k_hmc_lr (lanes.h, X1).
+//
+// One chain per wave.  Each private parameter of the program is dealt to one
+// (lane, slot) and its elements are streamed by that lane from LDS (the
+// planner's one-slice layout); the broadcast parameters sit in lanes 2k, 2k+1
+// (lanes.h LrShared).  The lane evaluators of lanes.h advance two chains in
+// packed FP32; here both halves carry the same chain (a packed instruction
+// costs what a scalar one does), so every evaluator is reused unchanged.
+//
+//   * The trajectory ends (q, r, grad of both ends) and the current sample
+//     (q, grad) are registers; a leaf is a leapfrog step from one end, one
+//     lane-resident gradient evaluation (moment sweeps, per-element terms,
+//     scalar terms, one wave_sum8) and a wave sum of the kinetic energy.
+//   * The subtrees' first leaves (q, r) and the candidate pool (q, grad) —
+//     slots picked by run-time indices — are in an LDS arena, one float per
+//     (slot, component, register slot, lane): conflict-free, no global
+//     memory in the tree walk.
+//   * The small per-level arrays of the walk (pending candidate / count per
+//     level, the pool's log p) live one entry per lane and are read with
+//     readlane.
+//   * U-turn tests are two dot products over the parameters (lane partials +
+//     one DPP wave sum each); summation order differs from k_nuts (j-strided
+//     group sums), every decision rule is the reference's.
+#pragma once
+#include "lanes.h"
+#include "nuts.h"
+
+namespace mc {
+
+// LDS arena of one wave: first-leaf slots (q, r) [MAXJ + 1] and the candidate
+// pool (q, g) [MAXJ + 2], each RS private values + the lane's shared value.
+__host__ __device__ constexpr int64_t nuts_lr_arena_floats(int rs, int max_depth) {
+    return (2 * (int64_t)(max_depth + 1) + 2 * (int64_t)(max_depth + 2)) * (rs + 1) * 64;
+}
+
+template <int RS, int NSH>
+__global__ void __launch_bounds__(64)
+k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, float* samples,
+          TraceDev tr) {
+    static_assert(NSH <= kLrMaxShared, "shared parameters");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const mc_run_config& cfg = A.cfg;
+    const int j = threadIdx.x;  // lane
+    const int64_t c = blockIdx.x;
+    if (c >= cfg.num_chains) return;
+    const int D = P.D, Dsh = P.Dsh;
+    const int MAXJ = cfg.max_tree_depth;
+
+    // ---- the one slice's block and the scalar terms into LDS --------------------
+    float* sd = smem;
+    const int64_t* blk = P.blocks;
+    const int64_t doff = blk[0];
+    const int dlen = (int)blk[1];
+    const int nact = (int)blk[2];
+    const int nsweep = (int)(blk[3] & 255);
+    const int ndirect = (int)((blk[3] >> 8) & 255);
+    const int nfast = nsweep + ndirect;
+    for (int i = j; 4 * i < dlen; i += 64)
+        *(float4*)(sd + 4 * i) = *(const float4*)(P.data + doff + 4 * i);
+    LrSterm* sst = (LrSterm*)(smem + P.sdata_floats);
+    const int sterm_floats = P.n_sterms * (int)(sizeof(LrSterm) / 4);
+    for (int i = j; i < sterm_floats / 4; i += 64) ((float4*)sst)[i] = ((const float4*)P.sterms)[i];
+    float* ar = smem + P.sdata_floats + sterm_floats;  // the arena (16-byte aligned)
+    __syncthreads();
+
+    // arena addressing: slot s of kind 0 (first: q, r) or 1 (pool: q, g),
+    // component comp, register slot r (RS: the shared value)
+    const int nfirst = MAXJ + 1;
+    auto at = [&](int kind, int s, int comp, int r) -> float* {
+        const int row = kind == 0 ? 2 * s + comp : 2 * nfirst + 2 * s + comp;
+        return ar + ((int64_t)row * (RS + 1) + r) * 64 + j;
+    };
+
+    const MC_CONST LrTerm* tt = cptr(P.terms);
+    const LrOwn own = lr_own_prior(P.n_sterms, sst, j, Dsh);
+    LrCounts<RS> KC;
+#pragma unroll
+    for (int t = 0; t < kLrSweep; ++t)
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            KC.cs[t][r] = 0.0f;
+            if (t < nsweep && r < tt[t].nslot)
+                KC.cs[t][r] = (float)((const int32_t*)sd)[tt[t].len_off + r * 64 + j];
+        }
+#pragma unroll
+    for (int t = 0; t < kLrDirect; ++t)
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            KC.pd[t][r] = false;
+            if (t < ndirect && r < tt[nsweep + t].nslot)
+                KC.pd[t][r] = ((const int32_t*)sd)[tt[nsweep + t].len_off + r * 64 + j] > 0;
+        }
+
+    // this lane's parameters: private slots gk[r]; shared k = j / 2 (both
+    // lanes 2k, 2k + 1 hold it: the two packed halves are the same chain)
+    int gk[RS];
+#pragma unroll
+    for (int r = 0; r < RS; ++r) gk[r] = P.gidx[(int64_t)r * 64 + j];
+    const int xk = j >> 1;
+    const bool xon = j < 2 * Dsh;
+    const bool xone = xon && (j & 1) == 0;  // counts the shared parameter once in sums
+    int xg = P.shl[0];
+#pragma unroll
+    for (int k = 1; k < kLrMaxShared; ++k) xg = (xk == k) ? P.shl[k] : xg;
+
+    // current sample (q, grad), both halves
+    f2 Cq[RS], Cg[RS];
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+        const float q = gk[r] >= 0 ? st_q[c * D + gk[r]] : 0.0f;
+        const float g = gk[r] >= 0 ? st_g[c * D + gk[r]] : 0.0f;
+        Cq[r] = (f2){q, q};
+        Cg[r] = (f2){g, g};
+    }
+    float Cqs = xon ? st_q[c * D + xg] : 1.0f, Cgs = xon ? st_g[c * D + xg] : 0.0f;
+
+    // the log density and gradient at (R.q, sh.q): R.g, sh.g; returns log p
+    LrPriv<RS> R;
+    LrShared sh;
+    auto derive = [&]() {
+        sh.is = 1.0f / sh.q;
+        sh.iv = 1.0f / (sh.q * sh.q);
+        sh.lg = logf(sh.q);
+    };
+    auto evaluate = [&]() -> float {
+        float gshp[kLrMaxShared][2];
+#pragma unroll
+        for (int k = 0; k < kLrMaxShared; ++k) gshp[k][0] = gshp[k][1] = 0.0f;
+#pragma unroll
+        for (int r = 0; r < RS; ++r) R.g[r][0] = R.g[r][1] = 0.0f;
+        LrMoments<RS> M;
+        lr_sweep<RS>(tt, nsweep, sd, j, R, M);
+        f2 lpp2 = {0.f, 0.f};
+        lr_finish<RS>(tt, nsweep, ndirect, R, sh, M, KC, lpp2, gshp);
+        float lpp[2] = {lpp2[0], lpp2[1]};
+        lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp);
+        float slp[2] = {0.f, 0.f}, sg_self = 0.0f;
+        lr_scalar_terms(P.n_sterms, P.n_sterms_generic, sst, own, sh, j, Dsh, slp, sg_self);
+        float v8[8], t8[8];
+        v8[0] = lpp[0];
+        v8[1] = lpp[1];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            v8[2 + 2 * k] = gshp[k][0];
+            v8[3 + 2 * k] = gshp[k][1];
+        }
+        wave_sum8(v8, t8);
+        float g3[2] = {0.f, 0.f};
+        if (NSH > 3) {
+            g3[0] = wave_sum(gshp[3][0]);
+            g3[1] = wave_sum(gshp[3][1]);
+        }
+        float gx = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NSH; ++k) {
+            const float tk = k < 3 ? ((j & 1) ? t8[3 + 2 * k] : t8[2 + 2 * k])
+                                   : ((j & 1) ? g3[1] : g3[0]);
+            if (xk == k) gx = tk;
+        }
+        sh.g = xon ? gx + sg_self : 0.0f;
+        return (t8[0] + slp[0]) + P.lp_const;
+    };
+    // the kinetic energy of (R.p, sh.p)
+    auto kinetic = [&]() {
+        float k = 0.0f;
+#pragma unroll
+        for (int r = 0; r < RS; ++r) k += R.p[r][0] * R.p[r][0];
+        if (xone) k += sh.p * sh.p;
+        return wave_sum(k);
+    };
+
+    MC_STAMP_INIT
+    mc_chain_scalars sc = scal[c];
+    float lp = sc.logp;
+    double eps = sc.step_size;
+    const uint32_t chain_id = (uint32_t)(cfg.chain_offset + c);
+    const int64_t it_end = cfg.iter_begin + cfg.iter_count;
+    int64_t n_grad = 0;
+
+    for (int64_t it = cfg.iter_begin; it < it_end; ++it) {
+        if (it == cfg.num_warmup) {  // nuts.py:318-319, 328-330
+            if (cfg.adapt_step_size) eps = sc.step_size_bar;
+            sc.warmup_accept = sc.n_accept;
+            sc.warmup_total = sc.n_total;
+            sc.warmup_depth_sum = sc.depth_sum;
+            sc.n_accept = 0;
+            sc.n_total = 0;
+            sc.depth_sum = 0;
+        }
+        const bool warm = it < cfg.num_warmup;
+        const double eps_used = eps;
+
+        // momentum, kinetic energy, H0 (nuts.py:223-231); parameter g takes
+        // normal g % 4 of Philox block g / 4 (k_nuts' mapping)
+        auto normal_of = [&](int gi) {
+            const mc_u32x4 rr = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_MOMENTUM, 0,
+                                        (uint32_t)(gi >> 2));
+            float z0, z1;
+            if ((gi & 3) < 2) mc_box_muller(rr.x, rr.y, &z0, &z1);
+            else mc_box_muller(rr.z, rr.w, &z0, &z1);
+            return (gi & 1) ? z1 : z0;
+        };
+        // both ends start at the current sample with the drawn momentum
+        LrPriv<RS> EM, EP;
+        float Mqs, Mrs, Mgs, Pqs, Prs, Pgs;
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            const float z = gk[r] >= 0 ? normal_of(gk[r]) : 0.0f;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                EM.q[r][h] = EP.q[r][h] = Cq[r][h];
+                EM.g[r][h] = EP.g[r][h] = Cg[r][h];
+                EM.p[r][h] = EP.p[r][h] = z;
+            }
+        }
+        {
+            const float z = xon ? normal_of(xg) : 0.0f;
+            Mqs = Pqs = Cqs;
+            Mgs = Pgs = Cgs;
+            Mrs = Prs = z;
+        }
+        float K0;
+        {
+            float k = 0.0f;
+#pragma unroll
+            for (int r = 0; r < RS; ++r) k += EM.p[r][0] * EM.p[r][0];
+            if (xone) k += Mrs * Mrs;
+            K0 = wave_sum(k);
+        }
+        const float H0 = -lp + 0.5f * K0;
+
+        // slice variable (nuts.py:234-237)
+        const mc_u32x4 rs = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_SLICE, 0, 0);
+        const double log_u = (double)(-H0) + (double)mc_logf_ref(mc_u01_f32(rs.x));
+        double logu;
+        if (cfg.slice_mode == 0) {
+            const float x = (float)log_u;
+            double ed = exp((double)x);
+            float uf;
+            if (ed < 1.1754943508222875e-38) {  // f32 gradual underflow, round-half-even
+                uf = (float)(rint(ed * 7.1362384635297994e+44) * 1.4012984643248171e-45);
+            } else {
+                uf = (float)ed;
+            }
+            logu = (uf == 0.0f) ? -__builtin_inf() : (double)mc_logf_ref(uf);
+        } else {
+            logu = log_u;
+        }
+
+        int n = 1;
+        bool s = true;
+        int jd = 0;
+        double alpha_sum = 0.0;
+        int n_alpha = 0;
+        int leaves = 0;
+        int divergent = 0;
+
+        // dot products of the U-turn test over every parameter
+        auto no_u_turn_lanes = [&](const float (&qm)[RS + 1], const float (&qp)[RS + 1],
+                                   const float (&rm)[RS + 1], const float (&rp)[RS + 1]) {
+            float a = 0.0f, b = 0.0f;
+#pragma unroll
+            for (int r = 0; r <= RS; ++r) {
+                if (r == RS && !xone) break;
+                const float d = qp[r] - qm[r];
+                a += d * rm[r];
+                b += d * rp[r];
+            }
+            const float dm = wave_sum(a);
+            const float dp = wave_sum(b);
+            return dm >= 0.0f && dp >= 0.0f;
+        };
+
+        while (s && jd < MAXJ) {
+            const mc_u32x4 rd = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_DEPTH,
+                                        (uint32_t)jd, 0);
+            const int v = (mc_u01_f32(rd.x) < 0.5f) ? 1 : -1;
+            const double ve = (double)v * eps;
+            const float h = (float)(0.5 * ve);
+            const float e = (float)ve;
+            // the end this subtree extends: into the working registers
+            if (v > 0) {
+                R = EP;
+                sh.q = Pqs;
+                sh.p = Prs;
+                sh.g = Pgs;
+            } else {
+                R = EM;
+                sh.q = Mqs;
+                sh.p = Mrs;
+                sh.g = Mgs;
+            }
+
+            // ---- build_tree(jd) iteratively ---------------------------------
+            uint32_t freemask = (1u << (MAXJ + 2)) - 1u;
+            bool s_sub = true;
+            int cand = -1, cn = 0;
+            float pool_lp = 0.0f;  // lane f: log p of pool slot f
+            int pend_idx = 0, pend_n = 0;  // lane l: the parked first half of level l
+            const int nleaf = 1 << jd;
+            for (int k = 0; k < nleaf; ++k) {
+                // leaf: leapfrog_step(theta, r, v*eps) + hamiltonian (nuts.py:160-164)
+#pragma unroll
+                for (int r = 0; r < RS; ++r)
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                        const float pj = R.p[r][hh] + h * R.g[r][hh];
+                        R.p[r][hh] = pj;
+                        R.q[r][hh] = R.q[r][hh] + e * pj;
+                    }
+                {
+                    const float pj = sh.p + h * sh.g;
+                    sh.p = pj;
+                    sh.q = sh.q + e * pj;
+                }
+                if (Dsh > 0) derive();
+                const float lpl = evaluate();
+#pragma unroll
+                for (int r = 0; r < RS; ++r)
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) R.p[r][hh] = R.p[r][hh] + h * R.g[r][hh];
+                sh.p = sh.p + h * sh.g;
+                const float Hl = -lpl + 0.5f * kinetic();
+                ++leaves;
+                const int n_leaf = (logu <= (double)(-Hl)) ? 1 : 0;
+                const bool s_leaf = logu < (double)(1000.0f - Hl);
+                const double a = (double)mc_expf_ref(-Hl + H0);
+                alpha_sum += (a < 1.0) ? a : 1.0;
+                n_alpha += 1;
+                if (!s_leaf) divergent += 1;
+
+                // park the leaf as a candidate and, if it opens a subtree of
+                // level >= 1, as that subtree's first leaf
+                const int f = __builtin_ctz(freemask);
+                freemask &= ~(1u << f);
+#pragma unroll
+                for (int r = 0; r < RS; ++r) {
+                    *at(1, f, 0, r) = R.q[r][0];
+                    *at(1, f, 1, r) = R.g[r][0];
+                }
+                *at(1, f, 0, RS) = sh.q;
+                *at(1, f, 1, RS) = sh.g;
+                pool_lp = (j == f) ? lpl : pool_lp;
+                const bool opens = (jd >= 1) && ((k & 1) == 0);
+                if (opens) {
+                    const int fslot = (k == 0) ? jd : ctz_u32((uint32_t)k);
+#pragma unroll
+                    for (int r = 0; r < RS; ++r) {
+                        *at(0, fslot, 0, r) = R.q[r][0];
+                        *at(0, fslot, 1, r) = R.p[r][0];
+                    }
+                    *at(0, fslot, 0, RS) = sh.q;
+                    *at(0, fslot, 1, RS) = sh.p;
+                }
+                if (!s_leaf) {
+                    s_sub = false;
+                    break;
+                }
+                cand = f;
+                cn = n_leaf;
+
+                // merge completed subtrees upward
+                bool parked = false;
+                for (int l = 0; l < jd; ++l) {
+                    if (((k + 1) >> l) & 1) {
+                        pend_idx = (j == l) ? cand : pend_idx;
+                        pend_n = (j == l) ? cn : pend_n;
+                        parked = true;
+                        break;
+                    }
+                    const int pidx = __builtin_amdgcn_readlane(pend_idx, l);
+                    const int pn = __builtin_amdgcn_readlane(pend_n, l);
+                    const mc_u32x4 rm = mc_draw(cfg.seed, chain_id, (uint32_t)it,
+                                                MC_RNG_TAG_MERGE, (uint32_t)jd,
+                                                ((uint32_t)l << 20) | (uint32_t)k);
+                    const double den = (double)(pn + cn) > 1.0 ? (double)(pn + cn) : 1.0;
+                    const bool take_second = (double)mc_u01_f32(rm.x) < (double)cn / den;
+                    if (take_second) {
+                        freemask |= (1u << pidx);
+                    } else {
+                        freemask |= (1u << cand);
+                        cand = pidx;
+                    }
+                    cn = pn + cn;
+                    // U-turn over the merged level-(l+1) subtree
+                    const int k0 = k + 1 - (2 << l);
+                    const int slot = (k0 == 0) ? jd : ctz_u32((uint32_t)k0);
+                    float bq[RS + 1], br[RS + 1], eq[RS + 1], er[RS + 1];
+#pragma unroll
+                    for (int r = 0; r <= RS; ++r) {
+                        bq[r] = *at(0, slot, 0, r);
+                        br[r] = *at(0, slot, 1, r);
+                        eq[r] = r < RS ? R.q[r][0] : sh.q;
+                        er[r] = r < RS ? R.p[r][0] : sh.p;
+                    }
+                    const bool ok = (v > 0) ? no_u_turn_lanes(bq, eq, br, er)
+                                            : no_u_turn_lanes(eq, bq, er, br);
+                    if (!ok) {
+                        s_sub = false;
+                        break;
+                    }
+                }
+                if (!s_sub) break;
+                if (parked) continue;
+                // l reached jd: the depth-jd subtree is complete
+            }
+            // the working registers back into the end they extended
+            if (v > 0) {
+                EP = R;
+                Pqs = sh.q;
+                Prs = sh.p;
+                Pgs = sh.g;
+            } else {
+                EM = R;
+                Mqs = sh.q;
+                Mrs = sh.p;
+                Mgs = sh.g;
+            }
+
+            // ---- top level (nuts.py:262-284) --------------------------------
+            if (s_sub) {
+                const double den = (double)n > 1.0 ? (double)n : 1.0;
+                double pacc = (double)cn / den;
+                pacc = (pacc < 1.0) ? pacc : 1.0;
+                if ((double)mc_u01_f32(rd.y) < pacc) {
+#pragma unroll
+                    for (int r = 0; r < RS; ++r) {
+                        const float q = *at(1, cand, 0, r), g = *at(1, cand, 1, r);
+                        Cq[r] = (f2){q, q};
+                        Cg[r] = (f2){g, g};
+                    }
+                    Cqs = *at(1, cand, 0, RS);
+                    Cgs = *at(1, cand, 1, RS);
+                    lp = rl(pool_lp, cand);
+                }
+            }
+            n += cn;
+            if (s_sub) {
+                float mq[RS + 1], pq[RS + 1], mr[RS + 1], pr[RS + 1];
+#pragma unroll
+                for (int r = 0; r < RS; ++r) {
+                    mq[r] = EM.q[r][0];
+                    pq[r] = EP.q[r][0];
+                    mr[r] = EM.p[r][0];
+                    pr[r] = EP.p[r][0];
+                }
+                mq[RS] = Mqs;
+                pq[RS] = Pqs;
+                mr[RS] = Mrs;
+                pr[RS] = Prs;
+                s = no_u_turn_lanes(mq, pq, mr, pr);
+            } else {
+                s = false;
+            }
+            jd += 1;
+        }
+
+        const double alpha = alpha_sum / (n_alpha > 1 ? (double)n_alpha : 1.0);
+        n_grad += leaves;
+        sc.n_divergent += divergent;
+        sc.alpha_sum += alpha;
+        sc.n_accept += (alpha > 0.5) ? 1 : 0;
+        sc.n_total += 1;
+        sc.depth_sum += jd;
+        if (warm && cfg.adapt_step_size) {  // dual averaging, nuts.py:299-310
+            const double m = (double)it;
+            const double eta = 1.0 / (m + 10.0);
+            sc.h_bar = (1.0 - eta) * sc.h_bar + eta * (cfg.target_accept - alpha);
+            const float lf = sc.mu - (float)(sqrt(m + 1.0) / 0.05 * sc.h_bar);
+            double le = (double)lf;
+            if (10.0 < le) le = 10.0;
+            if (-10.0 > le) le = -10.0;
+            eps = (double)mc_expf_ref((float)le);
+            const double m_eta = pow(m + 1.0, -0.75);
+            const double lb = m_eta * log(eps) + (1.0 - m_eta) * log(sc.step_size_bar);
+            sc.step_size_bar = (double)mc_expf_ref((float)lb);
+        }
+        if (!warm && samples != nullptr) {
+            const int64_t si = it - cfg.num_warmup - cfg.sample_begin;
+            if (si >= 0 && si < cfg.sample_capacity) {
+                float* out = samples + (c * cfg.sample_capacity + si) * (int64_t)D;
+#pragma unroll
+                for (int r = 0; r < RS; ++r)
+                    if (gk[r] >= 0) out[gk[r]] = Cq[r][0];
+                if (xone) out[xg] = Cqs;
+            }
+        }
+        if (j == 0) {
+            const int64_t ti = it - tr.iter_begin;
+            if (ti >= 0 && ti < tr.capacity) {
+                const int64_t o = c * tr.capacity + ti;
+                if (tr.accepted) tr.accepted[o] = (alpha > 0.5) ? 1 : 0;
+                if (tr.accept_stat) tr.accept_stat[o] = (float)alpha;
+                if (tr.step_size) tr.step_size[o] = eps_used;
+                if (tr.energy) tr.energy[o] = H0;
+                if (tr.tree_depth) tr.tree_depth[o] = jd;
+                if (tr.n_leapfrog) tr.n_leapfrog[o] = leaves;
+            }
+        }
+    }
+    MC_STAMP_FLUSH
+
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+        if (gk[r] >= 0) {
+            st_q[c * D + gk[r]] = Cq[r][0];
+            st_g[c * D + gk[r]] = Cg[r][0];
+        }
+    }
+    if (xone) {
+        st_q[c * D + xg] = Cqs;
+        st_g[c * D + xg] = Cgs;
+    }
+    if (j == 0) {
+        sc.logp = lp;
+        sc.step_size = eps;
+        sc.n_grad += n_grad;
+        scal[c] = sc;
+    }
+}
+
+}  // namespace mc

@@ -172,6 +172,8 @@ def run_sampler(algorithm: str, log_prob_fn, initial_params, *, num_samples: int
         n_divergent=(s["n_divergent"].copy() if algorithm == "nuts" else None),
         trace=trace.numpy() if trace is not None else None,
         device_samples=flat if keep_on_device else None, layout=layout)
+    info.extra["kernel"] = (program.nuts_kernel(max_tree_depth) if algorithm == "nuts"
+                            else program.slice_kernel)
     host = flat.cpu().numpy()
     per_name = layout.unflatten(host)  # name -> [C, S, *shape]
     if C == 1:

@@ -5,6 +5,11 @@ reference's ``nuts()`` (slice NUTS, Hoffman & Gelman 2014 Alg. 3, dual
 averaging).  Tree building runs iteratively inside the persistent HIP kernel
 ``k_nuts`` (csrc/nuts.h), one chain per chain group.
 
+``nuts_kernel``: "auto" runs the lane-resident kernel ``k_nuts_lr``
+(csrc/nuts_lanes.h: chain state in registers, tree arena in LDS) when the
+model plans as one lane-resident slice, else ``k_nuts``; "tape" keeps
+``k_nuts``.
+
 ``slice_mode="reference"`` (default) reproduces the reference's float32
 slice variable, which switches the slice test off once log u < ~-103.97
 (nuts.py:236-237); ``"exact"`` keeps log u in double precision.
@@ -21,7 +26,7 @@ def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_si
          max_tree_depth=10, adapt_step_size=True, target_accept=0.65, key=None, *,
          num_chains=1, chain_offset=0, slice_mode="reference", progress=True,
          return_info=False, return_trace=False, keep_on_device=False,
-         initial_positions=None):
+         initial_positions=None, nuts_kernel="auto"):
     """No-U-Turn Sampler (NUTS) for efficient HMC sampling.
 
     Returns ``(samples, acceptance_rate)`` like the reference, where the rate
@@ -34,7 +39,8 @@ def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_si
         key=key, max_tree_depth=max_tree_depth, num_chains=num_chains,
         chain_offset=chain_offset, slice_mode=slice_mode, progress=progress,
         return_trace=return_trace, keep_on_device=keep_on_device,
-        initial_positions=initial_positions)
+        initial_positions=initial_positions,
+        num_slices={"auto": 0, "tape": 1}[nuts_kernel])
     if return_info:
         return samples, rate, info
     return samples, rate

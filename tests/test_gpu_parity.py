@@ -135,16 +135,19 @@ def test_hmc_trace_parity_simple(gpu):
                                np.array(ref.trace["ratio"][:upto]), rtol=1e-3, atol=2e-3)
 
 
-def test_nuts_trace_parity_illcond(gpu):
+@pytest.mark.parametrize("kernel", ["auto", "tape"])
+def test_nuts_trace_parity_illcond(gpu, kernel):
     """Config 5 (kappa = 1000, slice active): identical tree depths and leaf
-    counts until the first near-tie."""
+    counts until the first near-tie — on the lane-resident NUTS kernel
+    (k_nuts_lr, the automatic choice for this model) and on k_nuts."""
     import mlx_mcmc_amd as m
 
     plp, pinit = W.illcond_normal(W.ns_product())
     olp, oinit = W.illcond_normal(W.ns_oracle())
     n_w, n_s = 30, 10
     _, _, info = m.nuts(plp, pinit, num_samples=n_s, num_warmup=n_w, key=m.random.key(11),
-                        progress=False, return_info=True, return_trace=True)
+                        progress=False, return_info=True, return_trace=True, nuts_kernel=kernel)
+    assert info.extra["kernel"] == ("lanes" if kernel == "auto" else "tape")
     ref = S.nuts(olp, oinit, num_samples=n_s, num_warmup=n_w, seed=11)
     depth = info.trace["tree_depth"][0]
     leaves = info.trace["n_leapfrog"][0]
@@ -160,3 +163,101 @@ def test_nuts_trace_parity_illcond(gpu):
                                np.array(ref.trace["alpha"][:8]), rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(info.trace["step_size"][0][:8],
                                np.array(ref.trace["step_size"][:8]), rtol=3e-4)  # x sqrt(m+1)/gamma gain
+
+
+def test_nuts_lanes_matches_tape_hierarchical(gpu):
+    """k_nuts_lr against k_nuts on a model with broadcast (mu, tau, sigma) and
+    private (theta) parameters: the same draws give the same trees until the
+    first fp32 near-tie (the kernels differ in summation order only), and
+    the same posterior."""
+    import mlx_mcmc_amd as m
+
+    lp, init = W.hierarchical(W.ns_product(), *W.SHAPES["small"])
+    runs = {}
+    for kernel in ("auto", "tape"):
+        s, _, info = m.nuts(lp, init, num_samples=300, num_warmup=200, key=m.random.key(5),
+                            num_chains=8, progress=False, return_info=True, return_trace=True,
+                            nuts_kernel=kernel)
+        runs[kernel] = (s, info)
+    assert runs["auto"][1].extra["kernel"] == "lanes"
+    assert runs["tape"][1].extra["kernel"] == "tape"
+    da, db = runs["auto"][1].trace["tree_depth"], runs["tape"][1].trace["tree_depth"]
+    la, lb = runs["auto"][1].trace["n_leapfrog"], runs["tape"][1].trace["n_leapfrog"]
+    same = []
+    for c in range(8):
+        k = 0
+        while k < da.shape[1] and da[c, k] == db[c, k] and la[c, k] == lb[c, k]:
+            k += 1
+        same.append(k)
+    assert sorted(same)[2] >= 10, f"trees diverged early: {same}"
+    for name in ("mu", "tau", "sigma"):
+        a, b = runs["auto"][0][name], runs["tape"][0][name]
+        sa = a.std() / np.sqrt(a.size / 20)   # generous MCSE (autocorrelated draws)
+        assert abs(a.mean() - b.mean()) < 5 * sa + 1e-3, (name, a.mean(), b.mean())
+
+
+@pytest.mark.parametrize("model", ["illcond", "eight_schools"])
+def test_dscale_lanes_hmc_matches_tape(gpu, model):
+    """Normal terms with a per-element data scale on the lane-resident kernels
+    (lanes.h LS_DSCALE: tiles of 1/s^2 and log s) against k_hmc (the tape,
+    num_slices=1): same draws, the same accept decisions until the first fp32
+    near-tie, positions within rtol 1e-3 before it."""
+    import mlx_mcmc_amd as m
+
+    lp, init = (W.illcond_normal(W.ns_product()) if model == "illcond"
+                else W.eight_schools(W.ns_product()))
+    step = 0.02 if model == "illcond" else 0.2
+    out = {}
+    for slices in (0, 1):
+        s, _, info = m.hmc(lp, init, num_samples=60, num_warmup=60, step_size=step,
+                           num_leapfrog_steps=10, key=m.random.key(2), num_chains=8,
+                           progress=False, return_info=True, return_trace=True,
+                           num_slices=slices)
+        out[slices] = (s, info)
+    assert out[0][1].extra["kernel"] == "lanes" and out[1][1].extra["kernel"] == "unsliced"
+    a, b = out[0][1].trace["accepted"], out[1][1].trace["accepted"]
+    assert 0 < a.mean() < 1
+    firsts = []
+    for c in range(8):
+        d = np.nonzero(a[c] != b[c])[0]
+        firsts.append(int(d[0]) if d.size else a.shape[1])
+    assert sorted(firsts)[2] >= 30, firsts
+    # positions: a fresh run's first draws (one warmup iteration, fixed eps),
+    # before any divergence
+    # (fp32 differences grow along the trajectories iteration by iteration:
+    # after 60 iterations of the eight-schools funnel they reach ~1e-2)
+    name = "x" if model == "illcond" else "theta"
+    pos = {}
+    for slices in (0, 1):
+        s, _, info = m.hmc(lp, init, num_samples=8, num_warmup=1, step_size=step,
+                           num_leapfrog_steps=10, key=m.random.key(9), num_chains=8,
+                           progress=False, return_info=True, return_trace=True,
+                           num_slices=slices, adapt_step_size=False)
+        pos[slices] = (s[name], info.trace["accepted"])
+    for c in range(8):
+        d = np.nonzero(pos[0][1][c] != pos[1][1][c])[0]  # (trace: 1 warmup + 8)
+        k = max(0, int(d[0]) - 1) if d.size else 8
+        np.testing.assert_allclose(pos[0][0][c, :k], pos[1][0][c, :k], rtol=1e-3, atol=1e-3)
+
+
+def test_nuts_lanes_eight_schools(gpu):
+    """k_nuts_lr on the data-scale model against k_nuts: same trees until the
+    first near-tie for most chains."""
+    import mlx_mcmc_amd as m
+
+    lp, init = W.eight_schools(W.ns_product())
+    tr = {}
+    for kernel in ("auto", "tape"):
+        _, _, info = m.nuts(lp, init, num_samples=50, num_warmup=50, key=m.random.key(4),
+                            num_chains=8, progress=False, return_info=True, return_trace=True,
+                            nuts_kernel=kernel)
+        tr[kernel] = info
+    assert tr["auto"].extra["kernel"] == "lanes"
+    same = []
+    for c in range(8):
+        k = 0
+        while (k < 100 and tr["auto"].trace["tree_depth"][c, k] == tr["tape"].trace["tree_depth"][c, k]
+               and tr["auto"].trace["n_leapfrog"][c, k] == tr["tape"].trace["n_leapfrog"][c, k]):
+            k += 1
+        same.append(k)
+    assert sorted(same)[2] >= 10, same

@@ -151,3 +151,23 @@ def event_rates(ns):
         return lp + ll
 
     return log_prob, {"rate": 2.0}
+
+
+# ---- per-element data scales (known measurement error): eight schools ---------
+EIGHT_SCHOOLS_Y = np.array([28.0, 8.0, -3.0, 7.0, -1.0, 1.0, 18.0, 12.0], np.float32)
+EIGHT_SCHOOLS_SIGMA = np.array([15.0, 10.0, 16.0, 11.0, 9.0, 11.0, 10.0, 18.0], np.float32)
+
+
+def eight_schools(ns):
+    """Centred eight schools: y_j ~ N(theta_j, sigma_j) with known sigma_j,
+    theta ~ N(mu, tau): a likelihood whose scale is a per-element data vector."""
+    y, sig = EIGHT_SCHOOLS_Y, EIGHT_SCHOOLS_SIGMA
+
+    def log_prob(params):
+        mu, tau, theta = params["mu"], params["tau"], params["theta"]
+        lp = ns.Normal(0, 5).log_prob(mu) + ns.HalfNormal(5).log_prob(tau)
+        lp = lp + ns.sum(ns.Normal(mu, tau).log_prob(theta))
+        return lp + ns.sum(ns.Normal(theta, sig).log_prob(ns.array(y)))
+
+    return log_prob, {"mu": np.float32(4.0), "tau": np.float32(3.0),
+                      "theta": np.full(8, 4.0, np.float32)}
