@@ -98,12 +98,26 @@ typedef struct mc_operand {
 
 typedef struct mc_term {
     int32_t    dist;       /* mc_dist_kind                                  */
-    int32_t    reserved0;
+    int32_t    affine;     /* 0, or k + 1: the loc is affine, affines[k]    */
     int64_t    n;          /* broadcast length (>= 1)                       */
     float      weight;     /* multiplies the term (1.0 for `lp += term`)    */
     float      reserved1;
     mc_operand value, loc, scale;
 } mc_term;
+
+/* An affine loc (the reference differentiates any MLX expression of the
+ * parameters, hmc.py:53-67; these are the linear-predictor forms):
+ *     loc_i = loc_i + slope_i * x_i      (f32: one product, then one sum)
+ * for a Normal term whose `affine` field is k + 1 (affines[k]).  slope is
+ * CONST or PSCALAR; x is DATA, PVEC or a GATHER; the term's own loc operand is
+ * CONST, PSCALAR, DATA, PVEC or a GATHER.  Gathers of an affine term must be
+ * injective, and x's parameter range must not overlap another accumulating
+ * operand of the term (MC_ERR_UNSUPPORTED otherwise).  Examples: a + b * x
+ * (linear regression), mu + tau * z (non-centred hierarchy).  Affine
+ * programs run on the chain-per-workgroup kernels (k_hmc, k_nuts, k_mh).   */
+typedef struct mc_affine {
+    mc_operand slope, x;
+} mc_affine;
 
 typedef struct mc_program mc_program;
 
@@ -117,6 +131,13 @@ int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t n_params,
                       const float* data, int64_t n_data,
                       const int32_t* index, int64_t n_index,
                       mc_program** out);
+/* mc_program_create with affine loc operands (affines[0 .. n_affines)).    */
+int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
+                             const mc_affine* affines, int32_t n_affines,
+                             int32_t n_params, float lp_const,
+                             const float* data, int64_t n_data,
+                             const int32_t* index, int64_t n_index,
+                             mc_program** out);
 int mc_program_destroy(mc_program* prog);
 int32_t mc_program_num_params(const mc_program* prog);
 /* The launch geometry the engine picked: waves per chain (1, 4 or 16).     */

@@ -72,13 +72,21 @@ class McOperand(ctypes.Structure):
 class McTerm(ctypes.Structure):
     _fields_ = [
         ("dist", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("affine", ctypes.c_int32),
         ("n", ctypes.c_int64),
         ("weight", ctypes.c_float),
         ("reserved1", ctypes.c_float),
         ("value", McOperand),
         ("loc", McOperand),
         ("scale", McOperand),
+    ]
+
+
+class McAffine(ctypes.Structure):
+    """mc_affine: loc_i = loc_i + slope_i * x_i for a term with affine = k + 1."""
+    _fields_ = [
+        ("slope", McOperand),
+        ("x", McOperand),
     ]
 
 
@@ -141,6 +149,10 @@ SIGNATURES = [
     ("mc_program_create", ctypes.c_int,
      [ctypes.POINTER(McTerm), ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
       _VP, ctypes.c_int64, _VP, ctypes.c_int64, ctypes.POINTER(_VP)]),
+    ("mc_program_create_affine", ctypes.c_int,
+     [ctypes.POINTER(McTerm), ctypes.c_int32, ctypes.POINTER(McAffine), ctypes.c_int32,
+      ctypes.c_int32, ctypes.c_float, _VP, ctypes.c_int64, _VP, ctypes.c_int64,
+      ctypes.POINTER(_VP)]),
     ("mc_program_destroy", ctypes.c_int, [_VP]),
     ("mc_program_num_params", ctypes.c_int32, [_VP]),
     ("mc_program_waves_per_chain", ctypes.c_int32, [_VP]),

@@ -18,6 +18,16 @@ Operands a term accepts (anything else raises ``TraceError``):
 Per-observation Python loops (examples/01_simple_normal.py:46-48,
 tests/test_nuts.py:194-196) trace to many scalar terms with identical
 distribution arguments; they are folded into one vector term.
+
+Arithmetic on parameters builds an *affine* location ``a + b * x`` (one
+product and one sum, as the reference's MLX ops round them): ``b`` a
+constant or scalar parameter, ``x`` a data array, a parameter vector / slice
+or an injective gather, ``a`` a constant, scalar parameter, data array,
+parameter vector or injective gather — linear regression ``Normal(a + b * x,
+sigma)``, non-centred hierarchies ``Normal(mu + tau * z, sigma_j)``.  It is
+accepted as a Normal ``loc`` only (mc_affine in include/mcmc355.h); anything
+else (two products, ``mx.log(sigma)``, a product of two parameters used as a
+scale ...) raises ``TraceError``.
 """
 from __future__ import annotations
 
@@ -116,8 +126,29 @@ class Param:
     def _unsupported(self, *a, **k):
         raise TraceError(f"arithmetic on traced parameter '{self.name}': " + _UNSUPPORTED)
 
-    __add__ = __radd__ = __sub__ = __rsub__ = __mul__ = __rmul__ = _unsupported
-    __truediv__ = __rtruediv__ = __pow__ = __neg__ = __abs__ = _unsupported
+    # affine arithmetic (a + b * x): see Affine
+    def __mul__(self, other):
+        return Affine.product(self, other)
+
+    __rmul__ = __mul__
+
+    def __add__(self, other):
+        return Affine.lift(self) + other
+
+    def __radd__(self, other):
+        return Affine.lift(self) + other
+
+    def __sub__(self, other):
+        return Affine.lift(self) + (-1.0) * other if not isinstance(other, Affine) else \
+            Affine.lift(self) + other * -1.0
+
+    def __rsub__(self, other):
+        return Affine.product(-1.0, self) + other
+
+    def __neg__(self):
+        return Affine.product(-1.0, self)
+
+    __truediv__ = __rtruediv__ = __pow__ = __abs__ = _unsupported
     __lt__ = __le__ = __gt__ = __ge__ = _unsupported
 
     def __float__(self):
@@ -128,6 +159,116 @@ class Param:
 
     def __repr__(self):
         return f"Param({self.name}, view={self.view})"
+
+
+def _is_slope(x) -> bool:
+    """A constant or a scalar parameter (an affine slope)."""
+    if isinstance(x, Param):
+        return x.shape == ()
+    if isinstance(x, (Affine, LogProbExpr)):
+        return False
+    try:
+        return np.asarray(_to_numpy(x)).size == 1 and np.asarray(_to_numpy(x)).ndim == 0
+    except Exception:
+        return False
+
+
+def _is_term_operand(x) -> bool:
+    """Something to_operand accepts (a parameter or view, data, a constant)."""
+    return not isinstance(x, (Affine, LogProbExpr))
+
+
+class Affine:
+    """A traced affine location ``loc + slope * x`` (mc_affine): one product
+    and one sum per element, rounded in f32 as the reference's MLX ops."""
+
+    __array_priority__ = 1000
+
+    def __init__(self, loc, slope, x):
+        self.loc = loc      # None (0), a constant, data, or a parameter (view)
+        self.slope = slope  # None (no product), a constant or a scalar parameter
+        self.x = x          # None, data, or a parameter vector / view
+
+    @staticmethod
+    def lift(v) -> "Affine":
+        return v if isinstance(v, Affine) else Affine(v, None, None)
+
+    @staticmethod
+    def product(a, b) -> "Affine":
+        if isinstance(a, Affine) or isinstance(b, Affine):
+            raise TraceError("a product of an affine expression: only loc + slope * x traces; "
+                             + _UNSUPPORTED)
+        if _is_slope(a) and not (_is_slope(b) and not isinstance(b, Param)):
+            slope, x = a, b
+        elif _is_slope(b):
+            slope, x = b, a
+        else:
+            raise TraceError("a product of two vectors: only loc + slope * x (slope a constant "
+                             "or scalar parameter) traces; " + _UNSUPPORTED)
+        if isinstance(x, Param) and x.shape == ():
+            raise TraceError("a product of two scalar parameters: " + _UNSUPPORTED)
+        if not isinstance(x, Param) and not isinstance(slope, Param):
+            raise TraceError("a constant product outside a parameter expression")
+        return Affine(None, slope, x)
+
+    def __add__(self, other):
+        if isinstance(other, LogProbExpr):
+            raise TraceError("adding a parameter expression to a log density: " + _UNSUPPORTED)
+        o = Affine.lift(other)
+        if self.x is not None and o.x is not None:
+            raise TraceError("a sum of two products (a + b*x + c*z): only loc + slope * x "
+                             "traces; " + _UNSUPPORTED)
+        if self.loc is not None and o.loc is not None:
+            if isinstance(self.loc, Param) or isinstance(o.loc, Param):
+                # a + z with both symbolic: z as x with slope 1
+                if self.x is None and o.x is None:
+                    a, b = self.loc, o.loc
+                    if _is_slope(b) and not _is_slope(a):  # the vector is x (slope 1)
+                        a, b = b, a
+                    if _is_slope(b):
+                        raise TraceError("a sum of two scalar parameters as a loc: "
+                                         + _UNSUPPORTED)
+                    return Affine(a, 1.0, b)  # (a + 1 * b rounds as a + b)
+                raise TraceError("a sum of two parameter terms besides the product: "
+                                 + _UNSUPPORTED)
+            loc = np.float32(np.asarray(self.loc, np.float32) + np.asarray(o.loc, np.float32))
+        else:
+            loc = self.loc if self.loc is not None else o.loc
+        prod = self if self.x is not None else o
+        return Affine(loc, prod.slope, prod.x)
+
+    __radd__ = __add__
+
+    def __sub__(self, other):
+        if isinstance(other, Param):
+            return self + Affine.product(-1.0, other)
+        if isinstance(other, Affine):
+            raise TraceError("subtracting an affine expression: " + _UNSUPPORTED)
+        return self + (-np.asarray(_to_numpy(other), np.float32))
+
+    def __rsub__(self, other):
+        raise TraceError("subtracting an affine expression: " + _UNSUPPORTED)
+
+    def _unsupported(self, *a, **k):
+        raise TraceError("this operation on a traced parameter expression: " + _UNSUPPORTED)
+
+    __mul__ = __rmul__ = __truediv__ = __rtruediv__ = __pow__ = __neg__ = __abs__ = _unsupported
+    __getitem__ = __lt__ = __le__ = __gt__ = __ge__ = _unsupported
+
+    def __float__(self):
+        raise TraceError("float() of a traced parameter expression: " + _UNSUPPORTED)
+
+    __bool__ = __int__ = __float__
+
+    def operands(self):
+        """(loc, slope, x) operands for mc_term / mc_affine."""
+        loc = to_operand(self.loc if self.loc is not None else 0.0)
+        if self.x is None:
+            return loc, None, None
+        return loc, to_operand(self.slope), to_operand(self.x)
+
+    def __repr__(self):
+        return f"Affine({self.loc!r} + {self.slope!r} * {self.x!r})"
 
 
 @dataclass
@@ -171,6 +312,9 @@ def to_operand(x) -> Operand:
         return Operand(_lib.MC_OP_GATHER, param_offset=x.offset, index=v[1], shape=tuple(v[2]))
     if isinstance(x, LogProbExpr):
         raise TraceError("a log density cannot be a distribution argument: " + _UNSUPPORTED)
+    if isinstance(x, Affine):
+        raise TraceError("a parameter expression (loc + slope * x) is accepted as a Normal "
+                         "loc only: " + _UNSUPPORTED)
     try:
         import torch
 
@@ -188,7 +332,7 @@ def to_operand(x) -> Operand:
 
 
 def is_symbolic(*xs) -> bool:
-    return any(isinstance(x, (Param, LogProbExpr)) for x in xs)
+    return any(isinstance(x, (Param, LogProbExpr, Affine)) for x in xs)
 
 
 @dataclass
@@ -199,6 +343,7 @@ class Term:
     scale: Operand
     n: int
     weight: float = 1.0
+    aff: Optional[Tuple[Operand, Operand]] = None  # affine loc: (slope, x)
 
 
 def broadcast_n(dist_name: str, ops: List[Operand]) -> Tuple[int, Tuple[int, ...]]:
@@ -276,7 +421,7 @@ class LogProbExpr:
 
 
 def _scaled(t: Term, c: float) -> Term:
-    return Term(t.dist, t.value, t.loc, t.scale, t.n, t.weight * c)
+    return Term(t.dist, t.value, t.loc, t.scale, t.n, t.weight * c, t.aff)
 
 
 def _scalar_const(x) -> float:
@@ -289,13 +434,24 @@ def _scalar_const(x) -> float:
 
 
 def make_term(dist: int, dist_name: str, value, loc, scale) -> LogProbExpr:
-    ops = [to_operand(value), NONE_OPERAND if loc is None else to_operand(loc),
-           to_operand(scale)]
-    n, shape = broadcast_n(dist_name, ops)
-    for o in ops:
+    aff = None
+    if isinstance(loc, Param) and dist_name == "Normal":
+        loc_op = to_operand(loc)
+    elif isinstance(loc, Affine):
+        if dist_name != "Normal":
+            raise TraceError(f"{dist_name}: a parameter expression as a shape operand: "
+                             + _UNSUPPORTED)
+        loc_op, slope_op, x_op = loc.operands()
+        if x_op is not None:
+            aff = (slope_op, x_op)
+    else:
+        loc_op = NONE_OPERAND if loc is None else to_operand(loc)
+    ops = [to_operand(value), loc_op, to_operand(scale)]
+    n, shape = broadcast_n(dist_name, ops + ([aff[1]] if aff else []))
+    for o in ops + (list(aff) if aff else []):
         if o.kind in (_lib.MC_OP_DATA, _lib.MC_OP_GATHER) and o.shape == ():
             o.shape = (1,)
-    return LogProbExpr([Term(dist, ops[0], ops[1], ops[2], n)], 0.0, shape)
+    return LogProbExpr([Term(dist, ops[0], ops[1], ops[2], n, 1.0, aff)], 0.0, shape)
 
 
 def stack(items) -> LogProbExpr:
@@ -326,7 +482,7 @@ def fold_terms(terms: List[Term]) -> List[Term]:
     out: List[Term] = []
     groups: Dict[tuple, int] = {}
     for t in terms:
-        foldable = (t.value.kind in (_lib.MC_OP_CONST, _lib.MC_OP_DATA)
+        foldable = (t.aff is None and t.value.kind in (_lib.MC_OP_CONST, _lib.MC_OP_DATA)
                     and t.loc.kind in (_lib.MC_OP_CONST, _lib.MC_OP_PSCALAR, _lib.MC_OP_NONE)
                     and t.scale.kind in (_lib.MC_OP_CONST, _lib.MC_OP_PSCALAR))
         if not foldable:
@@ -409,6 +565,8 @@ class TracedModel:
     data: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))
     index: np.ndarray = field(default_factory=lambda: np.zeros(0, np.int32))
     c_terms: object = None
+    c_affines: object = None
+    n_affines: int = 0
 
 
 def trace(log_prob_fn, initial_params: dict) -> TracedModel:
@@ -436,13 +594,21 @@ def _build_pools(model: TracedModel) -> None:
     nd = 0
     ni = 0
     arr = (_lib.McTerm * max(1, len(model.terms)))()
+    affs = [t for t in model.terms if t.aff is not None]
+    aarr = (_lib.McAffine * max(1, len(affs)))()
+    na = 0
     for k, t in enumerate(model.terms):
         ct = arr[k]
         ct.dist = t.dist
         ct.n = t.n
         ct.weight = t.weight
-        for slot, o in (("value", t.value), ("loc", t.loc), ("scale", t.scale)):
-            co = getattr(ct, slot)
+        slots = [(ct, "value", t.value), (ct, "loc", t.loc), (ct, "scale", t.scale)]
+        if t.aff is not None:
+            ct.affine = na + 1
+            slots += [(aarr[na], "slope", t.aff[0]), (aarr[na], "x", t.aff[1])]
+            na += 1
+        for owner, slot, o in slots:
+            co = getattr(owner, slot)
             co.kind = o.kind
             co.param_offset = o.param_offset
             co.value = o.value
@@ -457,6 +623,8 @@ def _build_pools(model: TracedModel) -> None:
     model.data = (np.concatenate(data_parts) if data_parts else np.zeros(0, np.float32))
     model.index = (np.concatenate(index_parts) if index_parts else np.zeros(0, np.int32))
     model.c_terms = arr
+    model.c_affines = aarr
+    model.n_affines = na
 
 
 class Program:
@@ -470,9 +638,9 @@ class Program:
         h = ctypes.c_void_p()
         data = np.ascontiguousarray(model.data, np.float32)
         index = np.ascontiguousarray(model.index, np.int32)
-        _lib.check(lib.mc_program_create(
-            model.c_terms, len(model.terms), self.D, model.lp_const,
-            data.ctypes.data_as(ctypes.c_void_p), data.size,
+        _lib.check(lib.mc_program_create_affine(
+            model.c_terms, len(model.terms), model.c_affines, model.n_affines, self.D,
+            model.lp_const, data.ctypes.data_as(ctypes.c_void_p), data.size,
             index.ctypes.data_as(ctypes.c_void_p), index.size, ctypes.byref(h)))
         self.handle = h
         self.waves_per_chain = lib.mc_program_waves_per_chain(h)

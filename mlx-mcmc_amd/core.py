@@ -26,7 +26,7 @@ int32 = np.int32
 def array(x, dtype=None):
     if isinstance(x, (list, tuple)) and any(isinstance(v, _trace.LogProbExpr) for v in x):
         return _trace.stack(list(x))
-    if isinstance(x, (_trace.LogProbExpr, _trace.Param)):
+    if isinstance(x, (_trace.LogProbExpr, _trace.Param, _trace.Affine)):
         return x
     a = np.asarray(_trace._to_numpy(x))
     if dtype is not None:

@@ -339,8 +339,17 @@ struct SlPartition {
     std::vector<std::vector<std::vector<int64_t>>> elems;  // [slice][term] element ids
 };
 
+static bool has_affine(const mc_program* p) {
+    for (const DevTerm& t : p->raw)
+        if (t.affine) return true;
+    return false;
+}
+
 static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = nullptr) {
     const std::vector<DevTerm>& raw = p->raw;
+    if (has_affine(p))
+        return fail(MC_ERR_UNSUPPORTED, "affine loc operands run on the chain-per-workgroup "
+                    "kernels (not sliceable)");
     const std::vector<float>& dp = p->h_data;
     const std::vector<int32_t>& ip = p->h_index;
     const int D = p->D;
@@ -1067,6 +1076,7 @@ static int64_t program_elements(const mc_program* p) {
 // stay unsliced (a per-step exchange costs more than the whole evaluation).
 static constexpr int64_t kLrAutoMinElements = 2048;
 static int auto_slices(const mc_program* p) {
+    if (has_affine(p)) return 1;
     const int64_t n = program_elements(p);
     if (n >= 65536) return 16;
     if (n >= 16384) return 8;
@@ -1203,7 +1213,18 @@ extern "C" int32_t mc_program_num_slices(const mc_program* p) { return p ? p->sl
 extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t n_params,
                                  float lp_const, const float* data, int64_t n_data,
                                  const int32_t* index, int64_t n_index, mc_program** out) {
+    return mc_program_create_affine(terms, n_terms, nullptr, 0, n_params, lp_const, data, n_data,
+                                    index, n_index, out);
+}
+
+extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
+                                        const mc_affine* affines, int32_t n_affines,
+                                        int32_t n_params, float lp_const, const float* data,
+                                        int64_t n_data, const int32_t* index, int64_t n_index,
+                                        mc_program** out) {
     if (!out) return fail(MC_ERR_INVALID, "out is NULL");
+    if (n_affines < 0 || (n_affines > 0 && !affines))
+        return fail(MC_ERR_INVALID, "bad affine array");
     *out = nullptr;
     if (n_params <= 0) return fail(MC_ERR_INVALID, "n_params must be positive (got %d)", n_params);
     if (n_terms < 0 || (n_terms > 0 && !terms)) return fail(MC_ERR_INVALID, "bad term array");
@@ -1229,10 +1250,29 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
         dt.n = n;
         dt.weight = src.weight;
         dt.c0 = dist_c0(src.dist);
-        const mc_operand* ops[3] = {&src.value, &src.loc, &src.scale};
-        for (int a = 0; a < 3; ++a) {
+        const mc_operand* ops[5] = {&src.value, &src.loc, &src.scale, nullptr, nullptr};
+        int nops = 3;
+        if (src.affine != 0) {
+            if (src.affine < 0 || src.affine > n_affines)
+                return fail(MC_ERR_INVALID, "term %d: affine index %d out of range", t,
+                            src.affine);
+            if (src.dist != MC_DIST_NORMAL)
+                return fail(MC_ERR_UNSUPPORTED, "term %d: an affine loc needs a Normal term", t);
+            const mc_affine& af = affines[src.affine - 1];
+            if (af.slope.kind != MC_OP_CONST && af.slope.kind != MC_OP_PSCALAR)
+                return fail(MC_ERR_UNSUPPORTED, "term %d: affine slope must be a constant or a "
+                            "scalar parameter", t);
+            if (af.x.kind != MC_OP_DATA && af.x.kind != MC_OP_PVEC && af.x.kind != MC_OP_GATHER)
+                return fail(MC_ERR_UNSUPPORTED, "term %d: affine x must be data, a parameter "
+                            "vector or a gather", t);
+            ops[3] = &af.slope;
+            ops[4] = &af.x;
+            nops = 5;
+            dt.affine = 1;
+        }
+        for (int a = 0; a < nops; ++a) {
             const mc_operand& o = *ops[a];
-            DevOperand& d = dt.op[a];
+            DevOperand& d = a < 3 ? dt.op[a] : (a == 3 ? dt.ab : dt.ax);
             d.kind = o.kind;
             d.poff = o.param_offset;
             d.pool = o.pool_offset;
@@ -1282,6 +1322,14 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
                     return fail(MC_ERR_INVALID, "term %d op %d: bad operand kind %d", t, a,
                                 o.kind);
             }
+        }
+        if (dt.affine) {
+            for (const DevOperand* d : {&dt.op[0], &dt.op[1], &dt.op[2], &dt.ab, &dt.ax})
+                if (d->kind == MC_OP_GATHER && !d->unique)
+                    return fail(MC_ERR_UNSUPPORTED, "term %d: an affine-loc term cannot gather "
+                                "through a non-injective index", t);
+            if (dt.op[1].kind == MC_OP_NONE)
+                return fail(MC_ERR_INVALID, "term %d: affine loc without a loc operand", t);
         }
         // the non-injective gather, if any, orders the term
         int primary = -1;
@@ -1373,6 +1421,33 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
             if (placed < 0) placed = npass++;
             masks[placed] |= bit;
         }
+        if (dt.affine) {
+            // the slope's and x's cotangents accumulate in the loc's sweep:
+            // x must not overlap another accumulating operand of the term
+            const bool acc = dt.ab.kind == MC_OP_PSCALAR || is_acc_vec(dt.ax.kind);
+            bool has_loc = false;
+            for (int ps = 0; ps < npass; ++ps) has_loc |= (masks[ps] & PASS_LOC) != 0;
+            if (acc && !has_loc) masks[0] |= PASS_LOC;
+            if (is_acc_vec(dt.ax.kind)) {
+                int64_t xl, xh;
+                if (dt.ax.kind == MC_OP_PVEC) {
+                    xl = dt.ax.poff;
+                    xh = dt.ax.poff + n - 1;
+                } else {
+                    int32_t mn = ipool[dt.ax.pool], mx = ipool[dt.ax.pool];
+                    for (int64_t i = 1; i < n; ++i) {
+                        mn = std::min(mn, ipool[dt.ax.pool + i]);
+                        mx = std::max(mx, ipool[dt.ax.pool + i]);
+                    }
+                    xl = dt.ax.poff + mn;
+                    xh = dt.ax.poff + mx;
+                }
+                for (int a = 0; a < 3; ++a)
+                    if (is_acc_vec(dt.op[a].kind) && !(xh < lo[a] || hi[a] < xl))
+                        return fail(MC_ERR_UNSUPPORTED, "term %d: the affine x overlaps operand "
+                                    "%d's parameters", t, a);
+            }
+        }
         dt.npass = npass;
         dt.pass_masks = masks[0] | (masks[1] << 4) | (masks[2] << 8);
         dt.wave_task = -1;
@@ -1387,13 +1462,19 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
     // broadcast-parameter cotangent slots and their fixed-order finalize list
     int32_t nslot = 0;
     std::vector<std::pair<int32_t, int32_t>> uses;  // (param, slot)
-    for (DevTerm& dt : dts)
+    for (DevTerm& dt : dts) {
         for (int a = 0; a < 3; ++a)
             if (dt.op[a].kind == MC_OP_PSCALAR) {
                 dt.op[a].slot = nslot;
                 uses.push_back({dt.op[a].poff, nslot});
                 ++nslot;
             }
+        if (dt.affine && dt.ab.kind == MC_OP_PSCALAR) {
+            dt.ab.slot = nslot;
+            uses.push_back({dt.ab.poff, nslot});
+            ++nslot;
+        }
+    }
     std::stable_sort(uses.begin(), uses.end(),
                      [](const std::pair<int32_t, int32_t>& x,
                         const std::pair<int32_t, int32_t>& y) { return x.first < y.first; });
@@ -1419,6 +1500,8 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
             bool vec_param = false;
             for (int a = 0; a < 3; ++a)
                 if (dt.op[a].kind == MC_OP_PVEC || dt.op[a].kind == MC_OP_GATHER) vec_param = true;
+            if (dt.affine && (dt.ax.kind == MC_OP_PVEC || dt.ax.kind == MC_OP_GATHER))
+                vec_param = true;
             if (dt.primary < 0 && dt.npass == 1 && dt.n <= 64 && !vec_param)
                 dt.wave_task = (next++) % wpc;
         }
@@ -1433,8 +1516,9 @@ extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t 
         std::vector<std::pair<int64_t, int64_t>> open_ranges;
         for (DevTerm& dt : dts) {
             std::vector<std::pair<int64_t, int64_t>> mine;
-            for (int a = 0; a < 3; ++a) {
-                const DevOperand& d = dt.op[a];
+            for (int a = 0; a < 4; ++a) {
+                if (a == 3 && !dt.affine) break;
+                const DevOperand& d = a < 3 ? dt.op[a] : dt.ax;
                 if (d.kind == MC_OP_PVEC) {
                     mine.push_back({d.poff, d.poff + dt.n - 1});
                 } else if (d.kind == MC_OP_GATHER) {

@@ -139,6 +139,11 @@ MC_DEV DevTerm load_term(const MC_CONST DevTerm* p) {
     t.tile_base = p->tile_base;
     t.lane_base = p->lane_base;
     t.comb_base = p->comb_base;
+    t.affine = p->affine;
+    if (t.affine) {
+        t.ab = load_op(&p->ab);
+        t.ax = load_op(&p->ax);
+    }
     return t;
 }
 
@@ -458,22 +463,41 @@ MC_DEV void accum(const DevOperand& o, int64_t i, float c, float& scalar_part, f
 }
 
 // Generic per-element path (vector scale, injective gathers): full formulas.
+// Affine loc (T.affine): m = loc + slope * x per element (the reference's two
+// f32 ops), and the loc cotangent cm also flows to the slope (cm * x, partial
+// pb) and to x (cm * slope).
 MC_DEV void strided_generic(const DevTerm& T, const DevCtx& P, const float* q, float* g, int tid,
                             int nthr, uint32_t mask, float uv, float um, float us, float ulogs,
-                            float ulg, float& lp_acc, float& pv, float& pm, float& ps) {
+                            float ulg, float& lp_acc, float& pv, float& pm, float& ps,
+                            float& pb) {
     const bool scale_vec = is_vec(T.op[2].kind);
     const bool lgv = lg_per_element(T.dist, T.op[1].kind, T.op[2].kind);
     const float w = T.weight;
+    const bool aff = T.affine != 0;
+    const float ub = aff ? uniform_value(T.ab, q) : 0.0f;
+    float dummy = 0.0f;
     for (int64_t i = tid; i < T.n; i += nthr) {
         const float v = fetch(T.op[0], i, uv, q, P);
-        const float m = fetch(T.op[1], i, um, q, P);
+        float m = fetch(T.op[1], i, um, q, P);
+        float xa = 0.0f;
+        if (aff) {
+            xa = fetch(T.ax, i, 0.0f, q, P);
+            m = m + ub * xa;
+        }
         const float s = fetch(T.op[2], i, us, q, P);
         const float logs = scale_vec ? logf(s) : ulogs;
         const float lg = lgv ? lgamma_norm(T.dist, m, s) : ulg;
         const ElemOut e = elem_eval(T.dist, T.c0, v, m, s, logs, lg);
         if (mask & PASS_LP) lp_acc += w * e.lp;
         if (mask & PASS_VALUE) accum(T.op[0], i, w * e.dv, pv, g, P);
-        if (mask & PASS_LOC) accum(T.op[1], i, w * e.dm, pm, g, P);
+        if (mask & PASS_LOC) {
+            const float cm = w * e.dm;
+            accum(T.op[1], i, cm, pm, g, P);
+            if (aff) {
+                pb += cm * xa;
+                accum(T.ax, i, cm * ub, dummy, g, P);
+            }
+        }
         if (mask & PASS_SCALE) accum(T.op[2], i, w * e.ds, ps, g, P);
     }
 }
@@ -709,14 +733,14 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
         const uint32_t mask =
             ((T.pass_masks >> (4 * pass)) & 0xFu) & (VALUE_ONLY ? PASS_LP : 0xFu);
         if (VALUE_ONLY && mask == 0) continue;  // uniform: no writes, no barrier needed
-        float pv = 0.0f, pm = 0.0f, ps = 0.0f;
+        float pv = 0.0f, pm = 0.0f, ps = 0.0f, pb = 0.0f;
         Moments M = {0.0f, 0.0f, 0.0f, false};
         bool moments = false;
 
         if (T.primary < 0) {
             const int fv = fast_kind(T.op[0].kind);
             const int fl = normal ? fast_kind(T.op[1].kind) : 0;
-            if (moment_dist && !scale_vec && fv >= 0 && fl >= 0) {
+            if (moment_dist && !scale_vec && fv >= 0 && fl >= 0 && !T.affine) {
                 moments = true;
                 const int code = normal ? (fv * 3 + fl) : (9 + fv);
                 switch (code) {
@@ -742,7 +766,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                 }
             } else {
                 strided_generic(T, P, q, g, tid, nthr, mask, uv, um, us, ulogs, ulg, lp_acc, pv,
-                                pm, ps);
+                                pm, ps, pb);
             }
         } else {
             float* vpart = S.vpart;
@@ -782,6 +806,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
         if ((mask & PASS_VALUE) && T.op[0].kind == MC_OP_PSCALAR) flush(T.op[0].slot, pv);
         if ((mask & PASS_LOC) && T.op[1].kind == MC_OP_PSCALAR) flush(T.op[1].slot, pm);
         if ((mask & PASS_SCALE) && T.op[2].kind == MC_OP_PSCALAR) flush(T.op[2].slot, ps);
+        if ((mask & PASS_LOC) && T.affine && T.ab.kind == MC_OP_PSCALAR) flush(T.ab.slot, pb);
         if (!VALUE_ONLY && pass + 1 < T.npass) G.sync();  // passes exist because their writes overlap
         MC_STAMP(22);
     }

@@ -61,6 +61,10 @@ struct DevTerm {
     int64_t tile_base;    // index pool: per tile {off, len_pad, len_min}
     int64_t lane_base;    // index pool: per virtual segment {k, len}
     int64_t comb_base;    // index pool: per segment {k, vfirst, vcount}
+    // ---- affine loc (mc_affine): loc_i = op[1]_i + ab_i * ax_i ----------------
+    int32_t affine;       // 0 / 1
+    int32_t pad_aff;
+    DevOperand ab, ax;    // slope (CONST / PSCALAR), x (DATA / PVEC / GATHER)
 };
 
 struct DevCtx {

@@ -38,10 +38,10 @@ def test_struct_layouts_match_header(tmp_path):
 #include "mcmc355.h"
 #define O(T, f) printf("%s.%s %zu\\n", #T, #f, offsetof(T, f));
 int main(void) {
-  printf("mc_operand %zu\\nmc_term %zu\\nmc_chain_scalars %zu\\nmc_run_config %zu\\nmc_trace %zu\\n",
+  printf("mc_operand %zu\\nmc_term %zu\\nmc_chain_scalars %zu\\nmc_run_config %zu\\nmc_trace %zu\\nmc_affine %zu\\n",
          sizeof(mc_operand), sizeof(mc_term), sizeof(mc_chain_scalars), sizeof(mc_run_config),
-         sizeof(mc_trace));
-  O(mc_term, value) O(mc_term, loc) O(mc_term, scale) O(mc_chain_scalars, logp)
+         sizeof(mc_trace), sizeof(mc_affine));
+  O(mc_term, affine) O(mc_affine, x) O(mc_term, value) O(mc_term, loc) O(mc_term, scale) O(mc_chain_scalars, logp)
   O(mc_chain_scalars, depth_sum) O(mc_chain_scalars, n_divergent) O(mc_run_config, seed)
   O(mc_run_config, step_size) O(mc_run_config, slice_mode) O(mc_trace, n_leapfrog)
   return 0;
@@ -58,7 +58,9 @@ int main(void) {
     assert int(out["mc_chain_scalars"]) == ctypes.sizeof(_lib.McChainScalars)
     assert int(out["mc_run_config"]) == ctypes.sizeof(_lib.McRunConfig)
     assert int(out["mc_trace"]) == ctypes.sizeof(_lib.McTrace)
+    assert int(out["mc_affine"]) == ctypes.sizeof(_lib.McAffine)
     for key, (cls, field) in {
+        "mc_term.affine": (_lib.McTerm, "affine"), "mc_affine.x": (_lib.McAffine, "x"),
         "mc_term.value": (_lib.McTerm, "value"), "mc_term.loc": (_lib.McTerm, "loc"),
         "mc_term.scale": (_lib.McTerm, "scale"),
         "mc_chain_scalars.logp": (_lib.McChainScalars, "logp"),

@@ -1,0 +1,123 @@
+"""Affine loc operands (include/mcmc355.h mc_affine; _trace.Affine): the
+reference differentiates any MLX expression of the parameters (hmc.py:53-67,
+nuts.py:76-87); the linear-predictor forms a + b * x (regression) and
+mu + tau * z (non-centred hierarchy) run on the GPU tape (eval.h
+strided_generic) and are checked against the CPU oracle, whose gradients are
+torch autograd over the same user model.
+
+Bars: tape log p within 2e-6 of sum |lp| (f32 summation order), gradients
+rtol 1e-4; HMC decisions / H / ratios equal to the oracle's until a proven
+near-tie (tests/_near_tie.py); NUTS trees identical for >= 10 iterations; MH
+decisions identical over 150 iterations; the regression posterior mean of the
+slope within 4 MCSE of the least-squares fit (flat-ish priors)."""
+import numpy as np
+import pytest
+
+import workloads as W
+from _near_tie import compare_trace, log_u
+from oracle import samplers as S
+
+pytestmark = pytest.mark.gpu
+
+MODELS = {"regression": lambda ns: W.linear_regression(ns, 1000),
+          "eight_schools_nc": W.eight_schools_nc}
+
+
+@pytest.mark.parametrize("model", list(MODELS))
+def test_affine_tape_matches_autograd(gpu, model):
+    from mlx_mcmc_amd import _engine, _trace
+
+    lp_fn, init = MODELS[model](W.ns_product())
+    prog = _trace.compile_model(lp_fn, init)
+    assert prog.num_slices == 1 and prog.slice_kernel == "unsliced"   # the tape kernels
+    olp, oinit = MODELS[model](W.ns_oracle())
+    M = S.EagerModel(olp, oinit)
+    rng = np.random.default_rng(7)
+    base = prog.layout.flatten(init)
+    pts = np.stack([base + rng.normal(0, 0.3, base.size).astype(np.float32) for _ in range(6)])
+    pts[:, prog.layout.names.index("sigma" if model == "regression" else "tau")] = \
+        np.abs(pts[:, prog.layout.names.index("sigma" if model == "regression" else "tau")]) + 0.2
+    lp, g = _engine.logp_grad(prog, pts)
+    lp, g = lp.cpu().numpy(), g.cpu().numpy()
+    for i, q in enumerate(pts):
+        rl, rg = M.logp_grad(q)
+        assert abs(lp[i] - rl) <= 2e-6 * max(1.0, abs(rl)) * 50, (i, lp[i], rl)
+        np.testing.assert_allclose(g[i], rg, rtol=1e-4, atol=1e-3 * max(1.0, np.abs(rg).max()))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_affine_hmc_trace_matches_oracle(gpu, seed):
+    import mlx_mcmc_amd as m
+
+    lp, _ = W.linear_regression(W.ns_product())
+    olp, _ = W.linear_regression(W.ns_oracle())
+    start = {"a": np.float32(1.4), "b": np.float32(1.9), "sigma": np.float32(0.6)}
+    kw = dict(num_samples=40, num_warmup=40, step_size=0.004, num_leapfrog_steps=10)
+    s, rate, info = m.hmc(lp, start, key=m.random.key(seed), progress=False, return_info=True,
+                          return_trace=True, **kw)
+    ref = S.hmc(olp, start, seed=seed, **kw)
+    n = len(ref.trace["accepted"])
+    tr = info.trace
+    gpu_c = {"accepted": tr["accepted"][0], "ratio": tr["accept_stat"][0],
+             "step_size": tr["step_size"][0], "energy": tr["energy"][0]}
+    ref_c = {k: np.asarray(ref.trace[k]) for k in ("accepted", "ratio", "step_size", "energy")}
+    ref_c["log_u"] = log_u(seed, 0, n)
+    same = compare_trace(gpu_c, ref_c, f"regression seed {seed}", verbose=True)
+    acc = np.asarray(ref.trace["accepted"][:same])
+    assert same >= 30 and acc.any() and not acc.all()
+    ns = max(0, same - 40)
+    np.testing.assert_allclose(s["b"][:ns], ref.samples[:ns, 1], rtol=1e-4, atol=1e-5)
+
+
+def test_affine_nuts_trace_matches_oracle(gpu):
+    import mlx_mcmc_amd as m
+
+    plp, pinit = W.eight_schools_nc(W.ns_product())
+    olp, oinit = W.eight_schools_nc(W.ns_oracle())
+    n_w, n_s = 30, 10
+    _, _, info = m.nuts(plp, pinit, num_samples=n_s, num_warmup=n_w, key=m.random.key(2),
+                        progress=False, return_info=True, return_trace=True)
+    assert info.extra["kernel"] == "tape"
+    ref = S.nuts(olp, oinit, num_samples=n_s, num_warmup=n_w, seed=2)
+    same = 0
+    for i in range(n_w + n_s):
+        if (info.trace["tree_depth"][0][i] != ref.trace["depth"][i]
+                or info.trace["n_leapfrog"][0][i] != ref.trace["leaves"][i]):
+            break
+        same += 1
+    assert same >= 10, f"trees diverged at iteration {same}"
+
+
+def test_affine_mh_trace_matches_oracle(gpu):
+    import mlx_mcmc_amd as m
+
+    lp, _ = W.linear_regression(W.ns_product())
+    olp, _ = W.linear_regression(W.ns_oracle())
+    start = {"a": 1.4, "b": 1.9, "sigma": 0.6}
+    n = 150
+    s, rate, info = m.metropolis_hastings(lp, start, num_samples=n, proposal_scale=0.02,
+                                          random_seed=5, return_info=True, return_trace=True)
+    ref = S.metropolis_hastings(olp, start, num_samples=n, proposal_scale=0.02, random_seed=5)
+    acc = info.trace["accepted"][0].astype(bool)
+    assert list(acc) == ref.trace["accepted"] and 0 < acc.mean() < 1
+    np.testing.assert_allclose(s["b"], ref.samples[:, 1], rtol=1e-5, atol=1e-6)
+
+
+def test_affine_regression_posterior(gpu):
+    import mlx_mcmc_amd as m
+
+    lp, _ = W.linear_regression(W.ns_product())
+    x, y = W.regression_data()
+    X = np.stack([np.ones_like(x), x], 1).astype(np.float64)
+    ab = np.linalg.lstsq(X, y.astype(np.float64), rcond=None)[0]
+    start = {"a": np.float32(ab[0]), "b": np.float32(ab[1]), "sigma": np.float32(0.5)}
+    s, rate, info = m.hmc(lp, start, num_samples=500, num_warmup=300, step_size=0.01,
+                          num_leapfrog_steps=10, key=m.random.key(1), num_chains=32,
+                          progress=False, return_info=True)
+    assert info.extra["kernel"] == "unsliced"
+    live = info.accept_rate > 0.05
+    assert live.sum() >= 16
+    for k, name in enumerate(("a", "b")):
+        d = s[name][live]                      # [C, S]
+        mcse = d.mean(1).std() / np.sqrt(d.shape[0])
+        assert abs(d.mean() - ab[k]) < 4 * mcse + 2e-3, (name, d.mean(), ab[k], mcse)

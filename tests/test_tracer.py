@@ -77,8 +77,58 @@ def test_slices_elements_and_weights():
     assert b.weight == -0.5 and tm.lp_const == 3.0
 
 
+def test_affine_loc_traces():
+    """Linear predictors trace to one Normal term with an affine loc
+    (include/mcmc355.h mc_affine): regression a + b * x over data, and the
+    non-centred mu + tau * z over a parameter vector."""
+    lp, init = W.linear_regression(W.ns_product(), 50)
+    tm = _trace.trace(lp, init)
+    lik = [t for t in tm.terms if t.aff is not None]
+    assert len(lik) == 1 and tm.n_affines == 1
+    t = lik[0]
+    assert (t.loc.kind, t.loc.param_offset) == (_lib.MC_OP_PSCALAR, 0)        # a
+    assert (t.aff[0].kind, t.aff[0].param_offset) == (_lib.MC_OP_PSCALAR, 1)  # b
+    assert t.aff[1].kind == _lib.MC_OP_DATA and t.n == 50
+    np.testing.assert_array_equal(t.aff[1].data, W.regression_data(50)[0])
+    assert tm.c_terms[[k for k, u in enumerate(tm.terms) if u.aff][0]].affine == 1
+    lp, init = W.eight_schools_nc(W.ns_product())
+    tm = _trace.trace(lp, init)
+    (t,) = [t for t in tm.terms if t.aff is not None]
+    assert t.loc.kind == _lib.MC_OP_PSCALAR and t.aff[0].kind == _lib.MC_OP_PSCALAR
+    assert (t.aff[1].kind, t.aff[1].param_offset, t.n) == (_lib.MC_OP_PVEC, 2, 8)
+    assert t.scale.kind == _lib.MC_OP_DATA and t.value.kind == _lib.MC_OP_DATA
+
+
+@pytest.mark.parametrize("expr, want", [
+    (lambda p: p["a"] + p["b"] * X3, ("p", "p", "d")),
+    (lambda p: X3 * p["b"] + p["a"], ("p", "p", "d")),
+    (lambda p: p["a"] - X3, ("p", "c", "d")),           # slope -1
+    (lambda p: 2.0 * p["v"], ("c", "c", "v")),            # loc 0
+    (lambda p: p["v"] + p["a"], ("p", "c", "v")),         # slope 1
+    (lambda p: p["b"] * p["v"] + 1.0, ("c", "p", "v")),
+])
+def test_affine_forms(expr, want):
+    def lp(p):
+        return mx.sum(m.Normal(expr(p), 1.0).log_prob(np.zeros(3, np.float32)))
+
+    tm = _trace.trace(lp, {"a": 1.0, "b": 2.0, "v": np.zeros(3, np.float32)})
+    (t,) = tm.terms
+    code = {_lib.MC_OP_PSCALAR: "p", _lib.MC_OP_CONST: "c", _lib.MC_OP_DATA: "d",
+            _lib.MC_OP_PVEC: "v"}
+    got = (code[t.loc.kind],) + ((code[t.aff[0].kind], code[t.aff[1].kind]) if t.aff else ())
+    assert got == want
+
+
+X3 = np.arange(3, dtype=np.float32)
+
+
 @pytest.mark.parametrize("bad", [
-    lambda p: m.Normal(0, 1).log_prob(p["x"] * 2.0),          # arithmetic on a param
+    lambda p: m.Normal(0, 1).log_prob(p["x"] * 2.0),          # an expression as a value
+    lambda p: mx.sum(m.Normal(p["x"] + p["x"] * X3 + p["x"] * X3, 1.0).log_prob(X3)),  # 2 products
+    lambda p: mx.sum(m.Normal(p["x"] * p["x"], 1.0).log_prob(X3)),  # product of parameters
+    lambda p: mx.sum(m.Normal(0.0, p["x"] * 2.0).log_prob(X3)),  # an expression as a scale
+    lambda p: m.Gamma(p["x"] * 2.0, 1.0).log_prob(p["x"]),      # not a Normal loc
+    lambda p: mx.sum(m.Normal((p["x"] + p["x"] * X3) * 2.0, 1.0).log_prob(X3)),  # scaled affine
     lambda p: m.Normal(0, 1).log_prob(p["x"]) if p["x"] > 0 else 0,  # Python branch
     lambda p: mx.log(p["x"]),                                   # unsupported primitive
     lambda p: m.Normal(0, 1).log_prob(p["v"]),                  # unsummed vector

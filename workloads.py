@@ -171,3 +171,38 @@ def eight_schools(ns):
 
     return log_prob, {"mu": np.float32(4.0), "tau": np.float32(3.0),
                       "theta": np.full(8, 4.0, np.float32)}
+
+
+def eight_schools_nc(ns):
+    """Non-centred eight schools: theta_j = mu + tau * z_j (an affine loc),
+    y_j ~ N(theta_j, sigma_j), z ~ N(0, 1)."""
+    y, sig = EIGHT_SCHOOLS_Y, EIGHT_SCHOOLS_SIGMA
+
+    def log_prob(params):
+        mu, tau, z = params["mu"], params["tau"], params["z"]
+        lp = ns.Normal(0, 5).log_prob(mu) + ns.HalfNormal(5).log_prob(tau)
+        lp = lp + ns.sum(ns.Normal(0, 1).log_prob(z))
+        return lp + ns.sum(ns.Normal(mu + tau * z, sig).log_prob(ns.array(y)))
+
+    return log_prob, {"mu": np.float32(4.0), "tau": np.float32(3.0),
+                      "z": np.zeros(8, np.float32)}
+
+
+# ---- linear regression: an affine loc a + b * x over data ------------------------
+def regression_data(n=1000, seed=3):
+    rng = np.random.default_rng(seed)
+    x = rng.normal(0.0, 1.0, n).astype(np.float32)
+    y = (1.5 + 2.0 * x + rng.normal(0.0, 0.5, n)).astype(np.float32)
+    return x, y
+
+
+def linear_regression(ns, n=1000):
+    x, y = regression_data(n)
+
+    def log_prob(params):
+        a, b, sigma = params["a"], params["b"], params["sigma"]
+        lp = ns.Normal(0, 10).log_prob(a) + ns.Normal(0, 10).log_prob(b)
+        lp = lp + ns.HalfNormal(5).log_prob(sigma)
+        return lp + ns.sum(ns.Normal(a + b * ns.array(x), sigma).log_prob(ns.array(y)))
+
+    return log_prob, {"a": np.float32(0.0), "b": np.float32(0.0), "sigma": np.float32(1.0)}
