@@ -225,6 +225,28 @@ def check(chains, where):
         sys.exit(3)
 
 
+def init_ranks():
+    """One process per GPU (torchrun): RCCL over the node's GPUs.  With
+    MC_DIST_BACKEND=gloo the ranks may share GPUs (rank r on GPU r % count): a
+    rehearsal of the multi-rank path on a one-GPU box, collectives on host
+    copies."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("MC_DIST_BACKEND", "nccl")
+    gpu = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
+    if world > 1:
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, local, torch.device("cuda", gpu)
+
+
 NUTS_D = 100
 # SURVEY 8d unit for NUTS: one leaf (leapfrog step + gradient + Hamiltonian);
 # algorithmic FP32 flops per leaf of the D-dim diagonal Gaussian: kicks and
@@ -272,13 +294,7 @@ def main_nuts(args):
     from mlx_mcmc_amd import _engine, _trace
     from mlx_mcmc_amd.distributed import max_over_ranks, shard
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    world, rank, local, dev = init_ranks()
     C, K, Wm, B = args.chains, args.steps, args.warmup, max(1, args.iters_per_launch)
     lp_fn, init = W.illcond_normal(W.ns_product(), NUTS_D)
     prog = _trace.compile_model(lp_fn, init)
@@ -373,13 +389,7 @@ def main():
     from mlx_mcmc_amd import _engine, _trace
     from mlx_mcmc_amd.distributed import gather_to_root, max_over_ranks, shard
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    world, rank, local, dev = init_ranks()
 
     G, N = W.SHAPES[args.shape]
     D = G + 3

@@ -84,7 +84,13 @@ def _all_reduce(t, group):
 
     if group is not False and dist.is_available() and dist.is_initialized() \
             and dist.get_world_size(group) > 1:
-        dist.all_reduce(t, group=group)
+        if dist.get_backend(group) == "gloo" and t.is_cuda:
+            # gloo (a CPU rehearsal of the RCCL path): reduce a host copy
+            h = t.cpu()
+            dist.all_reduce(h, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, group=group)
     return t
 
 

@@ -6,7 +6,9 @@ Independent chains shard embarrassingly: global chains
 is keyed by the *global* chain id, so the samples of a chain do not depend on
 how many GPUs run the job.  There is no exchange during sampling; the only
 collective is the final gather of the samples to rank 0 (``gather_to_root``),
-plus a max-reduction of wall times for reporting.
+plus a max-reduction of wall times for reporting.  With the gloo backend (a
+CPU rehearsal of the RCCL path, e.g. several ranks sharing one GPU) the
+collectives run on host copies.
 """
 from __future__ import annotations
 
@@ -34,6 +36,9 @@ def gather_to_root(t, group=None) -> Optional[object]:
     rank = dist.get_rank(group)
     if world == 1:
         return t
+    if dist.get_backend(group) == "gloo" and t.is_cuda:
+        out = gather_to_root(t.cpu(), group)
+        return None if out is None else out.to(t.device)
     n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
     counts = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(counts, n, group=group)
@@ -56,6 +61,8 @@ def max_over_ranks(x: float, device=None, group=None) -> float:
 
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return float(x)
+    if dist.get_backend(group) == "gloo":
+        device = "cpu"
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())

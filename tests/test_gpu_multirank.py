@@ -1,0 +1,109 @@
+"""The multi-rank product path on one GPU: two ranks share the
+box's GPU over the gloo backend (a rehearsal of the RCCL path the driver runs
+on 8 GPUs: same sharding, same chain-offset RNG contract, same collectives on
+host copies).
+
+* Two spawned ranks run the product sampler (HIP kernels) on their shards of
+  the chains; the samples gathered to rank 0 are bit-identical to one process
+  running every chain (draws are keyed by the global chain id), for HMC on the
+  lane-resident kernel and for NUTS.
+* bench.py under torchrun with two ranks prints one line whose value
+  aggregates both ranks (128 chains), with the diagnostics' all-reduce and the
+  sample gather exercised (the small hierarchical shape: one slice, so the two
+  processes' kernels need no cross-workgroup co-residency on the shared GPU).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(algo, C, offset):
+    import mlx_mcmc_amd as m
+
+    lp, init = W.hierarchical(W.ns_product(), *W.SHAPES["small"])
+    kw = dict(num_samples=40, num_warmup=40, key=m.random.key(6), num_chains=C,
+              chain_offset=offset, progress=False, keep_on_device=True, return_info=True)
+    if algo == "hmc":
+        _, _, info = m.hmc(lp, init, step_size=0.01, num_leapfrog_steps=10, **kw)
+    else:
+        _, _, info = m.nuts(lp, init, step_size=0.05, **kw)
+    return info.device_samples.contiguous()
+
+
+def _worker(rank, world, port, algo, C, q):
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import __graft_entry__ as ge
+
+    ge._ensure_pkg()
+    from mlx_mcmc_amd.distributed import gather_to_root, shard
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        off, cnt = shard(C, world, rank)
+        mine = _run(algo, cnt, off)
+        allc = gather_to_root(mine)
+        if rank == 0:
+            q.put(allc.cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("algo", ["hmc", "nuts"])
+def test_two_ranks_on_one_gpu_match_one_process(gpu, algo):
+    C, world = 12, 2
+    ref = _run(algo, C, 0).cpu().numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, algo, C, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=150)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got.shape == ref.shape
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_bench_two_ranks_gloo(gpu):
+    env = dict(os.environ, MC_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
+           "--chains", "64", "--shape", "small", "--gather", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=150, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["total_chains"] == 128
+    assert out["value"] > 0 and "gather_ms" in out
+    assert out["value"] == pytest.approx(128 * 20 * 20 / (out["ms_per_step"] * 20 / 1e3),
+                                         rel=1e-6)
