@@ -286,7 +286,10 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
                                                 MC_RNG_TAG_MERGE, (uint32_t)j,
                                                 ((uint32_t)l << 20) | (uint32_t)k);
                     const double den = (double)(pn + cn) > 1.0 ? (double)(pn + cn) : 1.0;
-                    const bool take_second = (double)mc_u01_f32(rm.x) < (double)cn / den;
+                    // U < cn / den (nuts.py:205) as U * den < cn: exact in f64 (U a
+                    // multiple of 2^-24, den < 2^24), the same decision as the
+                    // rounded quotient (no representable U lies between the two)
+                    const bool take_second = (double)mc_u01_f32(rm.x) * den < (double)cn;
                     if (take_second) {
                         freemask |= (1u << pidx);
                     } else {
@@ -315,9 +318,9 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
             // ---- top level (nuts.py:262-284) --------------------------------
             if (s_sub) {
                 const double den = (double)n > 1.0 ? (double)n : 1.0;
-                double pacc = (double)cn / den;
-                pacc = (pacc < 1.0) ? pacc : 1.0;
-                if ((double)mc_u01_f32(rd.y) < pacc) {
+                // U < min(1, cn / den) (nuts.py:269-272); U < 1 always, and U < cn / den
+                // as U * den < cn (exact, see the merge)
+                if ((double)mc_u01_f32(rd.y) * den < (double)cn) {
                     const float* cq = pool + (int64_t)(2 * cand) * Dp;
                     const float* cgp = pool + (int64_t)(2 * cand + 1) * Dp;
                     for (int jj = G.tid; jj < D; jj += T) {

@@ -138,6 +138,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp);
         float slp[2] = {0.f, 0.f}, sg_self = 0.0f;
         lr_scalar_terms(P.n_sterms, P.n_sterms_generic, sst, own, sh, j, Dsh, slp, sg_self);
+        if (Dsh == 0) {  // no shared cotangents: one reduction
+            sh.g = 0.0f;
+            return (wave_sum(lpp[0]) + slp[0]) + P.lp_const;
+        }
         float v8[8], t8[8];
         v8[0] = lpp[0];
         v8[1] = lpp[1];
@@ -180,6 +184,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
     int64_t n_grad = 0;
 
     for (int64_t it = cfg.iter_begin; it < it_end; ++it) {
+        MC_STAMP_DECL
         if (it == cfg.num_warmup) {  // nuts.py:318-319, 328-330
             if (cfg.adapt_step_size) eps = sc.step_size_bar;
             sc.warmup_accept = sc.n_accept;
@@ -252,6 +257,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         int n = 1;
         bool s = true;
         int jd = 0;
+        MC_STAMP(14);
         double alpha_sum = 0.0;
         int n_alpha = 0;
         int leaves = 0;
@@ -316,7 +322,9 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     sh.q = sh.q + e * pj;
                 }
                 if (Dsh > 0) derive();
+                MC_STAMP(8);
                 const float lpl = evaluate();
+                MC_STAMP(9);
 #pragma unroll
                 for (int r = 0; r < RS; ++r)
 #pragma unroll
@@ -330,6 +338,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                 alpha_sum += (a < 1.0) ? a : 1.0;
                 n_alpha += 1;
                 if (!s_leaf) divergent += 1;
+                MC_STAMP(10);
 
                 // park the leaf as a candidate and, if it opens a subtree of
                 // level >= 1, as that subtree's first leaf
@@ -354,6 +363,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     *at(0, fslot, 0, RS) = sh.q;
                     *at(0, fslot, 1, RS) = sh.p;
                 }
+                MC_STAMP(11);
                 if (!s_leaf) {
                     s_sub = false;
                     break;
@@ -376,7 +386,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                                                 MC_RNG_TAG_MERGE, (uint32_t)jd,
                                                 ((uint32_t)l << 20) | (uint32_t)k);
                     const double den = (double)(pn + cn) > 1.0 ? (double)(pn + cn) : 1.0;
-                    const bool take_second = (double)mc_u01_f32(rm.x) < (double)cn / den;
+                    // U < cn / den (nuts.py:205) as U * den < cn: exact in f64 (U a
+                    // multiple of 2^-24, den < 2^24), the same decision as the
+                    // rounded quotient (no representable U lies between the two)
+                    const bool take_second = (double)mc_u01_f32(rm.x) * den < (double)cn;
                     if (take_second) {
                         freemask |= (1u << pidx);
                     } else {
@@ -402,6 +415,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                         break;
                     }
                 }
+                MC_STAMP(12);
                 if (!s_sub) break;
                 if (parked) continue;
                 // l reached jd: the depth-jd subtree is complete
@@ -422,9 +436,9 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
             // ---- top level (nuts.py:262-284) --------------------------------
             if (s_sub) {
                 const double den = (double)n > 1.0 ? (double)n : 1.0;
-                double pacc = (double)cn / den;
-                pacc = (pacc < 1.0) ? pacc : 1.0;
-                if ((double)mc_u01_f32(rd.y) < pacc) {
+                // U < min(1, cn / den) (nuts.py:269-272); U < 1 always, and U < cn / den
+                // as U * den < cn (exact, see the merge)
+                if ((double)mc_u01_f32(rd.y) * den < (double)cn) {
 #pragma unroll
                     for (int r = 0; r < RS; ++r) {
                         const float q = *at(1, cand, 0, r), g = *at(1, cand, 1, r);
@@ -455,6 +469,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                 s = false;
             }
             jd += 1;
+            MC_STAMP(13);
         }
 
         const double alpha = alpha_sum / (n_alpha > 1 ? (double)n_alpha : 1.0);
@@ -499,6 +514,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                 if (tr.n_leapfrog) tr.n_leapfrog[o] = leaves;
             }
         }
+        MC_STAMP(15);
     }
     MC_STAMP_FLUSH
 
