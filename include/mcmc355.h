@@ -110,11 +110,13 @@ typedef struct mc_term {
  *     loc_i = loc_i + slope_i * x_i      (f32: one product, then one sum)
  * for a Normal term whose `affine` field is k + 1 (affines[k]).  slope is
  * CONST or PSCALAR; x is DATA, PVEC or a GATHER; the term's own loc operand is
- * CONST, PSCALAR, DATA, PVEC or a GATHER.  Gathers of an affine term must be
- * injective, and x's parameter range must not overlap another accumulating
- * operand of the term (MC_ERR_UNSUPPORTED otherwise).  Examples: a + b * x
- * (linear regression), mu + tau * z (non-centred hierarchy).  Affine
- * programs run on the chain-per-workgroup kernels (k_hmc, k_nuts, k_mh).   */
+ * CONST, PSCALAR, DATA, PVEC or a GATHER.  A non-injective gather may only
+ * be the loc itself with a DATA x (alpha[group] + beta * x: the segmented
+ * tape); x's parameter range must not overlap another accumulating operand
+ * of the term (MC_ERR_UNSUPPORTED otherwise).  Examples: a + b * x (linear
+ * regression), mu + tau * z (non-centred hierarchy), alpha[g] + beta * x
+ * (varying intercepts).  Affine programs run on the chain-per-workgroup
+ * kernels (k_hmc, k_nuts, k_mh).                                            */
 typedef struct mc_affine {
     mc_operand slope, x;
 } mc_affine;

@@ -236,9 +236,10 @@ static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<in
         d.pool = base;
         d.unique = 1;
     }
-    // tiled copies of every other vector operand
-    for (int b = 0; b < 3; ++b) {
-        DevOperand& d = dt.op[b];
+    // tiled copies of every other vector operand (and an affine loc's data x)
+    for (int b = 0; b < 4; ++b) {
+        if (b == 3 && !dt.affine) break;
+        DevOperand& d = b < 3 ? dt.op[b] : dt.ax;
         if (b == a || (d.kind != MC_OP_DATA && d.kind != MC_OP_GATHER)) continue;
         if (d.kind == MC_OP_DATA) {
             while (dpool.size() % 64) dpool.push_back(0.0f);
@@ -1324,10 +1325,14 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
             }
         }
         if (dt.affine) {
-            for (const DevOperand* d : {&dt.op[0], &dt.op[1], &dt.op[2], &dt.ab, &dt.ax})
-                if (d->kind == MC_OP_GATHER && !d->unique)
-                    return fail(MC_ERR_UNSUPPORTED, "term %d: an affine-loc term cannot gather "
-                                "through a non-injective index", t);
+            // a non-injective gather only as the loc itself (alpha[group] + b * x,
+            // the segmented path), with a data x
+            for (int k = 0; k < 5; ++k) {
+                const DevOperand* d = k < 3 ? &dt.op[k] : (k == 3 ? &dt.ab : &dt.ax);
+                if (d->kind == MC_OP_GATHER && !d->unique && !(k == 1 && dt.ax.kind == MC_OP_DATA))
+                    return fail(MC_ERR_UNSUPPORTED, "term %d: an affine-loc term gathers through "
+                                "a non-injective index only in its loc, with a data x", t);
+            }
             if (dt.op[1].kind == MC_OP_NONE)
                 return fail(MC_ERR_INVALID, "term %d: affine loc without a loc operand", t);
         }
@@ -1352,8 +1357,9 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
                 std::stable_sort(perm.begin(), perm.end(), [&](int64_t x, int64_t y) {
                     return ipool[ip + x] < ipool[ip + y];
                 });
-                for (int a = 0; a < 3; ++a) {
-                    DevOperand& d = dt.op[a];
+                for (int a = 0; a < 4; ++a) {
+                    if (a == 3 && !dt.affine) break;
+                    DevOperand& d = a < 3 ? dt.op[a] : dt.ax;  // (an affine x is data)
                     if (d.kind == MC_OP_DATA) {
                         const int64_t base = (int64_t)dpool.size();
                         for (int64_t i = 0; i < n; ++i) dpool.push_back(dpool[d.pool + perm[i]]);

@@ -648,7 +648,7 @@ template <int WPC>
 MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float* g,
                         const Group<WPC>& G, uint32_t mask, float uv, float um, float us,
                         float ulogs, float ulg, float& lp_acc, float& pv, float& pm, float& ps,
-                        float* vpart) {
+                        float& pb, float* vpart) {
     const int wave = G.tid >> 6;
     const int lane = G.tid & 63;
     const int a = T.primary;
@@ -661,6 +661,8 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
     const bool lgv = lg_per_element(T.dist, a == 1 ? MC_OP_PVEC : T.op[1].kind,
                                     a == 2 ? MC_OP_PVEC : T.op[2].kind);
     const float w = T.weight;
+    const bool aff = T.affine != 0;  // loc = (gathered) loc + slope * x, x data (tiled)
+    const float ub = aff ? uniform_value(T.ab, q) : 0.0f;
     for (int t = wave; t < T.ntiles; t += WPC) {
         const int off = tiles[3 * t];
         const int lpad = tiles[3 * t + 1];
@@ -674,7 +676,9 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
             if (u < len) {
                 const int64_t e = seg_elem(off, u, lane);
                 const float vv = seg_fetch(T.op[0], e, uv, th, a == 0, q, P);
-                const float m = seg_fetch(T.op[1], e, um, th, a == 1, q, P);
+                float m = seg_fetch(T.op[1], e, um, th, a == 1, q, P);
+                const float xa = aff ? P.data[T.ax.pool + e] : 0.0f;
+                if (aff) m = m + ub * xa;
                 const float s = seg_fetch(T.op[2], e, us, th, a == 2, q, P);
                 const float logs = (scale_vec || a == 2) ? logf(s) : ulogs;
                 const float lg = lgv ? lgamma_norm(T.dist, m, s) : ulg;
@@ -685,8 +689,10 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
                     else accum(T.op[0], e, w * o.dv, pv, g, P);
                 }
                 if (mask & PASS_LOC) {
-                    if (a == 1) cp += w * o.dm;
-                    else accum(T.op[1], e, w * o.dm, pm, g, P);
+                    const float cm = w * o.dm;
+                    if (a == 1) cp += cm;
+                    else accum(T.op[1], e, cm, pm, g, P);
+                    if (aff) pb += cm * xa;
                 }
                 if (mask & PASS_SCALE) {
                     if (a == 2) cp += w * o.ds;
@@ -771,7 +777,8 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
         } else {
             float* vpart = S.vpart;
             const int other_kind = T.primary == 1 ? T.op[0].kind : T.op[1].kind;
-            const bool fast = normal && !scale_vec && T.primary <= 1 && other_kind == MC_OP_DATA;
+            const bool fast = normal && !scale_vec && T.primary <= 1 && other_kind == MC_OP_DATA &&
+                              !T.affine;
             if (fast) {
                 moments = true;
                 if (T.primary == 1)
@@ -780,7 +787,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                     seg_normal_uscale<WPC, 0>(T, P, q, g, G, mask, var, M, vpart);
             } else {
                 seg_generic<WPC>(T, P, q, g, G, mask, uv, um, us, ulogs, ulg, lp_acc, pv, pm,
-                                 ps, vpart);
+                                 ps, pb, vpart);
             }
             if (T.ncomb > 0 && (mask & (1u << T.primary))) {
                 // split segments: add the virtual partials in order

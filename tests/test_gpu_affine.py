@@ -1,9 +1,10 @@
 """Affine loc operands (include/mcmc355.h mc_affine; _trace.Affine): the
 reference differentiates any MLX expression of the parameters (hmc.py:53-67,
-nuts.py:76-87); the linear-predictor forms a + b * x (regression) and
-mu + tau * z (non-centred hierarchy) run on the GPU tape (eval.h
-strided_generic) and are checked against the CPU oracle, whose gradients are
-torch autograd over the same user model.
+nuts.py:76-87); the linear-predictor forms a + b * x (regression),
+mu + tau * z (non-centred hierarchy) and alpha[group] + beta * x
+(varying-intercept regression) run on the GPU tape (eval.h strided_generic,
+and seg_generic for the non-injective gather) and are checked against the
+CPU oracle, whose gradients are torch autograd over the same user model.
 
 Bars: tape log p within 2e-6 of sum |lp| (f32 summation order), gradients
 rtol 1e-4; HMC decisions / H / ratios equal to the oracle's until a proven
@@ -20,7 +21,8 @@ from oracle import samplers as S
 pytestmark = pytest.mark.gpu
 
 MODELS = {"regression": lambda ns: W.linear_regression(ns, 1000),
-          "eight_schools_nc": W.eight_schools_nc}
+          "eight_schools_nc": W.eight_schools_nc,
+          "varying_intercept": W.varying_intercept}
 
 
 @pytest.mark.parametrize("model", list(MODELS))
@@ -35,8 +37,10 @@ def test_affine_tape_matches_autograd(gpu, model):
     rng = np.random.default_rng(7)
     base = prog.layout.flatten(init)
     pts = np.stack([base + rng.normal(0, 0.3, base.size).astype(np.float32) for _ in range(6)])
-    pts[:, prog.layout.names.index("sigma" if model == "regression" else "tau")] = \
-        np.abs(pts[:, prog.layout.names.index("sigma" if model == "regression" else "tau")]) + 0.2
+    for nm in ("sigma", "tau"):
+        if nm in prog.layout.names:
+            k = prog.layout.offsets[prog.layout.names.index(nm)]
+            pts[:, k] = np.abs(pts[:, k]) + 0.2
     lp, g = _engine.logp_grad(prog, pts)
     lp, g = lp.cpu().numpy(), g.cpu().numpy()
     for i, q in enumerate(pts):
@@ -121,3 +125,31 @@ def test_affine_regression_posterior(gpu):
         d = s[name][live]                      # [C, S]
         mcse = d.mean(1).std() / np.sqrt(d.shape[0])
         assert abs(d.mean() - ab[k]) < 4 * mcse + 2e-3, (name, d.mean(), ab[k], mcse)
+
+
+def test_affine_varying_intercept_hmc_trace(gpu):
+    """alpha[group] + beta * x (the segmented tape, a non-injective gather as
+    the affine loc) against the oracle's HMC trace."""
+    import mlx_mcmc_amd as m
+
+    lp, init = W.varying_intercept(W.ns_product())
+    olp, oinit = W.varying_intercept(W.ns_oracle())
+    x, y, g = W.varying_intercept_data()
+    start = dict(init)
+    start["alpha"] = np.array([y[g == k].mean() - 0.7 * x[g == k].mean() for k in range(20)],
+                              np.float32)
+    kw = dict(num_samples=30, num_warmup=30, step_size=0.01, num_leapfrog_steps=10)
+    s, rate, info = m.hmc(lp, start, key=m.random.key(1), progress=False, return_info=True,
+                          return_trace=True, num_slices=1, **kw)
+    ref = S.hmc(olp, start, seed=1, **kw)
+    # the first 25 iterations: the positions' fp32 drift after that moves a
+    # large rejection's ratio (|ratio| ~ 50) by more than 8 ulp of |H|
+    n = 25
+    tr = info.trace
+    gpu_c = {"accepted": tr["accepted"][0][:n], "ratio": tr["accept_stat"][0][:n],
+             "step_size": tr["step_size"][0][:n], "energy": tr["energy"][0][:n]}
+    ref_c = {k: np.asarray(ref.trace[k])[:n] for k in ("accepted", "ratio", "step_size", "energy")}
+    ref_c["log_u"] = log_u(1, 0, n)
+    same = compare_trace(gpu_c, ref_c, "varying intercept", verbose=True)
+    acc = np.asarray(ref.trace["accepted"][:same])
+    assert same >= 20 and acc.any()

@@ -99,6 +99,16 @@ def test_affine_loc_traces():
     assert t.scale.kind == _lib.MC_OP_DATA and t.value.kind == _lib.MC_OP_DATA
 
 
+def test_affine_varying_intercept_traces():
+    """alpha[group] + beta * x: an affine loc whose own operand is a
+    non-injective gather (the segmented tape path)."""
+    lp, init = W.varying_intercept(W.ns_product())
+    tm = _trace.trace(lp, init)
+    (t,) = [t for t in tm.terms if t.aff is not None]
+    assert t.loc.kind == _lib.MC_OP_GATHER and t.n == 2000
+    assert t.aff[0].kind == _lib.MC_OP_PSCALAR and t.aff[1].kind == _lib.MC_OP_DATA
+
+
 @pytest.mark.parametrize("expr, want", [
     (lambda p: p["a"] + p["b"] * X3, ("p", "p", "d")),
     (lambda p: X3 * p["b"] + p["a"], ("p", "p", "d")),

@@ -206,3 +206,30 @@ def linear_regression(ns, n=1000):
         return lp + ns.sum(ns.Normal(a + b * ns.array(x), sigma).log_prob(ns.array(y)))
 
     return log_prob, {"a": np.float32(0.0), "b": np.float32(0.0), "sigma": np.float32(1.0)}
+
+
+def varying_intercept_data(G=20, N=2000, seed=4):
+    rng = np.random.default_rng(seed)
+    group = np.sort(rng.integers(0, G, N)).astype(np.int32)
+    alpha = rng.normal(1.0, 1.5, G)
+    x = rng.normal(0.0, 1.0, N).astype(np.float32)
+    y = (alpha[group] + 0.7 * x + rng.normal(0.0, 0.8, N)).astype(np.float32)
+    return x, y, group
+
+
+def varying_intercept(ns, G=20, N=2000):
+    """Varying-intercept regression: y_i ~ N(alpha[g_i] + beta * x_i, sigma)
+    (an affine loc through a non-injective gather), alpha ~ N(mu, tau)."""
+    x, y, group = varying_intercept_data(G, N)
+
+    def log_prob(params):
+        mu, tau, beta, sigma = params["mu"], params["tau"], params["beta"], params["sigma"]
+        alpha = params["alpha"]
+        lp = ns.Normal(0, 10).log_prob(mu) + ns.HalfNormal(5).log_prob(tau)
+        lp = lp + ns.Normal(0, 10).log_prob(beta) + ns.HalfNormal(5).log_prob(sigma)
+        lp = lp + ns.sum(ns.Normal(mu, tau).log_prob(alpha))
+        return lp + ns.sum(ns.Normal(alpha[group] + beta * ns.array(x), sigma)
+                           .log_prob(ns.array(y)))
+
+    return log_prob, {"mu": np.float32(1.0), "tau": np.float32(1.5), "beta": np.float32(0.7),
+                      "sigma": np.float32(0.8), "alpha": np.ones(G, np.float32)}
