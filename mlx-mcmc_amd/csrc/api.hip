@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <map>
 #include <mutex>
 #include <tuple>
 #include <type_traits>
@@ -1624,8 +1625,20 @@ static bool hmc_use_lds(const mc_program* p) {
 template <typename K>
 static hipError_t allow_lds(K kernel, size_t bytes) {
     if (bytes <= 64 * 1024) return hipSuccess;
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    // once per (kernel, device, size): the attribute call costs host time on
+    // every launch otherwise (launch functions run once per chunk of iterations)
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, int, size_t>, hipError_t> done;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto key = std::make_tuple(reinterpret_cast<const void*>(kernel), dev, bytes);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = done.find(key);
+    if (it != done.end()) return it->second;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) done[key] = e;
+    return e;
 }
 
 static TraceDev trace_of(const mc_trace* t) {
@@ -1866,11 +1879,26 @@ static hipError_t launch_exchange(void (*k)(KA...), int64_t grid, int block, siz
 // workgroups of kernel k (block threads, lds bytes) the device holds at once
 template <typename K>
 static int64_t resident_capacity(K k, int block, size_t lds) {
+    // cached per (kernel, device, block, LDS): the occupancy query is a host
+    // call on every exchange launch otherwise
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, int, int, size_t>, int64_t> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto key = std::make_tuple(reinterpret_cast<const void*>(k), dev, block, lds);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(k), block,
                                                      lds) != hipSuccess)
         return -1;
-    return (int64_t)n * device_cus();
+    const int64_t cap = (int64_t)n * device_cus();
+    std::lock_guard<std::mutex> lk(mu);
+    cache[key] = cap;
+    return cap;
 }
 static int g_exchange_fault = 0;  // mc_debug_exchange_fault
 static bool sliced(const mc_program* p) { return p->sl.S >= 2 && p->sl.d_terms != nullptr; }
