@@ -12,7 +12,10 @@ which is launched in chunks of --iters-per-launch iterations (default 50).
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
 Warmup W = untimed warmup iterations of the sampler (the reference's step-size
-rule, Q4); K timed sampling iterations bracketed by barrier + synchronize;
+rule, Q4), preceded by --clock-warm-ms of untimed bf16 GEMMs that bring the
+GPU to its loaded clock (no sampler state is touched; measured: cold, the
+per-iteration time falls from 70 to 62 us over the first ~30 ms of sampler
+work); K timed sampling iterations bracketed by barrier + synchronize;
 value = sum over ranks of chain-leapfrog-steps / max-over-ranks wall time.
 The initial step size defaults to the one the reference's warmup rule reaches
 on this model after the SURVEY's W = 500 (mean over 256 chains,
@@ -78,6 +81,11 @@ def parse():
                     help="kernel of the sliced program (csrc/lanes.h or csrc/sliced.h)")
     ap.add_argument("--gather", action="store_true",
                     help="also gather every rank's samples to rank 0 over RCCL (untimed)")
+    ap.add_argument("--clock-warm-ms", type=float, default=500.0,
+                    help="untimed device work before the sampler warmup (bf16 GEMMs, no "
+                         "sampler state): the GPU raises its clock under sustained compute "
+                         "load over ~0.3 s, so a short run (the driver's --warmup 5) would "
+                         "otherwise time the sampler at the idle clock (~10 %% slower); 0: off")
     ap.add_argument("--workload", default="hmc", choices=["hmc", "nuts"],
                     help="hmc: the headline (BASELINE configs[2]/[3]); nuts: BASELINE "
                          "configs[4] (NUTS depth 10 + dual averaging, 100-dim kappa = 1000 "
@@ -225,6 +233,22 @@ def check(chains, where):
         sys.exit(3)
 
 
+def clock_warm(ms, dev):
+    """Keep the device busy for `ms` milliseconds with work unrelated to the
+    sampler (the GPU raises its clock under sustained load)."""
+    import torch
+
+    if ms <= 0:
+        return
+    a = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(10):
+            a = (a @ a).clamp_(-1.0, 1.0)
+        torch.cuda.synchronize()
+    del a
+
+
 def init_ranks():
     """One process per GPU (torchrun): RCCL over the node's GPUs.  With
     MC_DIST_BACKEND=gloo the ranks may share GPUs (rank r on GPU r % count): a
@@ -308,6 +332,7 @@ def main_nuts(args):
     def launches(first, count):
         return [(first + i, min(B, count - i)) for i in range(0, count, B)]
 
+    clock_warm(args.clock_warm_ms, dev)
     for it0, n in launches(0, Wm):
         chains.run_nuts(samples=samples, iter_begin=it0, iter_count=n, **cfg)
     torch.cuda.synchronize()
@@ -364,6 +389,7 @@ def main_nuts(args):
                 sc["n_total"], 1))),
             "accept_stat_mean": float(np.mean(sc["alpha_sum"]) / max(Wm + K, 1)),
             "step_size": float(np.mean(sc["step_size"])),
+            "clock_warm_ms": args.clock_warm_ms,
         }
         if world == 1 and not args.no_cpu_baseline:
             cb = nuts_cpu_baseline(min(args.cpu_seconds, 15.0))
@@ -413,6 +439,7 @@ def main():
     def launches(first, count):
         return [(first + i, min(B, count - i)) for i in range(0, count, B)]
 
+    clock_warm(args.clock_warm_ms, dev)
     # ---- untimed warmup (step-size adaptation) -------------------------------
     for it0, n in launches(0, Wm):
         chains.run_hmc(samples=samples, iter_begin=it0, iter_count=n, **cfg)
@@ -528,6 +555,7 @@ def main():
             # group index), times chain-steps/s; chains share it through LDS/L2
             "per_chain_streamed_gbs": 8.0 * N * value / 1e9,
         }
+        out["clock_warm_ms"] = args.clock_warm_ms
         if gather_ms is not None:
             out["gather_ms"] = gather_ms
         out["frozen_chains"] = frozen
