@@ -33,8 +33,13 @@ def main():
         wall = time.perf_counter() - t
         steps = 64 * 2000 * 10
         x = s["x"]
+        rate_s = 64 * 1000 * 10 / info.sampling_seconds
         out["config2_iso100_hmc" + label] = {
             "chains": 64,
+            # F = 16 D flops per chain-leapfrog-step (the direct Normal term
+            # 10 D, kicks and drift 6 D) against the FP32 vector peak; 64
+            # chains are 32 waves on 1024 SIMDs: latency-bound
+            "fp32_roofline_frac": rate_s * 16 * 100 / 157.3e12,
             "leapfrog_steps_per_s": steps / (info.warmup_seconds + info.sampling_seconds),
             "sampling_steps_per_s": 64 * 1000 * 10 / info.sampling_seconds,
             "wall_s": wall, "accept_rate": float(np.mean(rate)),

@@ -133,6 +133,16 @@ def test_hmc_trace_parity_simple(gpu):
                                   np.array(ref.trace["step_size"][:upto]))
     np.testing.assert_allclose(info.trace["accept_stat"][0][:upto],
                                np.array(ref.trace["ratio"][:upto]), rtol=1e-3, atol=2e-3)
+    # a divergence must be a proven near-tie (tests/_near_tie.py): |log U -
+    # ratio| within 8 ulp of |H|, ratios and H within that bound before it
+    from _near_tie import compare_trace, log_u
+
+    n = n_w + n_s
+    gpu_c = {"accepted": ga, "ratio": info.trace["accept_stat"][0],
+             "step_size": info.trace["step_size"][0], "energy": info.trace["energy"][0]}
+    ref_c = {k: np.asarray(ref.trace[k]) for k in ("accepted", "ratio", "step_size", "energy")}
+    ref_c["log_u"] = log_u(3, 0, n)
+    assert compare_trace(gpu_c, ref_c, "simple normal", verbose=True) == upto
 
 
 @pytest.mark.parametrize("kernel", ["auto", "tape"])
