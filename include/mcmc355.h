@@ -294,6 +294,10 @@ int mc_workspace_release(const void* workspace_dev);
  * chains of that block keep their state, mc_workspace_status then reports
  * MC_ERR_TIMEOUT and the next launch on the workspace starts clean.       */
 int mc_debug_exchange_fault(int on);
+/* Test hook: 0 runs the fast-form kernel k_hmc_lf with the term form read at
+ * run time (FORM = -1) instead of its compile-time instantiations; 1 restores
+ * the default.  Results agree up to fp32 summation order.                  */
+int mc_debug_lanes_forms(int on);
 /* After a sliced mc_hmc_run: MC_OK, or MC_ERR_TIMEOUT if an exchange timed
  * out (the launch then left its chains' state unchanged or partial).
  * Synchronises the stream.  Always MC_OK for an unsliced program.         */

@@ -2005,15 +2005,27 @@ static bool lanes_fast_enabled() {
     return on == 1;
 }
 
+// compile-time forms of k_hmc_lf: MC_LANES_FORM=0 in the environment or
+// mc_debug_lanes_forms(0) selects the run-time form kernel (A/B timing, tests)
+static int g_lanes_forms = -1;
+static bool lanes_forms_enabled() {
+    if (g_lanes_forms < 0) {
+        const char* e = std::getenv("MC_LANES_FORM");
+        g_lanes_forms = (e && e[0] == '0') ? 0 : 1;
+    }
+    return g_lanes_forms == 1;
+}
+extern "C" int mc_debug_lanes_forms(int on) {
+    g_lanes_forms = on ? 1 : 0;
+    return MC_OK;
+}
+
 template <int RS, int NSH, int NW, bool X1>
 static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* state,
                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
     const bool fast = p->lr.fast && lanes_fast_enabled();
     auto kern = fast ? k_hmc_lf<RS, NSH, NW, X1, -1> : k_hmc_lr<RS, NSH, NW, X1>;
-    static const bool forms = [] {  // MC_LANES_FORM=0: run-time forms only (A/B timing)
-        const char* e = std::getenv("MC_LANES_FORM");
-        return !(e && e[0] == '0');
-    }();
+    const bool forms = lanes_forms_enabled();
     if constexpr (NSH == 3) {  // the compile-time forms (one instantiation each)
         constexpr int HIER = LF_SW | LF_SWS | LF_DIR | LF_DM | LF_DS;
         if (fast && forms && p->lr.form == HIER) kern = k_hmc_lf<RS, lf_nroles(HIER), NW, X1, HIER>;

@@ -48,10 +48,24 @@ def _fixture():
     return out
 
 
-@pytest.mark.parametrize("kernel", ["lanes", "interpreter", "unsliced"])
+@pytest.mark.parametrize("kernel", ["lanes", "lanes_runtime_form", "interpreter", "unsliced"])
 def test_large_hmc_trace_matches_oracle(gpu, kernel):
+    """lanes: k_hmc_lf with the compile-time hierarchical form (the bench
+    kernel); lanes_runtime_form: the same kernel reading the form at run time
+    (mc_debug_lanes_forms(0))."""
     import mlx_mcmc_amd as m
+    from mlx_mcmc_amd import _lib
 
+    if kernel == "lanes_runtime_form":
+        _lib.load().mc_debug_lanes_forms(0)
+        try:
+            return _large_trace(m, "lanes")
+        finally:
+            _lib.load().mc_debug_lanes_forms(1)
+    _large_trace(m, kernel)
+
+
+def _large_trace(m, kernel):
     fx = _fixture()
     cfg = fx["config"]
     lp, init = W.hierarchical(W.ns_product(), *W.SHAPES["large"])
