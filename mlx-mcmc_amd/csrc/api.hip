@@ -2358,6 +2358,17 @@ extern "C" int32_t mc_program_nuts_lanes(const mc_program* p, int32_t max_tree_d
     return use_nuts_lanes(p, max_tree_depth) ? 1 : 0;
 }
 
+// every slice term of the one-slice lane plan has a specialised form and
+// every scalar term is an own prior (k_nuts_lr<..., SPEC>)
+static bool lanes_specialised(const mc_program* p) {
+    const LanePlan& L = p->lr;
+    if (L.n_generic != 0 || L.S != 1) return false;
+    const int nact = (int)L.blocks[2];
+    for (int t = 0; t < nact; ++t)
+        if (L.terms[t].sig == LS_GENERIC) return false;
+    return true;
+}
+
 template <int RS, int NSH>
 static int launch_nuts_lr(const mc_program* p, const mc_run_config* cfg, void* state,
                           float* samples, const mc_trace* tr, hipStream_t st) {
@@ -2368,10 +2379,11 @@ static int launch_nuts_lr(const mc_program* p, const mc_run_config* cfg, void* s
     std::memset(&A, 0, sizeof(A));
     A.cfg = *cfg;
     const size_t lds = nuts_lr_lds_bytes(p, cfg->max_tree_depth);
-    MC_HIP_TRY(allow_lds(k_nuts_lr<RS, NSH>, lds));
-    hipLaunchKernelGGL((k_nuts_lr<RS, NSH>), dim3((unsigned)cfg->num_chains), dim3(64), lds, st,
-                       lrctx_of(p), A, (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go),
-                       samples, trace_of(tr));
+    auto kern = lanes_specialised(p) ? k_nuts_lr<RS, NSH, true> : k_nuts_lr<RS, NSH, false>;
+    MC_HIP_TRY(allow_lds(kern, lds));
+    hipLaunchKernelGGL(kern, dim3((unsigned)cfg->num_chains), dim3(64), lds, st, lrctx_of(p), A,
+                       (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples,
+                       trace_of(tr));
     MC_HIP_TRY(hipGetLastError());
     return MC_OK;
 }

@@ -35,7 +35,11 @@ __host__ __device__ constexpr int64_t nuts_lr_arena_floats(int rs, int max_depth
     return (2 * (int64_t)(max_depth + 1) + 2 * (int64_t)(max_depth + 2)) * (rs + 1) * 64;
 }
 
-template <int RS, int NSH>
+// SPEC: every slice term has a specialised form (no LS_GENERIC term) and
+// every scalar term is an own prior (the planner checks it): the generic
+// per-element and scalar-term paths are compiled out, and with them their
+// register demand (inlined, it spills the tree walk's state).
+template <int RS, int NSH, bool SPEC>
 __global__ void __launch_bounds__(64)
 k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, float* samples,
           TraceDev tr) {
@@ -105,26 +109,44 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
 #pragma unroll
     for (int k = 1; k < kLrMaxShared; ++k) xg = (xk == k) ? P.shl[k] : xg;
 
-    // current sample (q, grad), both halves
-    f2 Cq[RS], Cg[RS];
+    // current sample (q, grad): one chain, no packed duplicate (registers)
+    float Cq[RS], Cg[RS];
 #pragma unroll
     for (int r = 0; r < RS; ++r) {
-        const float q = gk[r] >= 0 ? st_q[c * D + gk[r]] : 0.0f;
-        const float g = gk[r] >= 0 ? st_g[c * D + gk[r]] : 0.0f;
-        Cq[r] = (f2){q, q};
-        Cg[r] = (f2){g, g};
+        Cq[r] = gk[r] >= 0 ? st_q[c * D + gk[r]] : 0.0f;
+        Cg[r] = gk[r] >= 0 ? st_g[c * D + gk[r]] : 0.0f;
     }
     float Cqs = xon ? st_q[c * D + xg] : 1.0f, Cgs = xon ? st_g[c * D + xg] : 0.0f;
 
     // the log density and gradient at (R.q, sh.q): R.g, sh.g; returns log p
     LrPriv<RS> R;
     LrShared sh;
+    // an end (one chain) into / from the working registers (both packed halves)
+    auto load_end = [&](const auto& E) {
+#pragma unroll
+        for (int r = 0; r < RS; ++r)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                R.q[r][h] = E.q[r];
+                R.p[r][h] = E.p[r];
+                R.g[r][h] = E.g[r];
+            }
+    };
+    auto store_end = [&](auto& E) {
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            E.q[r] = R.q[r][0];
+            E.p[r] = R.p[r][0];
+            E.g[r] = R.g[r][0];
+        }
+    };
     auto derive = [&]() {
         sh.is = 1.0f / sh.q;
         sh.iv = 1.0f / (sh.q * sh.q);
         sh.lg = logf(sh.q);
     };
     auto evaluate = [&]() -> float {
+        MC_STAMP_DECL
         float gshp[kLrMaxShared][2];
 #pragma unroll
         for (int k = 0; k < kLrMaxShared; ++k) gshp[k][0] = gshp[k][1] = 0.0f;
@@ -135,12 +157,45 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         f2 lpp2 = {0.f, 0.f};
         lr_finish<RS>(tt, nsweep, ndirect, R, sh, M, KC, lpp2, gshp);
         float lpp[2] = {lpp2[0], lpp2[1]};
-        lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp);
+        MC_STAMP(2);
+        if constexpr (SPEC) {
+            for (int t = nfast; t < nact; ++t) {
+                const MC_CONST LrTerm* T = tt + t;
+                switch (T->sig) {
+                    case LS_DSCALE: lr_dscale_term<RS>(T, sd, j, R, sh, lpp, gshp); break;
+                    case LS_DATA_PP_SH:
+                        lr_normal_term<RS, SK_DATA, SK_PP, SK_SHARED>(T, sd, j, R, sh, lpp, gshp);
+                        break;
+                    case LS_DATA_PP_C:
+                        lr_normal_term<RS, SK_DATA, SK_PP, SK_CONST>(T, sd, j, R, sh, lpp, gshp);
+                        break;
+                    case LS_PP_SH_SH:
+                        lr_normal_term<RS, SK_PP, SK_SHARED, SK_SHARED>(T, sd, j, R, sh, lpp, gshp);
+                        break;
+                    case LS_PP_C_C:
+                        lr_normal_term<RS, SK_PP, SK_CONST, SK_CONST>(T, sd, j, R, sh, lpp, gshp);
+                        break;
+                    case LS_PP_DATA_SH:
+                        lr_normal_term<RS, SK_PP, SK_DATA, SK_SHARED>(T, sd, j, R, sh, lpp, gshp);
+                        break;
+                    default:
+                        lr_normal_term<RS, SK_DATA, SK_SHARED, SK_SHARED>(T, sd, j, R, sh, lpp, gshp);
+                        break;
+                }
+            }
+        } else {
+            lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp);
+        }
+        MC_STAMP(3);
         float slp[2] = {0.f, 0.f}, sg_self = 0.0f;
-        lr_scalar_terms(P.n_sterms, P.n_sterms_generic, sst, own, sh, j, Dsh, slp, sg_self);
+        lr_scalar_terms(P.n_sterms, SPEC ? 0 : P.n_sterms_generic, sst, own, sh, j, Dsh, slp,
+                        sg_self);
+        MC_STAMP(18);
         if (Dsh == 0) {  // no shared cotangents: one reduction
             sh.g = 0.0f;
-            return (wave_sum(lpp[0]) + slp[0]) + P.lp_const;
+            const float r = (wave_sum(lpp[0]) + slp[0]) + P.lp_const;
+            MC_STAMP(19);
+            return r;
         }
         float v8[8], t8[8];
         v8[0] = lpp[0];
@@ -208,17 +263,18 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
             return (gi & 1) ? z1 : z0;
         };
         // both ends start at the current sample with the drawn momentum
-        LrPriv<RS> EM, EP;
+        // the trajectory ends, one chain each (the working registers R carry
+        // the packed duplicate)
+        struct End {
+            float q[RS], p[RS], g[RS];
+        } EM, EP;
         float Mqs, Mrs, Mgs, Pqs, Prs, Pgs;
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             const float z = gk[r] >= 0 ? normal_of(gk[r]) : 0.0f;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                EM.q[r][h] = EP.q[r][h] = Cq[r][h];
-                EM.g[r][h] = EP.g[r][h] = Cg[r][h];
-                EM.p[r][h] = EP.p[r][h] = z;
-            }
+            EM.q[r] = EP.q[r] = Cq[r];
+            EM.g[r] = EP.g[r] = Cg[r];
+            EM.p[r] = EP.p[r] = z;
         }
         {
             const float z = xon ? normal_of(xg) : 0.0f;
@@ -230,7 +286,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         {
             float k = 0.0f;
 #pragma unroll
-            for (int r = 0; r < RS; ++r) k += EM.p[r][0] * EM.p[r][0];
+            for (int r = 0; r < RS; ++r) k += EM.p[r] * EM.p[r];
             if (xone) k += Mrs * Mrs;
             K0 = wave_sum(k);
         }
@@ -288,12 +344,12 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
             const float e = (float)ve;
             // the end this subtree extends: into the working registers
             if (v > 0) {
-                R = EP;
+                load_end(EP);
                 sh.q = Pqs;
                 sh.p = Prs;
                 sh.g = Pgs;
             } else {
-                R = EM;
+                load_end(EM);
                 sh.q = Mqs;
                 sh.p = Mrs;
                 sh.g = Mgs;
@@ -422,12 +478,12 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
             }
             // the working registers back into the end they extended
             if (v > 0) {
-                EP = R;
+                store_end(EP);
                 Pqs = sh.q;
                 Prs = sh.p;
                 Pgs = sh.g;
             } else {
-                EM = R;
+                store_end(EM);
                 Mqs = sh.q;
                 Mrs = sh.p;
                 Mgs = sh.g;
@@ -442,8 +498,8 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
 #pragma unroll
                     for (int r = 0; r < RS; ++r) {
                         const float q = *at(1, cand, 0, r), g = *at(1, cand, 1, r);
-                        Cq[r] = (f2){q, q};
-                        Cg[r] = (f2){g, g};
+                        Cq[r] = q;
+                        Cg[r] = g;
                     }
                     Cqs = *at(1, cand, 0, RS);
                     Cgs = *at(1, cand, 1, RS);
@@ -455,10 +511,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                 float mq[RS + 1], pq[RS + 1], mr[RS + 1], pr[RS + 1];
 #pragma unroll
                 for (int r = 0; r < RS; ++r) {
-                    mq[r] = EM.q[r][0];
-                    pq[r] = EP.q[r][0];
-                    mr[r] = EM.p[r][0];
-                    pr[r] = EP.p[r][0];
+                    mq[r] = EM.q[r];
+                    pq[r] = EP.q[r];
+                    mr[r] = EM.p[r];
+                    pr[r] = EP.p[r];
                 }
                 mq[RS] = Mqs;
                 pq[RS] = Pqs;
@@ -498,7 +554,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                 float* out = samples + (c * cfg.sample_capacity + si) * (int64_t)D;
 #pragma unroll
                 for (int r = 0; r < RS; ++r)
-                    if (gk[r] >= 0) out[gk[r]] = Cq[r][0];
+                    if (gk[r] >= 0) out[gk[r]] = Cq[r];
                 if (xone) out[xg] = Cqs;
             }
         }
@@ -521,8 +577,8 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
 #pragma unroll
     for (int r = 0; r < RS; ++r) {
         if (gk[r] >= 0) {
-            st_q[c * D + gk[r]] = Cq[r][0];
-            st_g[c * D + gk[r]] = Cg[r][0];
+            st_q[c * D + gk[r]] = Cq[r];
+            st_g[c * D + gk[r]] = Cg[r];
         }
     }
     if (xone) {
