@@ -97,6 +97,54 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                 KC.pd[t][r] = ((const int32_t*)sd)[tt[nsweep + t].len_off + r * 64 + j] > 0;
         }
 
+    // a data-scale term with at most one element per (lane, slot) (theta_i ~
+    // N(m, s_i), config 5): its per-slot constants in registers, read once per
+    // launch (lr_dscale_term's arithmetic, no LDS or constant loads per leaf)
+    int ddt = -1;
+    float dd_iv[RS], dd_ls[RS], dd_o[RS];
+    bool dd_on[RS];
+    int dd_ppo = 0, dd_ko = SK_CONST, dd_jo = 0;
+    float dd_w = 0.f, dd_c0 = 0.f, dd_cv = 0.f;
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+        dd_iv[r] = dd_ls[r] = dd_o[r] = 0.0f;
+        dd_on[r] = false;
+    }
+    if constexpr (SPEC) {
+        for (int t = nfast; t < nact; ++t)
+            if (tt[t].sig == LS_DSCALE) ddt = (ddt == -1) ? t : -2;
+        if (ddt >= 0) {
+            const MC_CONST LrTerm* T = tt + ddt;
+            const int32_t* lens = (const int32_t*)sd + T->len_off;
+            bool one = true;
+#pragma unroll
+            for (int r = 0; r < RS; ++r) {
+                const int len = r < T->nslot ? lens[r * 64 + j] : 0;
+                one = one && len <= 1;
+                dd_on[r] = len == 1;
+            }
+            if (__ballot(!one) != 0) {
+                ddt = -1;
+            } else {
+                dd_ppo = T->pp;
+                const int oth = 1 - dd_ppo;
+                dd_ko = T->kind[oth];
+                dd_jo = T->jsh[oth];
+                dd_w = T->weight;
+                dd_c0 = T->c0;
+                dd_cv = T->cval[oth];
+#pragma unroll
+                for (int r = 0; r < RS; ++r) {
+                    if (!dd_on[r]) continue;
+                    const int toff = T->toff[r] + 4 * j;
+                    dd_ls[r] = sd[T->doff[dd_ppo] + toff];
+                    dd_iv[r] = sd[T->doff[2] + toff];
+                    dd_o[r] = dd_ko == SK_DATA ? sd[T->doff[oth] + toff] : 0.0f;
+                }
+            }
+        }
+    }
+
     // this lane's parameters: private slots gk[r]; shared k = j / 2 (both
     // lanes 2k, 2k + 1 hold it: the two packed halves are the same chain)
     int gk[RS];
@@ -160,6 +208,35 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         MC_STAMP(2);
         if constexpr (SPEC) {
             for (int t = nfast; t < nact; ++t) {
+                if (t == ddt) {  // the register-resident data-scale term
+                    const f2 w = f2s(dd_w), c0 = f2s(dd_c0), half = f2s(0.5f);
+                    const f2 uo = dd_ko == SK_SHARED
+                                      ? (f2){rl(sh.q, 2 * dd_jo), rl(sh.q, 2 * dd_jo + 1)}
+                                      : f2s(dd_cv);
+                    f2 lpd = {0.f, 0.f}, po = {0.f, 0.f};
+#pragma unroll
+                    for (int r = 0; r < RS; ++r) {
+                        if (!dd_on[r]) continue;
+                        const f2 th = {R.q[r][0], R.q[r][1]};
+                        const f2 other = dd_ko == SK_DATA ? f2s(dd_o[r]) : uo;
+                        const f2 d = dd_ppo == 0 ? th - other : other - th;
+                        const f2 iv = f2s(dd_iv[r]);
+                        const f2 lpt = (c0 - f2s(dd_ls[r])) - (half * (d * d)) * iv;
+                        lpd += w * lpt;
+                        const f2 tt2 = w * (d * iv);
+                        const f2 gp = (f2){0.f, 0.f} + (dd_ppo == 0 ? -tt2 : tt2);
+                        po += dd_ppo == 0 ? tt2 : -tt2;
+                        R.g[r][0] += gp[0];
+                        R.g[r][1] += gp[1];
+                    }
+                    lpp[0] += lpd[0];
+                    lpp[1] += lpd[1];
+                    if (dd_ko == SK_SHARED) {
+                        add4(gshp, dd_jo, 0, po[0]);
+                        add4(gshp, dd_jo, 1, po[1]);
+                    }
+                    continue;
+                }
                 const MC_CONST LrTerm* T = tt + t;
                 switch (T->sig) {
                     case LS_DSCALE: lr_dscale_term<RS>(T, sd, j, R, sh, lpp, gshp); break;
