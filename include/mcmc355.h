@@ -182,6 +182,13 @@ int32_t mc_program_slice_kernel(const mc_program* prog);
  * broadcast parameter; MC_LANES_FAST=0 in the environment turns it off),
  * 0 when it runs k_hmc_lr or no lane-resident kernel, -1 on a null program. */
 int32_t mc_program_lanes_fast(const mc_program* prog);
+/* Why the program's HMC launches do not run the lane-resident kernel (e.g.
+ * "lane-resident kernel: more than 4 broadcast parameters"), or "" when they
+ * do or no plan was attempted; valid until the next set_slices /
+ * set_slice_kernel / destroy.  The chain-per-workgroup and interpreter
+ * kernels are 2-4x slower on programs the automatic plan would slice: the
+ * Python driver turns a non-empty note on such a program into a warning. */
+const char* mc_program_kernel_note(const mc_program* prog);
 /* 1 when mc_nuts_run with this max_tree_depth runs the lane-resident NUTS
  * kernel k_nuts_lr (a program planned as one lane-resident slice; its arena
  * fits LDS; MC_NUTS_LANES=0 in the environment turns it off), 0 when it runs

@@ -161,6 +161,7 @@ SIGNATURES = [
     ("mc_program_set_slice_kernel", ctypes.c_int, [_VP, ctypes.c_int32]),
     ("mc_program_slice_kernel", ctypes.c_int32, [_VP]),
     ("mc_program_lanes_fast", ctypes.c_int32, [_VP]),
+    ("mc_program_kernel_note", ctypes.c_char_p, [_VP]),
     ("mc_program_nuts_lanes", ctypes.c_int32, [_VP, ctypes.c_int32]),
     ("mc_logp_grad", ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP, _VP, _VP]),
     ("mc_dist_log_prob", ctypes.c_int,

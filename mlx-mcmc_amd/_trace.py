@@ -677,6 +677,16 @@ class Program:
         return "lanes" if k == 1 else "tape"
 
     @property
+    def kernel_note(self) -> str:
+        """Why HMC launches miss the lane-resident kernel ("" when they run it)."""
+        return (_lib.load().mc_program_kernel_note(self.handle) or b"").decode()
+
+    @property
+    def program_elements(self) -> int:
+        """Element count over the traced terms (the slice planner's size measure)."""
+        return int(sum(t.n for t in self.model.terms))
+
+    @property
     def lanes_fast(self) -> bool:
         """True when a lane-resident launch runs the fast-form kernel k_hmc_lf."""
         return _lib.load().mc_program_lanes_fast(self.handle) == 1

@@ -117,6 +117,9 @@ struct mc_program {
     SlicePlan sl;
     LanePlan lr;
     int32_t slice_kernel = 0;  // 0 automatic, 1 term interpreter, 2 lane-resident
+    // why the automatic plan did not reach the lane-resident kernel ("" when it
+    // did or was not asked to): mc_program_kernel_note
+    std::string note;
 };
 
 static DevCtx ctx_of(const mc_program* p) {
@@ -1092,13 +1095,18 @@ static int plan_lanes1(mc_program* p) {
     SlicePlan P;
     SlPartition part;
     const int rc = plan_slices(p, 1, P, &part);
-    if (rc != MC_OK) return rc;
+    if (rc != MC_OK) {
+        p->note = "lane-resident kernel: " + g_last_error;
+        return rc;
+    }
     if (plan_lanes(p, P, part, p->lr) != MC_OK) {
         const std::string why = p->lr.why;
         free_lanes(p->lr);
         p->lr.why = why;
+        p->note = "lane-resident kernel: " + why;
         return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: %s", why.c_str());
     }
+    p->note.clear();
     const hipError_t e = upload_lanes(p->lr);
     if (e != hipSuccess) {
         free_lanes(p->lr);
@@ -1115,6 +1123,7 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
     if (automatic) S = auto_slices(p);
     free_slices(p->sl);
     free_lanes(p->lr);
+    p->note.clear();
     if (S <= 1) {
         // automatic: the lane-resident kernel with one slice when the program
         // qualifies (1.4-4.5x k_hmc on D = 2..100 models at 64-1024 chains,
@@ -1138,7 +1147,9 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
     }
     if (rc != MC_OK) {
         free_slices(p->sl);
-        return automatic ? MC_OK : rc;  // automatic: stay on the unsliced kernels
+        if (!automatic) return rc;
+        p->note = "data slicing: " + g_last_error;
+        return MC_OK;  // automatic: stay on the unsliced kernels
     }
     SlicePlan& Q = p->sl;
     hipError_t e = upload(&Q.d_terms, Q.terms);
@@ -1166,6 +1177,7 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
         const std::string why = LP.why;
         free_lanes(LP);
         LP.why = why;
+        p->note = "lane-resident kernel: " + why;
         if (automatic && program_elements(p) < 16384) {  // only worth it on the lanes kernel
             free_slices(p->sl);
             if (p->slice_kernel != 1) (void)plan_lanes1(p);
@@ -1211,6 +1223,11 @@ extern "C" int32_t mc_program_lanes_fast(const mc_program* p) {
 }
 
 extern "C" int32_t mc_program_num_slices(const mc_program* p) { return p ? p->sl.S : -1; }
+
+extern "C" const char* mc_program_kernel_note(const mc_program* p) {
+    if (!p) return "";
+    return (mc_program_slice_kernel(p) == 2) ? "" : p->note.c_str();
+}
 
 extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t n_params,
                                  float lp_const, const float* data, int64_t n_data,

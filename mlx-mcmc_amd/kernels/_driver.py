@@ -9,6 +9,7 @@ return types.
 from __future__ import annotations
 
 import time
+import warnings
 from dataclasses import dataclass, field
 from typing import Dict, Optional
 
@@ -39,6 +40,11 @@ class RunInfo:
     extra: Dict = field(default_factory=dict)
 
 
+# csrc/api.hip kLrAutoMinElements: the automatic plan slices programs of at
+# least this many elements (and the lane-resident kernel is what pays for it)
+_LANES_WARN_ELEMENTS = 2048
+
+
 def _chunks(begin: int, end: int, every: int):
     """Split [begin, end) at multiples of `every` counted from `begin`."""
     it = begin
@@ -66,6 +72,13 @@ def run_sampler(algorithm: str, log_prob_fn, initial_params, *, num_samples: int
     program = _trace.compile_model(log_prob_fn, initial_params, slices=num_slices,
                                    slice_kernel=slice_kernel)
     layout = program.layout
+    note = program.kernel_note
+    if (algorithm == "hmc" and note and num_slices == 0 and slice_kernel == "auto"
+            and program.program_elements >= _LANES_WARN_ELEMENTS):
+        # a layout the lane-resident kernel declines runs
+        # on a 2-4x slower kernel; say so instead of degrading silently
+        warnings.warn(f"{note}; running on the {program.slice_kernel} kernel", RuntimeWarning,
+                      stacklevel=3)
     C = int(num_chains)
     if C < 1:
         raise ValueError("num_chains must be >= 1")
@@ -174,6 +187,8 @@ def run_sampler(algorithm: str, log_prob_fn, initial_params, *, num_samples: int
         device_samples=flat if keep_on_device else None, layout=layout)
     info.extra["kernel"] = (program.nuts_kernel(max_tree_depth) if algorithm == "nuts"
                             else program.slice_kernel)
+    if note and algorithm == "hmc":
+        info.extra["kernel_note"] = note
     host = flat.cpu().numpy()
     per_name = layout.unflatten(host)  # name -> [C, S, *shape]
     if C == 1:
