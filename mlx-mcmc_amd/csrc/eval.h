@@ -168,6 +168,26 @@ MC_DEV float wave_sum(float x) {
     const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 48));
     return ((r0 + r1) + r2) + r3;
 }
+// Two wave_sums side by side (bit-identical to wave_sum of each): the two
+// DPP chains interleave, so a lone wave waits for one chain's latency.
+MC_DEV void wave_sum2(float (&x)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) x[i] += dpp_row<0xB1>(x[i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) x[i] += dpp_row<0x4E>(x[i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) x[i] += dpp_row<0x141>(x[i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) x[i] += dpp_row<0x140>(x[i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[i]), 0));
+        const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[i]), 16));
+        const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[i]), 32));
+        const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[i]), 48));
+        x[i] = ((r0 + r1) + r2) + r3;
+    }
+}
 
 // A chain group: WPC wavefronts that together own one chain.  With WPC == 1
 // several chains share a workgroup and never use the workgroup barrier.

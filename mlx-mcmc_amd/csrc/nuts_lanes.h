@@ -193,7 +193,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         sh.iv = 1.0f / (sh.q * sh.q);
         sh.lg = logf(sh.q);
     };
-    auto evaluate = [&]() -> float {
+    // lane_lp != nullptr and no shared parameter: the log p is left as this
+    // lane's partial in *lane_lp (the caller reduces it together with the
+    // kinetic energy); the return value is then the part added after the sum
+    auto evaluate = [&](float* lane_lp) -> float {
         MC_STAMP_DECL
         float gshp[kLrMaxShared][2];
 #pragma unroll
@@ -270,6 +273,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         MC_STAMP(18);
         if (Dsh == 0) {  // no shared cotangents: one reduction
             sh.g = 0.0f;
+            if (lane_lp != nullptr) {
+                *lane_lp = lpp[0];
+                return slp[0];
+            }
             const float r = (wave_sum(lpp[0]) + slp[0]) + P.lp_const;
             MC_STAMP(19);
             return r;
@@ -407,9 +414,9 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                 a += d * rm[r];
                 b += d * rp[r];
             }
-            const float dm = wave_sum(a);
-            const float dp = wave_sum(b);
-            return dm >= 0.0f && dp >= 0.0f;
+            float ab[2] = {a, b};
+            wave_sum2(ab);
+            return ab[0] >= 0.0f && ab[1] >= 0.0f;
         };
 
         while (s && jd < MAXJ) {
@@ -456,14 +463,37 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                 }
                 if (Dsh > 0) derive();
                 MC_STAMP(8);
-                const float lpl = evaluate();
-                MC_STAMP(9);
+                float lpl, Kl;
+                if (Dsh == 0) {
+                    // the private gradients are complete in their lanes: the
+                    // half kick and the kinetic partial need no reduction, so
+                    // log p and the kinetic energy are reduced side by side
+                    // (two independent DPP chains, the same trees as apart)
+                    float lane_lp;
+                    const float post = evaluate(&lane_lp);
+                    MC_STAMP(9);
+                    float k = 0.0f;
 #pragma unroll
-                for (int r = 0; r < RS; ++r)
+                    for (int r = 0; r < RS; ++r) {
 #pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) R.p[r][hh] = R.p[r][hh] + h * R.g[r][hh];
-                sh.p = sh.p + h * sh.g;
-                const float Hl = -lpl + 0.5f * kinetic();
+                        for (int hh = 0; hh < 2; ++hh) R.p[r][hh] = R.p[r][hh] + h * R.g[r][hh];
+                        k += R.p[r][0] * R.p[r][0];
+                    }
+                    float ws[2] = {lane_lp, k};
+                    wave_sum2(ws);
+                    lpl = (ws[0] + post) + P.lp_const;
+                    Kl = ws[1];
+                } else {
+                    lpl = evaluate(nullptr);
+                    MC_STAMP(9);
+#pragma unroll
+                    for (int r = 0; r < RS; ++r)
+#pragma unroll
+                        for (int hh = 0; hh < 2; ++hh) R.p[r][hh] = R.p[r][hh] + h * R.g[r][hh];
+                    sh.p = sh.p + h * sh.g;
+                    Kl = kinetic();
+                }
+                const float Hl = -lpl + 0.5f * Kl;
                 ++leaves;
                 const int n_leaf = (logu <= (double)(-Hl)) ? 1 : 0;
                 const bool s_leaf = logu < (double)(1000.0f - Hl);
