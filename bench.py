@@ -379,7 +379,9 @@ def main_nuts(args):
             "roofline": {
                 "bound": "valu_fp32", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
-                "kernel": ("k_nuts_lr (lane-resident, one chain per wave)"
+                "kernel": (("k_nuts_lr (lane-resident, one chain per wave, register-only "
+                            "variant)" if prog.nuts_register_only(10) else
+                            "k_nuts_lr (lane-resident, one chain per wave)")
                            if prog.nuts_kernel(10) == "lanes" else f"k_nuts<{prog.waves_per_chain}>"),
                 "launch_ms": launch_ms,
                 "iters_per_launch": B, "flops_per_leaf": NUTS_FLOPS_PER_LEAF,

@@ -191,9 +191,12 @@ int32_t mc_program_lanes_fast(const mc_program* prog);
 const char* mc_program_kernel_note(const mc_program* prog);
 /* 1 when mc_nuts_run with this max_tree_depth runs the lane-resident NUTS
  * kernel k_nuts_lr (a program planned as one lane-resident slice; its arena
- * fits LDS; MC_NUTS_LANES=0 in the environment turns it off), 0 when it runs
- * k_nuts, -1 on a null program.  Both take the reference's decisions; they
- * differ in fp32 summation order only.                                      */
+ * fits LDS; MC_NUTS_LANES=0 in the environment turns it off), 2 when it runs
+ * its register-only variant (no broadcast parameter, no scalar term, one
+ * Normal term with at most one element per parameter and a data or constant
+ * scale: the gradient from per-parameter registers), 0 when it runs k_nuts,
+ * -1 on a null program.  All take the reference's decisions; they differ in
+ * fp32 summation order only.                                                */
 int32_t mc_program_nuts_lanes(const mc_program* prog, int32_t max_tree_depth);
 
 /* Batched tape evaluation: for every point p, logp[p] = log density at

@@ -674,7 +674,11 @@ class Program:
     def nuts_kernel(self, max_tree_depth: int = 10) -> str:
         """"lanes" (k_nuts_lr) or "tape" (k_nuts): what mc_nuts_run will run."""
         k = _lib.load().mc_program_nuts_lanes(self.handle, int(max_tree_depth))
-        return "lanes" if k == 1 else "tape"
+        return "lanes" if k >= 1 else "tape"
+
+    def nuts_register_only(self, max_tree_depth: int = 10) -> bool:
+        """True when mc_nuts_run runs k_nuts_lr's register-only variant."""
+        return _lib.load().mc_program_nuts_lanes(self.handle, int(max_tree_depth)) == 2
 
     @property
     def kernel_note(self) -> str:

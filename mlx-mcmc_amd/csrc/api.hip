@@ -2370,9 +2370,26 @@ static bool use_nuts_lanes(const mc_program* p, int max_depth) {
     return nuts_lanes_enabled() && p->sl.S < 2 && p->lr.ok && p->lr.S == 1 &&
            p->slice_kernel != 1 && nuts_lr_lds_bytes(p, max_depth) <= (size_t)kSlLdsBudget;
 }
+// no broadcast parameter, no scalar term and one slice term with at most one
+// element per (lane, slot): a data-scale term or a direct term with constant
+// loc and scale (k_nuts_lr<..., 2>: the gradient from per-slot registers)
+static bool lanes_register_only(const mc_program* p) {
+    const LanePlan& L = p->lr;
+    if (!L.ok || L.S != 1 || L.Dsh != 0 || !L.sterms.empty() || L.blocks[2] != 1) return false;
+    const LrTerm& T = L.terms[0];
+    const bool ds = T.sig == LS_DSCALE && T.kind[1 - T.pp] != SK_SHARED;
+    const bool dir = T.sig == LS_PP_C_C && T.pp == 0;
+    if (!ds && !dir) return false;
+    const int32_t* lens = (const int32_t*)&L.data[(size_t)L.blocks[0] + T.len_off];
+    for (int i = 0; i < T.nslot * 64; ++i)
+        if (lens[i] > 1) return false;
+    return true;
+}
+
 extern "C" int32_t mc_program_nuts_lanes(const mc_program* p, int32_t max_tree_depth) {
     if (!p) return -1;
-    return use_nuts_lanes(p, max_tree_depth) ? 1 : 0;
+    if (!use_nuts_lanes(p, max_tree_depth)) return 0;
+    return lanes_register_only(p) ? 2 : 1;
 }
 
 // every slice term of the one-slice lane plan has a specialised form and
@@ -2396,7 +2413,9 @@ static int launch_nuts_lr(const mc_program* p, const mc_run_config* cfg, void* s
     std::memset(&A, 0, sizeof(A));
     A.cfg = *cfg;
     const size_t lds = nuts_lr_lds_bytes(p, cfg->max_tree_depth);
-    auto kern = lanes_specialised(p) ? k_nuts_lr<RS, NSH, true> : k_nuts_lr<RS, NSH, false>;
+    auto kern = lanes_specialised(p) ? k_nuts_lr<RS, NSH, 1> : k_nuts_lr<RS, NSH, 0>;
+    if constexpr (NSH == 3)
+        if (lanes_register_only(p)) kern = k_nuts_lr<RS, NSH, 2>;
     MC_HIP_TRY(allow_lds(kern, lds));
     hipLaunchKernelGGL(kern, dim3((unsigned)cfg->num_chains), dim3(64), lds, st, lrctx_of(p), A,
                        (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples,

@@ -35,11 +35,16 @@ __host__ __device__ constexpr int64_t nuts_lr_arena_floats(int rs, int max_depth
     return (2 * (int64_t)(max_depth + 1) + 2 * (int64_t)(max_depth + 2)) * (rs + 1) * 64;
 }
 
-// SPEC: every slice term has a specialised form (no LS_GENERIC term) and
+// SPEC 1: every slice term has a specialised form (no LS_GENERIC term) and
 // every scalar term is an own prior (the planner checks it): the generic
 // per-element and scalar-term paths are compiled out, and with them their
 // register demand (inlined, it spills the tree walk's state).
-template <int RS, int NSH, bool SPEC>
+// SPEC 2 (register-only programs, api.hip lanes_register_only): no broadcast
+// parameter, no scalar term and one slice term with at most one element per
+// (lane, slot) — a data-scale term (config 5's theta_i ~ N(0, s_i)) or a
+// direct term with constant loc and scale (theta_i ~ N(m, s)): the gradient
+// is that term's arithmetic on per-slot registers, nothing else is compiled.
+template <int RS, int NSH, int SPEC>
 __global__ void __launch_bounds__(64)
 k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, float* samples,
           TraceDev tr) {
@@ -49,7 +54,8 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
     const int j = threadIdx.x;  // lane
     const int64_t c = blockIdx.x;
     if (c >= cfg.num_chains) return;
-    const int D = P.D, Dsh = P.Dsh;
+    constexpr bool REG = SPEC == 2;
+    const int D = P.D, Dsh = REG ? 0 : P.Dsh;
     const int MAXJ = cfg.max_tree_depth;
 
     // ---- the one slice's block and the scalar terms into LDS --------------------
@@ -82,6 +88,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
     LrCounts<RS> KC;
 #pragma unroll
     for (int t = 0; t < kLrSweep; ++t)
+        if (!REG)
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             KC.cs[t][r] = 0.0f;
@@ -90,6 +97,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         }
 #pragma unroll
     for (int t = 0; t < kLrDirect; ++t)
+        if (!REG)
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             KC.pd[t][r] = false;
@@ -110,7 +118,29 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         dd_iv[r] = dd_ls[r] = dd_o[r] = 0.0f;
         dd_on[r] = false;
     }
-    if constexpr (SPEC) {
+    if constexpr (REG) {
+        // the one term: a data-scale term (1/s^2 and log s tiles) or a direct
+        // term with constant loc and scale (its reciprocals per slot)
+        const MC_CONST LrTerm* T = tt;
+        const int32_t* lens = (const int32_t*)sd + T->len_off;
+        const bool ds = T->sig == LS_DSCALE;
+        ddt = 0;
+        dd_ppo = ds ? T->pp : 0;
+        const int oth = 1 - dd_ppo;
+        dd_ko = T->kind[oth];
+        dd_w = T->weight;
+        dd_c0 = T->c0;
+        dd_cv = T->cval[oth];
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+            dd_on[r] = r < T->nslot && lens[r * 64 + j] == 1;
+            if (!dd_on[r]) continue;
+            const int toff = T->toff[r] + 4 * j;
+            dd_ls[r] = ds ? sd[T->doff[dd_ppo] + toff] : T->clogs;
+            dd_iv[r] = ds ? sd[T->doff[2] + toff] : T->cinv2;
+            dd_o[r] = dd_ko == SK_DATA ? sd[T->doff[oth] + toff] : 0.0f;
+        }
+    } else if constexpr (SPEC == 1) {
         for (int t = nfast; t < nact; ++t)
             if (tt[t].sig == LS_DSCALE) ddt = (ddt == -1) ? t : -2;
         if (ddt >= 0) {
@@ -203,17 +233,21 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         for (int k = 0; k < kLrMaxShared; ++k) gshp[k][0] = gshp[k][1] = 0.0f;
 #pragma unroll
         for (int r = 0; r < RS; ++r) R.g[r][0] = R.g[r][1] = 0.0f;
-        LrMoments<RS> M;
-        lr_sweep<RS>(tt, nsweep, sd, j, R, M);
         f2 lpp2 = {0.f, 0.f};
-        lr_finish<RS>(tt, nsweep, ndirect, R, sh, M, KC, lpp2, gshp);
+        if constexpr (!REG) {
+            LrMoments<RS> M;
+            lr_sweep<RS>(tt, nsweep, sd, j, R, M);
+            lr_finish<RS>(tt, nsweep, ndirect, R, sh, M, KC, lpp2, gshp);
+        }
         float lpp[2] = {lpp2[0], lpp2[1]};
         MC_STAMP(2);
-        if constexpr (SPEC) {
-            for (int t = nfast; t < nact; ++t) {
+        if constexpr (SPEC >= 1) {
+            // (REG: the one term, whichever list the planner put it in)
+            for (int t = REG ? 0 : nfast; t < (REG ? 1 : nact); ++t) {
                 if (t == ddt) {  // the register-resident data-scale term
                     const f2 w = f2s(dd_w), c0 = f2s(dd_c0), half = f2s(0.5f);
-                    const f2 uo = dd_ko == SK_SHARED
+                    const bool ko_sh = !REG && dd_ko == SK_SHARED;  // (REG: no shared)
+                    const f2 uo = ko_sh
                                       ? (f2){rl(sh.q, 2 * dd_jo), rl(sh.q, 2 * dd_jo + 1)}
                                       : f2s(dd_cv);
                     f2 lpd = {0.f, 0.f}, po = {0.f, 0.f};
@@ -234,12 +268,13 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     }
                     lpp[0] += lpd[0];
                     lpp[1] += lpd[1];
-                    if (dd_ko == SK_SHARED) {
+                    if (ko_sh) {
                         add4(gshp, dd_jo, 0, po[0]);
                         add4(gshp, dd_jo, 1, po[1]);
                     }
                     continue;
                 }
+                if constexpr (REG) continue;
                 const MC_CONST LrTerm* T = tt + t;
                 switch (T->sig) {
                     case LS_DSCALE: lr_dscale_term<RS>(T, sd, j, R, sh, lpp, gshp); break;
@@ -268,8 +303,9 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         }
         MC_STAMP(3);
         float slp[2] = {0.f, 0.f}, sg_self = 0.0f;
-        lr_scalar_terms(P.n_sterms, SPEC ? 0 : P.n_sterms_generic, sst, own, sh, j, Dsh, slp,
-                        sg_self);
+        if constexpr (!REG)
+            lr_scalar_terms(P.n_sterms, SPEC ? 0 : P.n_sterms_generic, sst, own, sh, j, Dsh, slp,
+                            sg_self);
         MC_STAMP(18);
         if (Dsh == 0) {  // no shared cotangents: one reduction
             sh.g = 0.0f;

@@ -271,3 +271,47 @@ def test_nuts_lanes_eight_schools(gpu):
             k += 1
         same.append(k)
     assert sorted(same)[2] >= 10, same
+
+
+def _measurement(ns, D=100):
+    """y_i ~ N(theta_i, s_i), one observation per parameter (no prior): a
+    data-scale term whose private operand is the loc and whose value is data."""
+    rng = np.random.default_rng(8)
+    s = (0.5 + rng.random(D)).astype(np.float32)
+    y = rng.normal(0.0, 2.0, D).astype(np.float32)
+
+    def log_prob(p):
+        return ns.sum(ns.Normal(p["theta"], s).log_prob(y))
+
+    return log_prob, {"theta": y.copy()}
+
+
+@pytest.mark.parametrize("model", ["iso", "illcond", "measurement"])
+def test_nuts_register_only_trees_match_oracle(gpu, model):
+    """k_nuts_lr's register-only variant (one Normal term, one element per
+    parameter, constant or data scale; api.hip lanes_register_only): identical
+    tree depths and leaf counts to the oracle for the first iterations, on a
+    direct term with constant loc / scale (iso), a data-scale term with the
+    value private (illcond, config 5) and with the loc private (measurement)."""
+    import mlx_mcmc_amd as m
+    from mlx_mcmc_amd import _trace
+
+    mk = {"iso": W.iso_normal, "illcond": W.illcond_normal, "measurement": _measurement}[model]
+    plp, pinit = mk(W.ns_product())
+    olp, oinit = mk(W.ns_oracle())
+    assert _trace.compile_model(plp, pinit).nuts_register_only(10)
+    n_w, n_s = 20, 10
+    _, _, info = m.nuts(plp, pinit, num_samples=n_s, num_warmup=n_w, key=m.random.key(13),
+                        progress=False, return_info=True, return_trace=True)
+    assert info.extra["kernel"] == "lanes"
+    ref = S.nuts(olp, oinit, num_samples=n_s, num_warmup=n_w, seed=13)
+    same = 0
+    for i in range(n_w + n_s):
+        if (info.trace["tree_depth"][0][i] != ref.trace["depth"][i]
+                or info.trace["n_leapfrog"][0][i] != ref.trace["leaves"][i]):
+            break
+        same += 1
+    assert same >= 10, f"trees diverged at iteration {same}"
+    assert max(ref.trace["depth"][:same]) >= 2   # real trees, not single leaves
+    np.testing.assert_allclose(info.trace["accept_stat"][0][:6],
+                               np.array(ref.trace["alpha"][:6]), rtol=1e-4, atol=1e-6)
