@@ -548,8 +548,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     *at(1, f, 0, r) = R.q[r][0];
                     *at(1, f, 1, r) = R.g[r][0];
                 }
-                *at(1, f, 0, RS) = sh.q;
-                *at(1, f, 1, RS) = sh.g;
+                if (Dsh > 0) {  // (no broadcast parameter: the shared slot is unused)
+                    *at(1, f, 0, RS) = sh.q;
+                    *at(1, f, 1, RS) = sh.g;
+                }
                 pool_lp = (j == f) ? lpl : pool_lp;
                 const bool opens = (jd >= 1) && ((k & 1) == 0);
                 if (opens) {
@@ -559,8 +561,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                         *at(0, fslot, 0, r) = R.q[r][0];
                         *at(0, fslot, 1, r) = R.p[r][0];
                     }
-                    *at(0, fslot, 0, RS) = sh.q;
-                    *at(0, fslot, 1, RS) = sh.p;
+                    if (Dsh > 0) {
+                        *at(0, fslot, 0, RS) = sh.q;
+                        *at(0, fslot, 1, RS) = sh.p;
+                    }
                 }
                 MC_STAMP(11);
                 if (!s_leaf) {
@@ -602,8 +606,9 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     float bq[RS + 1], br[RS + 1], eq[RS + 1], er[RS + 1];
 #pragma unroll
                     for (int r = 0; r <= RS; ++r) {
-                        bq[r] = *at(0, slot, 0, r);
-                        br[r] = *at(0, slot, 1, r);
+                        const bool in = r < RS || Dsh > 0;
+                        bq[r] = in ? *at(0, slot, 0, r) : 0.0f;
+                        br[r] = in ? *at(0, slot, 1, r) : 0.0f;
                         eq[r] = r < RS ? R.q[r][0] : sh.q;
                         er[r] = r < RS ? R.p[r][0] : sh.p;
                     }
@@ -644,8 +649,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                         Cq[r] = q;
                         Cg[r] = g;
                     }
-                    Cqs = *at(1, cand, 0, RS);
-                    Cgs = *at(1, cand, 1, RS);
+                    if (Dsh > 0) {
+                        Cqs = *at(1, cand, 0, RS);
+                        Cgs = *at(1, cand, 1, RS);
+                    }
                     lp = rl(pool_lp, cand);
                 }
             }
