@@ -86,6 +86,9 @@ def parse():
                          "sampler state): the GPU raises its clock under sustained compute "
                          "load over ~0.3 s, so a short run (the driver's --warmup 5) would "
                          "otherwise time the sampler at the idle clock (~10 %% slower); 0: off")
+    ap.add_argument("--clock-warm-kind", default="gemm", choices=["gemm", "sampler"],
+                    help="gemm: bf16 GEMMs; sampler: the sampler kernel on a throw-away chain "
+                         "set of the same program (its own state, seed and sample buffer)")
     ap.add_argument("--workload", default="hmc", choices=["hmc", "nuts"],
                     help="hmc: the headline (BASELINE configs[2]/[3]); nuts: BASELINE "
                          "configs[4] (NUTS depth 10 + dual averaging, 100-dim kappa = 1000 "
@@ -233,12 +236,20 @@ def check(chains, where):
         sys.exit(3)
 
 
-def clock_warm(ms, dev):
+def clock_warm(ms, dev, scratch=None):
     """Keep the device busy for `ms` milliseconds with work unrelated to the
-    sampler (the GPU raises its clock under sustained load)."""
+    measured chains (the GPU raises its clock under sustained load).
+    `scratch(n)` (kind "sampler"): n iterations of the same kernel on a
+    throw-away chain set; otherwise bf16 GEMMs."""
     import torch
 
     if ms <= 0:
+        return
+    if scratch is not None:
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < ms:
+            scratch(10)
+            torch.cuda.synchronize()
         return
     a = torch.randn(4096, 4096, device=dev, dtype=torch.bfloat16)
     t0 = time.perf_counter()
@@ -441,7 +452,19 @@ def main():
     def launches(first, count):
         return [(first + i, min(B, count - i)) for i in range(0, count, B)]
 
-    clock_warm(args.clock_warm_ms, dev)
+    scratch = None
+    if args.clock_warm_kind == "sampler":
+        tmp = _engine.ChainSet(prog, C, prog.layout.flatten(init), args.step_size, device=dev)
+        tmp_s = torch.empty((C, 10, D), dtype=torch.float32, device=dev)
+        tmp_cfg = dict(cfg, seed=args.seed + 7919, num_warmup=0, num_samples=10,
+                       sample_capacity=10)
+
+        def scratch(n):
+            tmp.run_hmc(samples=tmp_s, iter_begin=0, iter_count=n, **tmp_cfg)
+    clock_warm(args.clock_warm_ms, dev, scratch)
+    if scratch is not None:
+        check(tmp, "clock warm")
+        del tmp, tmp_s
     # ---- untimed warmup (step-size adaptation) -------------------------------
     for it0, n in launches(0, Wm):
         chains.run_hmc(samples=samples, iter_begin=it0, iter_count=n, **cfg)
