@@ -494,6 +494,7 @@ def main():
     full = [a.elapsed_time(b) for (a, b), (_, n) in zip(ev, timed) if n == B] or \
            [a.elapsed_time(b) / n for (a, b), (_, n) in zip(ev, timed)]
     launch_ms = float(np.mean(full)) if K else float("nan")
+    each_ms = [round(a.elapsed_time(b), 4) for a, b in ev]
     iters_per_launch = B if any(n == B for _, n in timed) else 1
     kern_ms = launch_ms / iters_per_launch
     elapsed = max_over_ranks(elapsed, device=dev)
@@ -565,6 +566,7 @@ def main():
                 "kernel": kernel_label(prog, C),
                 "kernel_ms": kern_ms,
                 "launch_ms": launch_ms,
+                "each_launch_ms": each_ms if len(each_ms) <= 25 else None,
                 "iters_per_launch": iters_per_launch,
                 "flops_per_launch": flops_per_launch,
                 "note": ("FP32 VALU bound (SURVEY 8d: no dense contraction, no MFMA; vector FP32 "
