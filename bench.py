@@ -327,7 +327,7 @@ def main_nuts(args):
     _ensure_pkg()
     import workloads as W
     from mlx_mcmc_amd import _engine, _trace
-    from mlx_mcmc_amd.distributed import max_over_ranks, shard
+    from mlx_mcmc_amd.distributed import max_over_ranks, shard, sum_over_ranks
 
     world, rank, local, dev = init_ranks()
     C, K, Wm, B = args.chains, args.steps, args.warmup, max(1, args.iters_per_launch)
@@ -371,7 +371,7 @@ def main_nuts(args):
     launch_ms = float(np.mean(full)) if K else float("nan")
     launch_ms_total = float(sum(a.elapsed_time(b) for a, b in ev))
     elapsed = max_over_ranks(elapsed, device=dev)
-    leaves_all = int(max_over_ranks(float(leaves), device=dev)) * world if world > 1 else leaves
+    leaves_all = int(sum_over_ranks(float(leaves), device=dev))   # every rank's chains
     if rank == 0:
         value = leaves_all / elapsed
         # per launch: the timed leaves spread over the launches by their time
@@ -398,7 +398,7 @@ def main_nuts(args):
                 "iters_per_launch": B, "flops_per_leaf": NUTS_FLOPS_PER_LEAF,
                 "note": (f"latency bound: {C} chains = {C * prog.waves_per_chain} waves on "
                          "1024 SIMDs; F = 19 D flops per leaf (SURVEY 8d unit: one leaf)")},
-            "leaves": leaves, "mean_tree_depth": float(np.mean(sc["depth_sum"] / np.maximum(
+            "leaves": leaves_all, "leaves_rank0": leaves, "mean_tree_depth": float(np.mean(sc["depth_sum"] / np.maximum(
                 sc["n_total"], 1))),
             "accept_stat_mean": float(np.mean(sc["alpha_sum"]) / max(Wm + K, 1)),
             "step_size": float(np.mean(sc["step_size"])),

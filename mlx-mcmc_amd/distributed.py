@@ -6,7 +6,7 @@ Independent chains shard embarrassingly: global chains
 is keyed by the *global* chain id, so the samples of a chain do not depend on
 how many GPUs run the job.  There is no exchange during sampling; the only
 collective is the final gather of the samples to rank 0 (``gather_to_root``),
-plus a max-reduction of wall times for reporting.  With the gloo backend (a
+plus a max-reduction of wall times and sums of per-rank counts for reporting.  With the gloo backend (a
 CPU rehearsal of the RCCL path, e.g. several ranks sharing one GPU) the
 collectives run on host copies.
 """
@@ -55,7 +55,7 @@ def gather_to_root(t, group=None) -> Optional[object]:
     return torch.cat([b[:c] for b, c in zip(bufs, counts)])
 
 
-def max_over_ranks(x: float, device=None, group=None) -> float:
+def _reduce_scalar(x: float, op, device=None, group=None) -> float:
     import torch
     import torch.distributed as dist
 
@@ -64,5 +64,18 @@ def max_over_ranks(x: float, device=None, group=None) -> float:
     if dist.get_backend(group) == "gloo":
         device = "cpu"
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    dist.all_reduce(t, op=op, group=group)
     return float(t.item())
+
+
+def max_over_ranks(x: float, device=None, group=None) -> float:
+    import torch.distributed as dist
+
+    return _reduce_scalar(x, dist.ReduceOp.MAX, device, group)
+
+
+def sum_over_ranks(x: float, device=None, group=None) -> float:
+    """Sum of a per-rank count (exact in f64 below 2**53)."""
+    import torch.distributed as dist
+
+    return _reduce_scalar(x, dist.ReduceOp.SUM, device, group)

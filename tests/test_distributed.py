@@ -13,7 +13,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from mlx_mcmc_amd.distributed import gather_to_root, max_over_ranks, shard
+from mlx_mcmc_amd.distributed import gather_to_root, max_over_ranks, shard, sum_over_ranks
 
 
 def test_shard_plan_covers_chains_in_order():
@@ -45,8 +45,9 @@ def _worker(rank, world, port, C, q):
         mine = _chains(off, cnt)
         allc = gather_to_root(mine)
         t = max_over_ranks(float(rank + 1))
+        n = sum_over_ranks(float(cnt))   # per-rank counts (NUTS leaves in bench.py)
         if rank == 0:
-            q.put((allc.numpy(), t))
+            q.put((allc.numpy(), t, n))
     finally:
         dist.destroy_process_group()
 
@@ -67,10 +68,11 @@ def test_two_rank_shards_match_single_process():
     procs = [ctx.Process(target=_worker, args=(r, world, port, C, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got, tmax = q.get(timeout=300)
+    got, tmax, nsum = q.get(timeout=300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     ref = _chains(0, C).numpy()
     np.testing.assert_array_equal(got, ref)
     assert tmax == 2.0
+    assert nsum == C

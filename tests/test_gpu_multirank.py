@@ -7,8 +7,8 @@ host copies).
   the chains; the samples gathered to rank 0 are bit-identical to one process
   running every chain (draws are keyed by the global chain id), for HMC on the
   lane-resident kernel and for NUTS.
-* bench.py under torchrun with two ranks prints one line whose value
-  aggregates both ranks (128 chains), with the diagnostics' all-reduce and the
+* bench.py under torchrun with two and eight ranks prints one line whose value
+  aggregates every rank (64 chains each), with the diagnostics' all-reduce and the
   sample gather exercised (the small hierarchical shape: one slice, so the two
   processes' kernels need no cross-workgroup co-residency on the shared GPU).
 """
@@ -92,18 +92,32 @@ def test_two_ranks_on_one_gpu_match_one_process(gpu, algo):
     np.testing.assert_array_equal(got, ref)
 
 
-def test_bench_two_ranks_gloo(gpu):
+@pytest.mark.parametrize("world,workload", [(2, "hmc"), (8, "hmc"), (2, "nuts")])
+def test_bench_ranks_gloo(gpu, world, workload):
+    """world 8: the rank arithmetic of BASELINE configs[3] (8 ranks, chains
+    sharded per rank) on one shared GPU, 64 chains per rank; nuts: the
+    configs[4] line's multi-rank path (leaves summed over ranks)."""
     env = dict(os.environ, MC_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
-           "--chains", "64", "--shape", "small", "--gather", "--no-cpu-baseline"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=150, env=env, cwd=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "20", "--warmup", "5",
+           "--chains", "64", "--no-cpu-baseline", "--clock-warm-ms", "0"]
+    cmd += ["--workload", "nuts"] if workload == "nuts" else ["--shape", "small", "--gather"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=170, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["config"]["total_chains"] == 128
-    assert out["value"] > 0 and "gather_ms" in out
-    assert out["value"] == pytest.approx(128 * 20 * 20 / (out["ms_per_step"] * 20 / 1e3),
-                                         rel=1e-6)
+    C = 64 * world
+    assert out["n_gpus"] == world and out["config"]["total_chains"] == C
+    assert out["value"] > 0
+    if workload == "nuts":
+        # leaves of every rank's chains over the max-over-ranks time
+        assert out["value"] == pytest.approx(out["leaves"] / (out["ms_per_step"] * 20 / 1e3),
+                                             rel=1e-6)
+        assert out["leaves"] >= C * 20
+    else:
+        assert "gather_ms" in out
+        assert out["value"] == pytest.approx(C * 20 * 20 / (out["ms_per_step"] * 20 / 1e3),
+                                             rel=1e-6)
