@@ -1865,17 +1865,21 @@ static int device_cus() {
 }
 // Exchange kernels (k_hmc_sl, k_hmc_lr with S >= 2) spin on records of the
 // other workgroups of their chain block, so every workgroup of a launch must
-// be resident at once.  They are launched cooperatively (the runtime checks
-// the grid against what the device can hold and runs it only when all of it
-// fits, also beside other work on the device) after an occupancy query of
-// the same kernel, block size and LDS: a launch that cannot be co-resident
-// fails fast with MC_ERR_UNSUPPORTED instead of spinning into MC_ERR_TIMEOUT.
-// MC_COOPERATIVE=0 in the environment selects plain launches (A/B timing).
+// be resident at once.  An occupancy query of the same kernel, block size and
+// LDS caps the grid at what the device holds: a launch that cannot be
+// co-resident fails fast with MC_ERR_UNSUPPORTED.  They are then launched
+// plainly: on a device shared with other work that keeps some of the grid
+// out, the spin times out and the launch reports MC_ERR_TIMEOUT with the
+// stranded block's state unchanged (mc_workspace_status).  MC_COOPERATIVE=1
+// in the environment selects cooperative launches (the runtime runs the grid
+// only when all of it fits, also beside other work), at ~50 us per launch on
+// MI355X (profiles/r2/v17_coop_ab.json: 1.25 vs 1.195 ms per 20-iteration
+// launch of the bench kernel).
 static bool coop_enabled() {
     static int on = -1;
     if (on < 0) {
         const char* e = std::getenv("MC_COOPERATIVE");
-        on = (e && e[0] == '0') ? 0 : 1;
+        on = (e && e[0] == '1') ? 1 : 0;
     }
     return on == 1;
 }
