@@ -12,10 +12,13 @@ which is launched in chunks of --iters-per-launch iterations (default 50).
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
 Warmup W = untimed warmup iterations of the sampler (the reference's step-size
-rule, Q4), preceded by --clock-warm-ms of untimed bf16 GEMMs that bring the
-GPU to its loaded clock (no sampler state is touched; measured: cold, the
-per-iteration time falls from 70 to 62 us over the first ~30 ms of sampler
-work); K timed sampling iterations bracketed by barrier + synchronize;
+rule, Q4), preceded by --clock-warm-ms of untimed device work (default
+--clock-warm-kind same: the sampler kernel on the measured chain set's own
+buffers and workspace, its state then restored bit-exactly, so the timed
+iterations compute exactly what they would without it; measured: cold, the
+per-iteration time falls from 70-74 to 60 us over the first ~30 ms of sampler
+work, profiles/r2/v17_clock_probe.json); K timed sampling iterations
+bracketed by barrier + synchronize;
 value = sum over ranks of chain-leapfrog-steps / max-over-ranks wall time.
 The initial step size defaults to the one the reference's warmup rule reaches
 on this model after the SURVEY's W = 500 (mean over 256 chains,
@@ -82,13 +85,15 @@ def parse():
     ap.add_argument("--gather", action="store_true",
                     help="also gather every rank's samples to rank 0 over RCCL (untimed)")
     ap.add_argument("--clock-warm-ms", type=float, default=500.0,
-                    help="untimed device work before the sampler warmup (bf16 GEMMs, no "
-                         "sampler state): the GPU raises its clock under sustained compute "
-                         "load over ~0.3 s, so a short run (the driver's --warmup 5) would "
-                         "otherwise time the sampler at the idle clock (~10 %% slower); 0: off")
-    ap.add_argument("--clock-warm-kind", default="gemm", choices=["gemm", "sampler"],
+                    help="untimed device work before the sampler warmup (--clock-warm-kind; "
+                         "the measured state is never changed by it): cold, the sampler's "
+                         "first ~30 ms run 15-20 %% slower, so a short run (the driver's "
+                         "--warmup 5) would otherwise time the cold kernel; 0: off")
+    ap.add_argument("--clock-warm-kind", default="same", choices=["gemm", "sampler", "same"],
                     help="gemm: bf16 GEMMs; sampler: the sampler kernel on a throw-away chain "
-                         "set of the same program (its own state, seed and sample buffer)")
+                         "set of the same program (its own state, seed and sample buffer); "
+                         "same: the sampler kernel on the measured chain set's buffers and "
+                         "workspace, its state restored bit-exactly afterwards")
     ap.add_argument("--workload", default="hmc", choices=["hmc", "nuts"],
                     help="hmc: the headline (BASELINE configs[2]/[3]); nuts: BASELINE "
                          "configs[4] (NUTS depth 10 + dual averaging, 100-dim kappa = 1000 "
@@ -453,8 +458,13 @@ def main():
         return [(first + i, min(B, count - i)) for i in range(0, count, B)]
 
     scratch = None
-    if args.clock_warm_kind == "sampler":
+    saved = None
+    if args.clock_warm_kind == "same":
+        saved = chains.state.clone()
+        tmp = chains
+    elif args.clock_warm_kind == "sampler":
         tmp = _engine.ChainSet(prog, C, prog.layout.flatten(init), args.step_size, device=dev)
+    if args.clock_warm_kind != "gemm":
         tmp_s = torch.empty((C, 10, D), dtype=torch.float32, device=dev)
         tmp_cfg = dict(cfg, seed=args.seed + 7919, num_warmup=0, num_samples=10,
                        sample_capacity=10)
@@ -465,6 +475,10 @@ def main():
     if scratch is not None:
         check(tmp, "clock warm")
         del tmp, tmp_s
+    if saved is not None:
+        chains.state.copy_(saved)   # the measured chains start from their initial state
+        torch.cuda.synchronize()
+        del saved
     # ---- untimed warmup (step-size adaptation) -------------------------------
     for it0, n in launches(0, Wm):
         chains.run_hmc(samples=samples, iter_begin=it0, iter_count=n, **cfg)
@@ -583,6 +597,7 @@ def main():
             "per_chain_streamed_gbs": 8.0 * N * value / 1e9,
         }
         out["clock_warm_ms"] = args.clock_warm_ms
+        out["clock_warm_kind"] = args.clock_warm_kind
         if gather_ms is not None:
             out["gather_ms"] = gather_ms
         out["frozen_chains"] = frozen
