@@ -133,6 +133,8 @@ int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t n_params,
                       const float* data, int64_t n_data,
                       const int32_t* index, int64_t n_index,
                       mc_program** out);
+/* mc_program_create ignores mc_term.affine (formerly reserved0); only
+ * mc_program_create_affine reads it, so zero-initialise it there.          */
 /* mc_program_create with affine loc operands (affines[0 .. n_affines)).    */
 int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
                              const mc_affine* affines, int32_t n_affines,

@@ -226,8 +226,11 @@ class Affine:
                     if _is_slope(b) and not _is_slope(a):  # the vector is x (slope 1)
                         a, b = b, a
                     if _is_slope(b):
-                        raise TraceError("a sum of two scalar parameters as a loc: "
-                                         + _UNSUPPORTED)
+                        if isinstance(a, Param) and isinstance(b, Param):
+                            raise TraceError("a sum of two scalar parameters as a loc: "
+                                             + _UNSUPPORTED)
+                        raise TraceError("a scalar parameter plus a constant is not traced as "
+                                         "a loc: " + _UNSUPPORTED)
                     return Affine(a, 1.0, b)  # (a + 1 * b rounds as a + b)
                 raise TraceError("a sum of two parameter terms besides the product: "
                                  + _UNSUPPORTED)

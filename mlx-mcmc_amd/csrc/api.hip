@@ -1232,8 +1232,13 @@ extern "C" const char* mc_program_kernel_note(const mc_program* p) {
 extern "C" int mc_program_create(const mc_term* terms, int32_t n_terms, int32_t n_params,
                                  float lp_const, const float* data, int64_t n_data,
                                  const int32_t* index, int64_t n_index, mc_program** out) {
-    return mc_program_create_affine(terms, n_terms, nullptr, 0, n_params, lp_const, data, n_data,
-                                    index, n_index, out);
+    // the non-affine entry point ignores mc_term.affine (it was reserved0
+    // before affine locs existed, and callers were free to leave it unset)
+    if (n_terms < 0 || (n_terms > 0 && !terms)) return fail(MC_ERR_INVALID, "terms");
+    std::vector<mc_term> t(terms, terms + n_terms);
+    for (mc_term& x : t) x.affine = 0;
+    return mc_program_create_affine(t.data(), n_terms, nullptr, 0, n_params, lp_const, data,
+                                    n_data, index, n_index, out);
 }
 
 extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
@@ -1642,19 +1647,22 @@ static bool hmc_use_lds(const mc_program* p) {
 template <typename K>
 static hipError_t allow_lds(K kernel, size_t bytes) {
     if (bytes <= 64 * 1024) return hipSuccess;
-    // once per (kernel, device, size): the attribute call costs host time on
-    // every launch otherwise (launch functions run once per chunk of iterations)
+    // the attribute is a per-(kernel, device) maximum: the largest value set so
+    // far is cached and a launch needing no more skips the call (it costs host
+    // time on every launch otherwise; launch functions run once per chunk of
+    // iterations).  A launch needing more raises it — never lowers it, so a
+    // later large launch of the same instantiation is never refused.
     static std::mutex mu;
-    static std::map<std::tuple<const void*, int, size_t>, hipError_t> done;
+    static std::map<std::pair<const void*, int>, size_t> max_set;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    const auto key = std::make_tuple(reinterpret_cast<const void*>(kernel), dev, bytes);
+    const auto key = std::make_pair(reinterpret_cast<const void*>(kernel), dev);
     std::lock_guard<std::mutex> lk(mu);
-    auto it = done.find(key);
-    if (it != done.end()) return it->second;
+    auto it = max_set.find(key);
+    if (it != max_set.end() && bytes <= it->second) return hipSuccess;
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    if (e == hipSuccess) done[key] = e;
+    if (e == hipSuccess) max_set[key] = bytes;
     return e;
 }
 

@@ -33,6 +33,8 @@ def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_si
     is the fraction of sampling iterations whose mean acceptance statistic
     exceeds 0.5 (nuts.py:347).
     """
+    if nuts_kernel not in ("auto", "tape"):
+        raise ValueError(f"nuts_kernel must be 'auto' or 'tape', not {nuts_kernel!r}")
     samples, rate, info = run_sampler(
         "nuts", log_prob_fn, initial_params, num_samples=num_samples, num_warmup=num_warmup,
         step_size=step_size, target_accept=target_accept, adapt_step_size=adapt_step_size,

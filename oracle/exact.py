@@ -1,0 +1,162 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY (never imported by mlx_mcmc_amd/).
+
+Float64 known answers for the posteriors of BASELINE.json's synthetic models
+(SURVEY 8d), so that "posterior moments within 1 %" (north_star) can be
+checked against an answer with no Monte-Carlo error of its own:
+
+  hierarchical_moments  workloads.hierarchical (configs[2]/[3], README
+        "Large" row and the small / medium shapes):
+            mu ~ N(0, 10), tau ~ HalfNormal(5), sigma ~ HalfNormal(5),
+            theta_g ~ N(mu, tau), y_i ~ N(theta_{g_i}, sigma)
+        (the log density of examples/02_hmc_comparison.py:40-52 with the
+        reference's Normal / HalfNormal, normal.py:28-31, halfnormal.py:55-63).
+        Given (tau, sigma) the model is linear-Gaussian in (mu, theta):
+        theta_g integrates out through the group sufficient statistics
+        n_g, ybar_g, SS_g (ybar_g | mu ~ N(mu, tau^2 + sigma^2/n_g)), then mu
+        against its Normal prior, leaving a 2-D marginal p(tau, sigma | y)
+        that is integrated on a tensor grid in (log tau, log sigma) around its
+        mode (+-10 Laplace standard deviations; the integrand is smooth and
+        decays like a Gaussian, so the equally spaced rule converges
+        geometrically — `quadrature_error` measures it by halving the grid).
+        Means and variances of mu and theta_g follow from the conditional
+        ones by the laws of total expectation and variance.
+  gaussian_moments  configs[1] (isotropic N(0, I)) and configs[4]
+        (N(0, diag(s^2)), s_i = 10^(-1.5 i / 99)): mean 0, variance s^2.
+
+The parameters are in the product's layout order (mu, tau, sigma,
+theta[0..G-1]) — the order of workloads.hierarchical's init dict.
+The data are the f32 values the samplers see (workloads.hierarchical_data),
+summed in f64.  The reference's own samplers target the same density, so a
+sampler that matches these moments matches the reference's posterior up to
+the reference's Monte-Carlo error; MLX itself cannot run here.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+PRIOR_MU_SD = 10.0      # Normal(0, 10) on mu
+PRIOR_HALF_SD = 5.0     # HalfNormal(5) on tau and sigma
+
+
+def group_stats(y, group, G):
+    """n_g, ybar_g, SS_g (within-group sum of squares) in f64."""
+    y = np.asarray(y, np.float32).astype(np.float64)
+    group = np.asarray(group, np.int64)
+    n = np.bincount(group, minlength=G).astype(np.float64)
+    if np.any(n == 0):
+        raise ValueError("every group needs an observation")
+    ybar = np.bincount(group, weights=y, minlength=G) / n
+    ss = np.bincount(group, weights=(y - ybar[group]) ** 2, minlength=G)
+    return n, ybar, ss
+
+
+class _Marginal:
+    """log p(tau, sigma | y) up to a constant and the conditional moments of
+    (mu, theta) given (tau, sigma)."""
+
+    def __init__(self, n, ybar, ss):
+        self.n, self.ybar, self.ss = n, ybar, ss
+        self.N = float(n.sum())
+        self.G = len(n)
+        self.ssw = float(ss.sum())
+
+    def logp(self, tau, sigma):
+        """tau, sigma: [A] arrays -> log density of (tau, sigma) [A]
+        (density w.r.t. d tau d sigma; constants dropped)."""
+        tau = np.asarray(tau, np.float64)[:, None]
+        sigma = np.asarray(sigma, np.float64)[:, None]
+        v = tau ** 2 + sigma ** 2 / self.n                    # Var(ybar_g | mu)
+        w = 1.0 / v
+        P = 1.0 / PRIOR_MU_SD ** 2 + w.sum(1)                 # posterior precision of mu
+        b = (w * self.ybar).sum(1)
+        quad = (w * self.ybar ** 2).sum(1) - b * b / P
+        tau, sigma = tau[:, 0], sigma[:, 0]
+        lp = -0.5 * np.log(v).sum(1) - 0.5 * np.log(P) - 0.5 * quad
+        lp += -(self.N - self.G) * np.log(sigma) - self.ssw / (2.0 * sigma ** 2)
+        lp += -tau ** 2 / (2 * PRIOR_HALF_SD ** 2) - sigma ** 2 / (2 * PRIOR_HALF_SD ** 2)
+        return lp
+
+    def conditional(self, tau, sigma):
+        """Given scalars (tau, sigma): E/Var of mu and of theta [G]."""
+        v = tau ** 2 + sigma ** 2 / self.n
+        w = 1.0 / v
+        P = 1.0 / PRIOR_MU_SD ** 2 + w.sum()
+        m = (w * self.ybar).sum() / P
+        s2 = 1.0 / (1.0 / tau ** 2 + self.n / sigma ** 2)     # Var(theta_g | mu, ...)
+        c = s2 / tau ** 2                                     # d E[theta_g | mu] / d mu
+        a = s2 * self.n * self.ybar / sigma ** 2
+        return m, 1.0 / P, a + c * m, s2 + c * c / P
+
+
+def _mode(M):
+    from scipy.optimize import minimize
+
+    def f(x):
+        t, s = np.exp(x)
+        return -(M.logp([t], [s])[0] + x[0] + x[1])           # log-coordinates' Jacobian
+
+    x0 = np.log([max(np.std(M.ybar), 1e-3), np.sqrt(max(M.ssw, 1e-12) / max(M.N - M.G, 1))])
+    r = minimize(f, x0, method="Nelder-Mead", options=dict(xatol=1e-10, fatol=1e-12,
+                                                           maxiter=4000))
+    x = r.x
+    h = 1e-4
+    H = np.zeros((2, 2))
+    for i in range(2):
+        for j in range(2):
+            ei, ej = np.eye(2)[i] * h, np.eye(2)[j] * h
+            H[i, j] = (f(x + ei + ej) - f(x + ei - ej) - f(x - ei + ej) + f(x - ei - ej)) / (4 * h * h)
+    cov = np.linalg.inv(H)
+    return x, np.sqrt(np.diag(cov))
+
+
+def hierarchical_moments(y, group, G, n_grid=161, width=10.0):
+    """Exact posterior means / variances in layout order (mu, tau, sigma,
+    theta[0..G-1]): returns dict(mean=[G+3], var=[G+3])."""
+    M = _Marginal(*group_stats(y, group, G))
+    x0, sd = _mode(M)
+    u = x0[0] + sd[0] * np.linspace(-width, width, n_grid)
+    v = x0[1] + sd[1] * np.linspace(-width, width, n_grid)
+    U, V = np.meshgrid(u, v, indexing="ij")
+    T, S = np.exp(U.ravel()), np.exp(V.ravel())
+    lw = np.concatenate([M.logp(T[i:i + 2048], S[i:i + 2048]) for i in range(0, T.size, 2048)])
+    lw += U.ravel() + V.ravel()                               # d tau d sigma = tau sigma du dv
+    w = np.exp(lw - lw.max())
+    w /= w.sum()
+    keep = np.nonzero(w > 1e-300)[0]
+    # first pass: means; second pass: variances about those means (no cancellation)
+    Em, Et = 0.0, np.zeros(G)
+    cond = []
+    for k in keep:
+        m, vm, et, vt = M.conditional(T[k], S[k])
+        cond.append((w[k], m, vm, et, vt))
+        Em += w[k] * m
+        Et += w[k] * et
+    Vm, Vt = 0.0, np.zeros(G)
+    for wk, m, vm, et, vt in cond:
+        Vm += wk * (vm + (m - Em) ** 2)
+        Vt += wk * (vt + (et - Et) ** 2)
+    Etau = float(np.sum(w * T))
+    Esig = float(np.sum(w * S))
+    Vtau = float(np.sum(w * (T - Etau) ** 2))
+    Vsig = float(np.sum(w * (S - Esig) ** 2))
+    mean = np.concatenate([[Em, Etau, Esig], Et])
+    var = np.concatenate([[Vm, Vtau, Vsig], Vt])
+    edge = max(w.reshape(n_grid, n_grid)[[0, -1], :].max(), w.reshape(n_grid, n_grid)[:, [0, -1]].max())
+    return {"mean": mean, "var": var, "mode_log_tau_sigma": x0.tolist(),
+            "laplace_sd_log_tau_sigma": sd.tolist(), "edge_weight": float(edge)}
+
+
+def quadrature_error(y, group, G, n_grid=161):
+    """Max relative change of every mean / variance when the grid spacing is
+    halved (n_grid -> 2 n_grid - 1 over the same box): the quadrature's
+    error bound."""
+    a = hierarchical_moments(y, group, G, n_grid)
+    b = hierarchical_moments(y, group, G, 2 * n_grid - 1)
+    sd = np.sqrt(b["var"])
+    return (float(np.max(np.abs(a["mean"] - b["mean"]) / np.maximum(np.abs(b["mean"]), sd))),
+            float(np.max(np.abs(a["var"] - b["var"]) / b["var"])))
+
+
+def gaussian_moments(scales):
+    s = np.asarray(scales, np.float32).astype(np.float64)
+    return {"mean": np.zeros_like(s), "var": s * s}

@@ -315,3 +315,18 @@ def test_nuts_register_only_trees_match_oracle(gpu, model):
     assert max(ref.trace["depth"][:same]) >= 2   # real trees, not single leaves
     np.testing.assert_allclose(info.trace["accept_stat"][0][:6],
                                np.array(ref.trace["alpha"][:6]), rtol=1e-4, atol=1e-6)
+
+
+def test_lds_attribute_large_small_large(gpu):
+    """one kernel instantiation launched with more, then less, then
+    more dynamic LDS (k_nuts<WPC, LDS>: the tree arena grows with
+    max_tree_depth) — the per-kernel LDS attribute is raised, never lowered,
+    so the third launch is not refused."""
+    import mlx_mcmc_amd as m
+
+    lp, init = W.hierarchical(W.ns_product(), *W.SHAPES["small"])
+    for depth in (10, 2, 10, 1, 10):
+        s, rate = m.nuts(lp, init, num_samples=2, num_warmup=2, step_size=0.01,
+                         max_tree_depth=depth, key=m.random.key(0), num_chains=8,
+                         progress=False, nuts_kernel="tape")
+        assert np.all(np.isfinite(s["mu"]))

@@ -177,3 +177,20 @@ def test_mcmc_method_errors():
             mc.run({"x": 0.0}, method="metropolis", verbose=False)
     with pytest.raises(ValueError):
         mc.summary()
+
+
+def test_scalar_param_plus_constant_loc_message():
+    """`mu + 1.0` as a loc names the real cause (a constant), not
+    'a sum of two scalar parameters'."""
+    y = W.simple_normal_data()
+
+    def shifted(p):
+        return mx.sum(m.Normal(p["mu"] + 1.0, 1.0).log_prob(mx.array(y)))
+
+    def two(p):
+        return mx.sum(m.Normal(p["mu"] + p["nu"], 1.0).log_prob(mx.array(y)))
+
+    with pytest.raises(_trace.TraceError, match="plus a constant"):
+        _trace.trace(shifted, {"mu": 0.0})
+    with pytest.raises(_trace.TraceError, match="two scalar parameters"):
+        _trace.trace(two, {"mu": 0.0, "nu": 0.0})
