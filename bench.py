@@ -74,6 +74,13 @@ def parse():
                          "processes with the GPU device open, which torch's import in each "
                          "worker counts as, this one included; 0: skip)")
     ap.add_argument("--no-ess", action="store_true")
+    ap.add_argument("--ess-draws", type=int, default=5000,
+                    help="draws of the converged-ESS run (N=1, untimed by the headline: fixed "
+                         "eps, R-hat checked); 0: skip")
+    ap.add_argument("--ess-warmup", type=int, default=1000)
+    ap.add_argument("--ess-step-size", type=float, default=None,
+                    help="fixed step size of the converged-ESS run (default: the posterior "
+                         "tests' value for the shape: large 2e-3, medium 5e-3, small 0.01)")
     ap.add_argument("--iters-per-launch", type=int, default=50,
                     help="HMC iterations per sampler launch (hmc() launches its persistent "
                          "kernel in chunks of 500, or once per phase without progress "
@@ -99,6 +106,8 @@ def parse():
                          "configs[4] (NUTS depth 10 + dual averaging, 100-dim kappa = 1000 "
                          "Gaussian, 64 chains per GPU; a measurement line, not the headline)")
     args = ap.parse_args()
+    if args.ess_step_size is None:
+        args.ess_step_size = {"large": 2e-3, "medium": 5e-3, "small": 0.01}[args.shape]
     if args.workload == "nuts" and not any(a.startswith("--chains") for a in sys.argv[1:]):
         args.chains = 64
     return args
@@ -227,6 +236,122 @@ def kernel_label(prog, C):
     if kind == "interpreter":
         return f"k_hmc_sl<{16 if C > 8 else 8}> (S={prog.num_slices} slices)"
     return f"k_hmc<{prog.waves_per_chain}>"
+
+
+def pmc_traffic(shape, iters_per_launch):
+    """HBM bytes per launch of `iters_per_launch` iterations from
+    profiles/pmc_traffic.json (scripts/pmc_traffic.py): records keyed
+    "<shape>@<iters per launch>", measured at that launch size (a launch has
+    fixed bytes — the slice blocks are loaded once per launch — so a record
+    of another size is not rescaled).  (None, reason) when absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        data = json.load(open(path))
+    except (OSError, ValueError):
+        return None, "no profiles/pmc_traffic.json"
+    key = f"{shape}@{iters_per_launch}"
+    rec = data.get(key)
+    if rec is None:
+        return None, f"no PMC record for {key}"
+    return rec.get("hbm_bytes_per_launch"), f"profiles/pmc_traffic.json[{key}] ({rec.get('profile', '')})"
+
+
+def ess_block(samples, accept_n, K, elapsed):
+    """ESS/s over the timed draws (reference rule, examples/06_nuts_comparison.py:22-41,
+    summed over chains) — published only from chains that moved, with at least
+    100 draws and split R-hat max <= 1.1; otherwise null with the reason."""
+    import numpy as np
+    import torch
+
+    from mlx_mcmc_amd.diagnostics import chain_diagnostics
+
+    moving = np.nonzero(accept_n > 0)[0]
+    out = {"draws": K, "chains_used": int(moving.size), "frozen_chains": int(accept_n.size - moving.size)}
+    if K < 100:
+        out["ess_per_sec"] = None
+        out["ess_null_reason"] = f"{K} timed draws < 100"
+        return out
+    if moving.size < 2:
+        out["ess_per_sec"] = None
+        out["ess_null_reason"] = "fewer than two chains accepted a proposal"
+        return out
+    idx = torch.from_numpy(moving).to(samples.device)
+    d = chain_diagnostics(samples[:, :K, :].index_select(0, idx), group=False)
+    rh = d["rhat"]
+    out["rhat"] = {"max": float(np.nanmax(rh)), "median": float(np.nanmedian(rh)), "split": True}
+    if d["n_constant"] or not np.isfinite(rh).all() or np.nanmax(rh) > 1.1:
+        out["ess_per_sec"] = None
+        out["ess_null_reason"] = (f"split R-hat max {np.nanmax(rh):.3g} > 1.1 over the {K} timed "
+                                  f"draws of {moving.size} moving chains (and {d['n_constant']} "
+                                  "constant series): the draws are not yet from the posterior")
+        return out
+    if np.any(d["ess"] <= 0):
+        out["ess_per_sec"] = None
+        out["ess_null_reason"] = (f"the reference ESS rule gives {int(np.sum(d['ess'] <= 0))} "
+                                  "non-positive per-chain ESS values (antithetic draws)")
+        return out
+    out["ess_per_sec"] = {"min": float(d["ess_sum"].min()) / elapsed,
+                          "median": float(np.median(d["ess_sum"])) / elapsed,
+                          "unit": "effective samples/s (sum over moving chains)"}
+    return out
+
+
+def converged_ess(prog, C, q0, dev, L, args):
+    """ESS/s where the draws are from the posterior: the same kernel, model and
+    chain count at the fixed step size of the posterior tests (eps = 2e-3,
+    tests/test_gpu_posterior_exact.py: accept ~0.98), W = --ess-warmup,
+    S = --ess-draws sampling iterations timed; reported only with split R-hat
+    max <= 1.1.  ESS/s over the sampling seconds and over warmup + sampling
+    (SURVEY 8d)."""
+    import numpy as np
+    import torch
+
+    from mlx_mcmc_amd import _engine
+    from mlx_mcmc_amd.diagnostics import chain_diagnostics
+
+    S, Wm, eps = args.ess_draws, args.ess_warmup, args.ess_step_size
+    chains = _engine.ChainSet(prog, C, q0, eps, device=dev)
+    samples = torch.empty((C, S, prog.D), dtype=torch.float32, device=dev)
+    cfg = dict(chain_offset=0, num_warmup=Wm, num_samples=S, sample_begin=0, sample_capacity=S,
+               seed=args.seed + 1, step_size=eps, target_accept=0.8, num_leapfrog_steps=L,
+               adapt_step_size=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for it0 in range(0, Wm, 500):
+        chains.run_hmc(samples=samples, iter_begin=it0, iter_count=min(500, Wm - it0), **cfg)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for it0 in range(Wm, Wm + S, 500):
+        chains.run_hmc(samples=samples, iter_begin=it0, iter_count=min(500, Wm + S - it0), **cfg)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    check(chains, "converged-ESS run")
+    sc = chains.scalars()
+    d = chain_diagnostics(samples, group=False)
+    rh = d["rhat"]
+    out = {"step_size": eps, "warmup": Wm, "draws": S, "chains": C,
+           "accept_rate": float(np.mean(sc["n_accept"] / np.maximum(sc["n_total"], 1))),
+           "sampling_s": t2 - t1, "warmup_s": t1 - t0,
+           "rhat": {"max": float(np.nanmax(rh)), "median": float(np.nanmedian(rh)), "split": True}}
+    if d["n_constant"] or not np.isfinite(rh).all() or np.nanmax(rh) > 1.1:
+        out["ess_per_sec"] = None
+        out["ess_null_reason"] = f"split R-hat max {np.nanmax(rh):.3g} > 1.1"
+    elif np.any(d["ess"] <= 0):
+        # the reference rule (examples/06_nuts_comparison.py:22-41) keeps the
+        # first autocorrelation below 0.05 even when it is strongly negative
+        # (antithetic HMC draws), which makes n / (1 + 2 sum rho) negative
+        out["ess_per_sec"] = None
+        out["ess_null_reason"] = (f"the reference ESS rule gives {int(np.sum(d['ess'] <= 0))} "
+                                  "non-positive per-chain ESS values (antithetic draws)")
+    else:
+        e = d["ess_sum"]
+        out["ess_per_sec"] = {"min": float(e.min()) / (t2 - t1),
+                              "median": float(np.median(e)) / (t2 - t1),
+                              "min_over_warmup_and_sampling": float(e.min()) / (t2 - t0),
+                              "unit": "effective samples/s (sum over chains, reference rule)"}
+        out["ess_sum"] = {"min": float(e.min()), "median": float(np.median(e))}
+    del chains, samples
+    return out
 
 
 def check(chains, where):
@@ -503,14 +628,15 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     check(chains, "timed region")
-    # per-iteration kernel time from the full launches (HIP events on the
-    # launch stream)
-    full = [a.elapsed_time(b) for (a, b), (_, n) in zip(ev, timed) if n == B] or \
-           [a.elapsed_time(b) / n for (a, b), (_, n) in zip(ev, timed)]
-    launch_ms = float(np.mean(full)) if K else float("nan")
+    # kernel time per launch from the largest launches of the timed region
+    # (HIP events on the launch stream): a run of K < B iterations is one
+    # K-iteration launch, and every field below describes that launch
+    ipl = max((n for _, n in timed), default=0)
+    full = [a.elapsed_time(b) for (a, b), (_, n) in zip(ev, timed) if n == ipl]
+    launch_ms = float(np.mean(full)) if full else float("nan")
     each_ms = [round(a.elapsed_time(b), 4) for a, b in ev]
-    iters_per_launch = B if any(n == B for _, n in timed) else 1
-    kern_ms = launch_ms / iters_per_launch
+    iters_per_launch = max(ipl, 1)
+    iter_ms = launch_ms / iters_per_launch
     elapsed = max_over_ranks(elapsed, device=dev)
 
     sc = chains.scalars()
@@ -520,16 +646,17 @@ def main():
     eps = float(np.mean(sc["step_size"]))
 
     # ---- diagnostics on the device (not timed) ----------------------------------
-    # ESS per (chain, element) with the reference rule and split R-hat; across
-    # ranks only [2, D] f64 moment blocks are all-reduced (RCCL), no samples move
-    diag = None
+    # ESS per (chain, element) with the reference rule and split R-hat over the
+    # timed draws of the chains that moved (ess_block says when it is null)
+    ess = None
     diag_ms = None
-    if not args.no_ess and K >= 10:
-        from mlx_mcmc_amd.diagnostics import chain_diagnostics
-
+    if not args.no_ess and K >= 1 and world == 1:
         td = time.perf_counter()
-        diag = chain_diagnostics(samples[:, :K, :])
+        ess = ess_block(samples, sc["n_accept"], K, elapsed)
         diag_ms = (time.perf_counter() - td) * 1e3
+    ess_conv = None
+    if not args.no_ess and world == 1 and args.ess_draws > 0:
+        ess_conv = converged_ess(prog, C, prog.layout.flatten(init), dev, L, args)
     gather_ms = None
     if world > 1 and args.gather:
         tg = time.perf_counter()
@@ -543,17 +670,7 @@ def main():
         value = steps_total / elapsed
         flops_per_launch = C * L * W.hierarchical_flops_per_step(G, N) * iters_per_launch
         achieved = flops_per_launch / (launch_ms * 1e-3) / 1e12
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            try:
-                rec = json.load(open(pmc)).get(args.shape, {})
-                traffic = rec.get("hbm_bytes_per_launch")
-                # per launch of this run's size (the profile's launches may differ)
-                if traffic is not None:
-                    traffic *= iters_per_launch / rec.get("iters_per_launch", 1)
-            except Exception:
-                traffic = None
+        traffic, traffic_src = pmc_traffic(args.shape, iters_per_launch)
         out = {
             "metric": METRIC,
             "value": value,
@@ -578,7 +695,7 @@ def main():
                 "bound": "valu_fp32", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
                 "kernel": kernel_label(prog, C),
-                "kernel_ms": kern_ms,
+                "iteration_ms": iter_ms,
                 "launch_ms": launch_ms,
                 "each_launch_ms": each_ms if len(each_ms) <= 25 else None,
                 "iters_per_launch": iters_per_launch,
@@ -586,10 +703,12 @@ def main():
                 "note": ("FP32 VALU bound (SURVEY 8d: no dense contraction, no MFMA; vector FP32 "
                          "peak 157.3 TF); "
                          "F = 5N + 13D flops per chain-leapfrog-step, C*L per iteration, "
-                         "iters_per_launch iterations per launch; launch_ms = HIP events around "
-                         "each full launch on its stream, kernel_ms = launch_ms per iteration; "
-                         "traffic = (2*FETCH_SIZE + WRITE_SIZE) per launch from "
-                         "profiles/pmc_traffic.json (its launch size in that file)"),
+                         "iters_per_launch iterations per launch (the largest launch of the "
+                         "timed region); launch_ms = HIP events around each such launch on "
+                         "its stream, iteration_ms = launch_ms / iters_per_launch; "
+                         "traffic = (2*FETCH_SIZE + WRITE_SIZE) per launch of this size from "
+                         "profiles/pmc_traffic.json"),
+                "traffic_source": traffic_src,
             },
             "accept_rate": accept, "step_size": eps,
             # the data every chain reads per step (8N bytes: y and the
@@ -601,25 +720,12 @@ def main():
         if gather_ms is not None:
             out["gather_ms"] = gather_ms
         out["frozen_chains"] = frozen
-        if diag is not None:
-            ess_sum = diag["ess_sum"]                         # per element, all chains
-            rh = diag["rhat"]
-            if frozen or diag["n_constant"]:
-                # the reference rule scores a constant series as ESS = n: an
-                # ESS/s from chains that never moved would be fiction
-                out["ess_per_sec"] = None
-                out["rhat"] = None
-                out["ess_null_reason"] = (f"{frozen} chains accepted no proposal and "
-                                          f"{diag['n_constant']} series have zero variance "
-                                          f"over the {K} timed draws")
-            else:
-                out["ess_per_sec"] = {"min": float(ess_sum.min()) / elapsed,
-                                      "median": float(np.median(ess_sum)) / elapsed,
-                                      "unit": "effective samples/s (sum over chains)",
-                                      "draws": K}
-                out["rhat"] = ({"max": float(np.nanmax(rh)), "median": float(np.nanmedian(rh)),
-                                "split": True} if np.isfinite(rh).any() else None)
+        if ess is not None:
+            out["ess_per_sec"] = ess.pop("ess_per_sec")
+            out["ess_timed"] = ess
             out["diagnostics_ms"] = diag_ms
+        if ess_conv is not None:
+            out["ess_converged"] = ess_conv
         if world == 1 and not args.no_cpu_baseline:
             nproc = args.cpu_procs if args.cpu_procs >= 0 else min(15, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(G, N, L, max(eps, 1e-4), args.cpu_seconds, nproc,
@@ -628,11 +734,8 @@ def main():
     # release the device objects (program, chain state, workspace) before the
     # interpreter's exit handlers run, so nothing calls into HIP after a
     # profiler's teardown
-    del chains, prog, samples, diag
+    del chains, prog, samples
     torch.cuda.synchronize()
-    if os.environ.get("MC_DUMP_MAPS"):  # diagnostic: map exit-time crash addresses
-        with open(os.environ["MC_DUMP_MAPS"], "w") as f:
-            f.write(open("/proc/self/maps").read())
     if world > 1:
         dist.destroy_process_group()
 

@@ -310,6 +310,11 @@ int mc_debug_exchange_fault(int on);
  * run time (FORM = -1) instead of its compile-time instantiations; 1 restores
  * the default.  Results agree up to fp32 summation order.                  */
 int mc_debug_lanes_forms(int on);
+/* Test hook for k_nuts_lr's variants: -1 (default) picks the fastest variant
+ * the program qualifies for; 0 forces the generic lane evaluator (SPEC 0);
+ * 1 forces the specialised variant (SPEC 1) where the program qualifies,
+ * skipping the register-only one.  Trees agree up to fp32 summation order. */
+int mc_debug_nuts_variant(int variant);
 /* After a sliced mc_hmc_run: MC_OK, or MC_ERR_TIMEOUT if an exchange timed
  * out (the launch then left its chains' state unchanged or partial).
  * Synchronises the stream.  Always MC_OK for an unsliced program.         */

@@ -176,6 +176,7 @@ SIGNATURES = [
     ("mc_workspace_release", ctypes.c_int, [_VP]),
     ("mc_debug_exchange_fault", ctypes.c_int, [ctypes.c_int]),
     ("mc_debug_lanes_forms", ctypes.c_int, [ctypes.c_int]),
+    ("mc_debug_nuts_variant", ctypes.c_int, [ctypes.c_int]),
     ("mc_hmc_run", ctypes.c_int,
      [_VP, ctypes.POINTER(McRunConfig), _VP, _VP, ctypes.POINTER(McTrace), _VP,
       ctypes.c_int64, _VP]),

@@ -1878,32 +1878,16 @@ static int device_cus() {
 // co-resident fails fast with MC_ERR_UNSUPPORTED.  They are then launched
 // plainly: on a device shared with other work that keeps some of the grid
 // out, the spin times out and the launch reports MC_ERR_TIMEOUT with the
-// stranded block's state unchanged (mc_workspace_status).  MC_COOPERATIVE=1
-// in the environment selects cooperative launches (the runtime runs the grid
-// only when all of it fits, also beside other work), at ~50 us per launch on
-// MI355X (profiles/r2/v17_coop_ab.json: 1.25 vs 1.195 ms per 20-iteration
-// launch of the bench kernel).
-static bool coop_enabled() {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = std::getenv("MC_COOPERATIVE");
-        on = (e && e[0] == '1') ? 1 : 0;
-    }
-    return on == 1;
-}
+// stranded block's state unchanged (mc_workspace_status).  (Round 2 also
+// offered cooperative launches behind an environment switch: ~50 us more per
+// launch on MI355X, profiles/r2/v17_coop_ab.json, and a crash in torch's HIP
+// exit handlers under rocprofv3 whose cause was not found — removed.)
 template <typename... KA, typename... A>
 static hipError_t launch_exchange(void (*k)(KA...), int64_t grid, int block, size_t lds,
                                   hipStream_t st, A&&... a) {
-    std::tuple<std::decay_t<KA>...> t(std::forward<A>(a)...);
-    void* ptrs[sizeof...(KA)];
-    std::apply([&](auto&... x) {
-        int i = 0;
-        ((ptrs[i++] = (void*)&x), ...);
-    }, t);
-    if (coop_enabled())
-        return hipLaunchCooperativeKernel((const void*)k, dim3((unsigned)grid), dim3(block), ptrs,
-                                          (unsigned)lds, st);
-    return hipLaunchKernel((const void*)k, dim3((unsigned)grid), dim3(block), ptrs, lds, st);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(block), lds, st,
+                       std::decay_t<KA>(std::forward<A>(a))...);
+    return hipGetLastError();
 }
 // workgroups of kernel k (block threads, lds bytes) the device holds at once
 template <typename K>
@@ -2104,9 +2088,6 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
                 kern, grid, 64 * NW, lds, st, ctx, A, g0 * NB, ng,
                 (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples, trace_of(tr),
                 xch, status, base);
-            if (e == hipErrorCooperativeLaunchTooLarge)
-                return fail(MC_ERR_UNSUPPORTED, "lane-resident HMC: grid of %lld workgroups is "
-                            "too large to be co-resident", (long long)grid);
             MC_HIP_TRY(e);
         }
         base += (uint32_t)per_launch;
@@ -2151,9 +2132,6 @@ static int launch_hmc_sl(const mc_program* p, const mc_run_config* cfg, void* st
                                              A, g0 * NB, ng, (mc_chain_scalars*)b,
                                              (float*)(b + qo), (float*)(b + go), samples,
                                              trace_of(tr), xch, status);
-        if (e == hipErrorCooperativeLaunchTooLarge)
-            return fail(MC_ERR_UNSUPPORTED, "sliced HMC: grid of %lld workgroups is too large "
-                        "to be co-resident", (long long)grid);
         MC_HIP_TRY(e);
     }
     return MC_OK;
@@ -2415,6 +2393,12 @@ static bool lanes_specialised(const mc_program* p) {
     return true;
 }
 
+static int g_nuts_variant = -1;  // mc_debug_nuts_variant
+extern "C" int mc_debug_nuts_variant(int variant) {
+    g_nuts_variant = (variant < -1 || variant > 1) ? -1 : variant;
+    return MC_OK;
+}
+
 template <int RS, int NSH>
 static int launch_nuts_lr(const mc_program* p, const mc_run_config* cfg, void* state,
                           float* samples, const mc_trace* tr, hipStream_t st) {
@@ -2427,7 +2411,8 @@ static int launch_nuts_lr(const mc_program* p, const mc_run_config* cfg, void* s
     const size_t lds = nuts_lr_lds_bytes(p, cfg->max_tree_depth);
     auto kern = lanes_specialised(p) ? k_nuts_lr<RS, NSH, 1> : k_nuts_lr<RS, NSH, 0>;
     if constexpr (NSH == 3)
-        if (lanes_register_only(p)) kern = k_nuts_lr<RS, NSH, 2>;
+        if (lanes_register_only(p) && g_nuts_variant < 0) kern = k_nuts_lr<RS, NSH, 2>;
+    if (g_nuts_variant == 0) kern = k_nuts_lr<RS, NSH, 0>;
     MC_HIP_TRY(allow_lds(kern, lds));
     hipLaunchKernelGGL(kern, dim3((unsigned)cfg->num_chains), dim3(64), lds, st, lrctx_of(p), A,
                        (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples,

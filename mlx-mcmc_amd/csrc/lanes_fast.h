@@ -495,9 +495,14 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             pj = pj + xh * sh.g;
             sh.p = pj;
             sh.q = sh.q + xe * pj;
-            sh.is = 1.0f / sh.q;
-            sh.iv = 1.0f / (sh.q * sh.q);
-            sh.lg = logf(sh.q);
+            // the shared scale's reciprocals and log (moment form): hardware
+            // v_rcp_f32 / v_log_f32 (<= 1 ulp) instead of the IEEE division
+            // and logf sequences — one dependent chain of ~40 VALU on every
+            // step's critical path becomes 5; the same bits in every slice,
+            // so the replicas stay identical
+            sh.is = __builtin_amdgcn_rcpf(sh.q);
+            sh.iv = sh.is * sh.is;
+            sh.lg = __builtin_amdgcn_logf(sh.q) * 0.693147180559945f;  // log2 q * ln 2
         };
         f2 M1[RS], M2[RS];
         drift_private(false);
@@ -509,9 +514,20 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             // term (k_hmc_lr's lr_finish; same arithmetic, both chains packed):
             // log p partial, complete private gradients, cotangent partials of
             // the swept scale (cs), the direct loc (cm) and scale (cd)
+            // (the first contribution to each sum is assigned, not added to
+            // zero: x + 0 is not folded under IEEE signed zeros)
             f2 lpp = {0.f, 0.f}, cs = {0.f, 0.f}, cm = {0.f, 0.f}, cd = {0.f, 0.f};
+            bool lpp0 = true, cs0 = true, cm0 = true, cd0 = true;
+            bool g0r[RS];
 #pragma unroll
-            for (int r = 0; r < RS; ++r) g[r] = (f2){0.f, 0.f};
+            for (int r = 0; r < RS; ++r) {
+                g[r] = (f2){0.f, 0.f};
+                g0r[r] = true;
+            }
+            auto acc = [](f2& s, bool& first, f2 v) {
+                s = first ? v : s + v;
+                first = false;
+            };
             if (SW) {
                 const f2 is = SWS ? lf_sh2(sh.is, ksw) : sw_cinv;
                 const f2 iv = SWS ? lf_sh2(sh.iv, ksw) : sw_cinv2;
@@ -519,11 +535,19 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 const f2 c0lg = sw_c0 - lg;
 #pragma unroll
                 for (int r = 0; r < RS; ++r) {
-                    if (len[r] == 0) continue;
+                    const bool on = len[r] != 0;
                     const f2 lpt = cnt[r] * c0lg - (half * M2[r]) * iv;
-                    lpp += sw_w * lpt;
-                    g[r] += sw_w * (M1[r] * iv);
-                    cs += sw_w * ((M2[r] * iv - cnt[r]) * is);
+                    const f2 z = {0.f, 0.f};
+                    if (RS == 1) {  // one slot: an empty lane's terms are zeros
+                        lpp = on ? sw_w * lpt : z;
+                        g[r] = on ? sw_w * (M1[r] * iv) : z;
+                        cs = on ? sw_w * ((M2[r] * iv - cnt[r]) * is) : z;
+                        lpp0 = cs0 = g0r[r] = false;
+                    } else if (on) {
+                        acc(lpp, lpp0, sw_w * lpt);
+                        acc(g[r], g0r[r], sw_w * (M1[r] * iv));
+                        acc(cs, cs0, sw_w * ((M2[r] * iv - cnt[r]) * is));
+                    }
                 }
             }
             if (DIR) {
@@ -538,11 +562,11 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     const f2 d = q[r] - um;
                     const f2 s2 = d * d;
                     const f2 lpt = c0lg - (half * s2) * iv;
-                    lpp += d_w * lpt;
+                    acc(lpp, lpp0, d_w * lpt);
                     const f2 u = d_w * (d * iv);
-                    g[r] += -u;
-                    cm += u;
-                    cd += d_w * ((s2 * iv - one) * is);
+                    acc(g[r], g0r[r], -u);
+                    acc(cm, cm0, u);
+                    acc(cd, cd0, d_w * ((s2 * iv - one) * is));
                 }
             }
             // the own prior of this lane's shared parameter (moment form with
@@ -649,35 +673,39 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             }
             // poll: pass ps reads pair 4 ps + perm[row] of slice col
             const bool kstep = (l == 0) || (l == L - 1);
-            uint32_t need = need_v | (l == 0 ? need_k0 : 0u) | (l == L - 1 ? need_k1 : 0u);
+            const uint32_t need = need_v | (l == 0 ? need_k0 : 0u) | (l == L - 1 ? need_k1 : 0u);
             float vals[NPASS];
 #pragma unroll
             for (int ps = 0; ps < NPASS; ++ps) vals[ps] = 0.0f;
             // every pass's granules loaded at once (one round trip; lanes that
-            // need none read an in-bounds line and ignore it), then checked
+            // need none read an in-bounds line and ignore it); ready when every
+            // needed tag is this step's.  A granule of this step is never
+            // rewritten before this wave publishes the next one (the line
+            // parity alternates per step), so the values of the last load
+            // are the record's.
             auto poll = [&]() {
                 unsigned long long y[NPASS];
 #pragma unroll
                 for (int ps = 0; ps < NPASS; ++ps)
                     y[ps] = (ps < NPASS_V || kstep) ? granule_load(gp[par] + 4 * ps) : 0ull;
+                bool ready = true;  // (bitwise: lane masks, no branches)
 #pragma unroll
                 for (int ps = 0; ps < NPASS; ++ps) {
-                    if (((need >> ps) & 1u) && (uint32_t)(y[ps] >> 32) == epoch) {
-                        vals[ps] = __uint_as_float((uint32_t)y[ps]);
-                        need &= ~(1u << ps);
-                    }
+                    vals[ps] = __uint_as_float((uint32_t)y[ps]);
+                    ready = ready & (((need >> ps) & 1u) == 0u | (uint32_t)(y[ps] >> 32) == epoch);
                 }
+                return ready;
             };
-            if (!X1) poll();
+            bool ready = X1 ? true : poll();
             MC_STAMP(7);
             uint32_t spins = 0;
-            while (__ballot(need != 0)) {
+            while (__ballot(!ready)) {
                 if (++spins > kSpinLimit) {
                     ok = false;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
-                poll();
+                ready = poll();
             }
             if (!ok) {
                 __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

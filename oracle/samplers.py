@@ -232,15 +232,26 @@ def _slice_log_u(log_u: float, mode: str) -> float:
 
 def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_size=0.1,
          max_tree_depth=10, adapt_step_size=True, target_accept=0.65, seed=0, chain=0,
-         slice_mode="reference", record=True) -> OracleRun:
+         slice_mode="reference", record=True, step_sizes=None) -> OracleRun:
+    """Restates nuts.py:16-358.  Test-only extras: ``record`` keeps per
+    iteration alpha, depth, eps, H0, leaves and the decision margins (the
+    smallest |log u + H'| over the leaves — the slice test nuts.py:170 —,
+    the smallest |log u - (1000 - H')| — the divergence test :171 — and the
+    smallest relative U-turn dot |d.r| / sum|d_i r_i| of any U-turn check,
+    nuts.py:119-135), so a test can prove a flipped decision a near-tie;
+    ``step_sizes`` (per iteration) replaces the step size of every iteration
+    (the dual-averaging values are still computed and recorded as
+    ``da_step_size``): the oracle replays a run's step-size sequence."""
     M = EagerModel(log_prob_fn, initial_params)
     q = M.flatten(initial_params)
     mu = R.logf_ref(F32(10 * step_size))   # nuts.py:63
     epsilon_bar = 1.0
     H_bar = 0.0
     gamma, t0, kappa = 0.05, 10.0, 0.75
-    trace = {"alpha": [], "depth": [], "step_size": [], "energy": [], "leaves": []}
+    trace = {"alpha": [], "depth": [], "step_size": [], "energy": [], "leaves": [],
+             "slice_gap": [], "div_gap": [], "uturn_margin": [], "da_step_size": []}
     n_grad = 0
+    margins = {"slice": math.inf, "div": math.inf, "uturn": math.inf}
 
     def no_u_turn(tm, tp, rm, rp):
         d = tp - tm
@@ -250,6 +261,12 @@ def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_si
             n = int(np.prod(s)) if s else 1
             dot_minus = F32(dot_minus + np.sum(d[o:o + n] * rm[o:o + n], dtype=np.float32))
             dot_plus = F32(dot_plus + np.sum(d[o:o + n] * rp[o:o + n], dtype=np.float32))
+        if record:
+            d64 = d.astype(np.float64)
+            for dot, r in ((dot_minus, rm), (dot_plus, rp)):
+                scale = float(np.sum(np.abs(d64 * r.astype(np.float64))))
+                if scale > 0:
+                    margins["uturn"] = min(margins["uturn"], abs(float(dot)) / scale)
         return float(dot_minus) >= 0 and float(dot_plus) >= 0
 
     def build_tree(theta, r, logu, v, j, eps, H0, it, jtop, k0):
@@ -260,6 +277,9 @@ def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_si
             H1 = M.hamiltonian(theta1, r1)
             n1 = 1 if logu <= float(-H1) else 0
             s1 = logu < float(F32(DELTA_MAX) - H1)
+            if record and math.isfinite(logu) and math.isfinite(float(H1)):
+                margins["slice"] = min(margins["slice"], abs(logu + float(H1)))
+                margins["div"] = min(margins["div"], abs(logu - float(F32(DELTA_MAX) - H1)))
             alpha = min(1.0, float(R.expf_ref(F32(-H1 + H0))))
             return theta1, theta1, r1, r1, theta1, n1, s1, alpha, 1
         tm, tp, rm, rp, t1, n1, s1, a1, na1 = build_tree(theta, r, logu, v, j - 1, eps, H0,
@@ -295,6 +315,7 @@ def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_si
         theta_prime = theta
         alpha_sum, n_alpha = 0.0, 0
         g0 = n_grad
+        margins.update(slice=math.inf, div=math.inf, uturn=math.inf)
         while s and j < max_tree_depth:
             w = R.draw(seed, chain, it, R.TAG_DEPTH, j, 0)
             v = 1 if float(R.u01_f32(w[0])) < 0.5 else -1
@@ -320,12 +341,17 @@ def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_si
             trace["step_size"].append(eps)
             trace["energy"].append(float(H0))
             trace["leaves"].append((n_grad - g0) // 2)
+            trace["slice_gap"].append(margins["slice"])
+            trace["div_gap"].append(margins["div"])
+            trace["uturn_margin"].append(margins["uturn"])
         return theta_prime, alpha, j
 
     epsilon = step_size
     n_accept = n_total = 0
     total_depth = 0
     for m in range(num_warmup):
+        if step_sizes is not None:
+            epsilon = float(step_sizes[m])
         q, alpha, depth = nuts_step(q, epsilon, m)
         n_accept += int(alpha > 0.5)
         n_total += 1
@@ -339,6 +365,8 @@ def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_si
             m_eta = float(m + 1) ** (-kappa)
             log_epsilon_bar = m_eta * math.log(epsilon) + (1 - m_eta) * math.log(epsilon_bar)
             epsilon_bar = float(R.expf_ref(F32(log_epsilon_bar)))
+        if record:
+            trace["da_step_size"].append(epsilon)
     if adapt_step_size:
         epsilon = epsilon_bar
     warmup_accept_rate = n_accept / n_total       # ZeroDivisionError at num_warmup=0
@@ -346,6 +374,8 @@ def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_si
     n_accept = n_total = 0
     samples = []
     for m in range(num_samples):
+        if step_sizes is not None:
+            epsilon = float(step_sizes[m + num_warmup])
         q, alpha, depth = nuts_step(q, epsilon, m + num_warmup)
         samples.append(q.copy())
         n_accept += int(alpha > 0.5)
@@ -372,3 +402,22 @@ def compute_ess(samples) -> float:
         if c < 0.05:
             break
     return n / (1 + 2 * np.sum(acf))
+
+
+def dual_averaging_steps(alpha, eps0, num_warmup, target_accept=0.65):
+    """The step size of every warmup iteration and the final eps-bar produced
+    by dual averaging (nuts.py:63-68,299-310, with the f32 round trips of
+    nuts() above) from a given sequence of mean acceptance statistics."""
+    mu = R.logf_ref(F32(10 * eps0))
+    eps, eps_bar, h_bar = eps0, 1.0, 0.0
+    out = []
+    for m in range(num_warmup):
+        out.append(eps)
+        eta = 1.0 / (m + 10.0)
+        h_bar = (1 - eta) * h_bar + eta * (target_accept - float(alpha[m]))
+        log_eps = F32(mu - F32((math.sqrt(m + 1) / 0.05) * h_bar))
+        log_eps = max(min(log_eps, 10.0), -10.0)
+        eps = float(R.expf_ref(F32(log_eps)))
+        m_eta = float(m + 1) ** (-0.75)
+        eps_bar = float(R.expf_ref(F32(m_eta * math.log(eps) + (1 - m_eta) * math.log(eps_bar))))
+    return np.array(out), eps_bar

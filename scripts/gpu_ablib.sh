@@ -16,9 +16,9 @@ i=0
 for lib in "$@"; do
   i=$((i+1))
   if [ "$lib" = "-" ]; then
-    timeout -k 10 300 python bench.py --no-cpu-baseline --steps 200 --warmup 50 > gpurun_out/${TAG}_bench_$i.json 2> gpurun_out/${TAG}_bench_$i.err || { echo "bench $lib failed"; tail -20 gpurun_out/${TAG}_bench_$i.err; exit 1; }
+    timeout -k 10 300 python bench.py --no-cpu-baseline --no-ess --steps 200 --warmup 50 > gpurun_out/${TAG}_bench_$i.json 2> gpurun_out/${TAG}_bench_$i.err || { echo "bench $lib failed"; tail -20 gpurun_out/${TAG}_bench_$i.err; exit 1; }
   else
-    timeout -k 10 300 python scripts/ab_lib.py $lib --no-cpu-baseline --steps 200 --warmup 50 > gpurun_out/${TAG}_bench_$i.json 2> gpurun_out/${TAG}_bench_$i.err || { echo "bench $lib failed"; tail -20 gpurun_out/${TAG}_bench_$i.err; exit 1; }
+    timeout -k 10 300 python scripts/ab_lib.py $lib --no-cpu-baseline --no-ess --steps 200 --warmup 50 > gpurun_out/${TAG}_bench_$i.json 2> gpurun_out/${TAG}_bench_$i.err || { echo "bench $lib failed"; tail -20 gpurun_out/${TAG}_bench_$i.err; exit 1; }
   fi
   python -c "
 import json

@@ -8,7 +8,7 @@ TAG=${1:-sq}
 mkdir -p "$R/gpurun_out"
 cd "$R"
 timeout -k 10 120 python scripts/stamps_lr.py 256 > gpurun_out/${TAG}_stamps.log 2>&1 || { echo "stamps failed"; tail -5 gpurun_out/${TAG}_stamps.log; exit 1; }
-export TMPDIR=/tmp MC_COOPERATIVE=0
+export TMPDIR=/tmp
 cd /tmp
 ARGS="--steps 100 --warmup 50 --iters-per-launch 50 --no-cpu-baseline --no-ess"
 run() {

@@ -8,7 +8,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r2p}
 mkdir -p "$R/gpurun_out"
-export TMPDIR=/tmp MC_COOPERATIVE=0
+export TMPDIR=/tmp
 cd /tmp
 ARGS="--steps 100 --warmup 50 --iters-per-launch 50 --no-cpu-baseline --no-ess"
 run() {  # name, rocprof args...

@@ -149,3 +149,30 @@ def test_large_trace_fixture_is_mixed():
 
     c = int(fx["chains"][2])
     assert fx["log_u"][2][5] == R.logf_ref(R.uniform(0, c, 5, R.TAG_ACCEPT))
+
+
+def test_oracle_nuts_fixture_replay_and_dual_averaging():
+    """The committed NUTS traces (scripts/gen_golden_nuts.py) are what the
+    oracle computes: replaying chain 0 with the recorded step sizes gives the
+    same trees, and dual averaging restated from the recorded alphas gives
+    the recorded step sizes (the helper the GPU test recomputes the kernel's
+    adaptation with)."""
+    import json
+
+    from oracle import samplers as S
+
+    fx = np.load(os.path.join(GOLD, "nuts_illcond_trace.npz"), allow_pickle=False)
+    cfg = json.loads(str(fx["config"]))
+    da, eps_bar = S.dual_averaging_steps(fx["alpha"][0], cfg["step_size"], cfg["num_warmup"],
+                                         cfg["target_accept"])
+    np.testing.assert_array_equal(da, fx["step_size"][0][:cfg["num_warmup"]])
+    assert np.all(fx["step_size"][0][cfg["num_warmup"]:] == eps_bar)
+    lp, init = W.illcond_normal(W.ns_oracle())
+    r = S.nuts(lp, init, seed=cfg["seed"], chain=int(fx["chains"][0]),
+               step_sizes=fx["step_size"][0],
+               **{k: cfg[k] for k in ("num_warmup", "num_samples", "step_size", "max_tree_depth",
+                                      "target_accept")})
+    np.testing.assert_array_equal(r.trace["depth"], fx["depth"][0])
+    np.testing.assert_array_equal(r.trace["leaves"], fx["leaves"][0])
+    np.testing.assert_array_equal(r.samples, fx["samples"][0])
+    assert fx["depth"].max() >= 5
