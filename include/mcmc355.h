@@ -315,6 +315,11 @@ int mc_debug_lanes_forms(int on);
  * 1 forces the specialised variant (SPEC 1) where the program qualifies,
  * skipping the register-only one.  Trees agree up to fp32 summation order. */
 int mc_debug_nuts_variant(int variant);
+/* Test hooks (host code, no device): the samplers' Box-Muller pair from two
+ * Philox words per pair (words [n][2] -> out [n][2] f32) and their double
+ * log of a uniform in [2^-40, 1] (philox.h mc_box_muller / mc_log_unit).   */
+int mc_box_muller_host(const uint32_t* words, int64_t n, float* out);
+int mc_log_unit_host(const double* x, int64_t n, double* out);
 /* After a sliced mc_hmc_run: MC_OK, or MC_ERR_TIMEOUT if an exchange timed
  * out (the launch then left its chains' state unchanged or partial).
  * Synchronises the stream.  Always MC_OK for an unsliced program.         */

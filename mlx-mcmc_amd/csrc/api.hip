@@ -2615,5 +2615,18 @@ extern "C" int mc_select(int64_t C, int64_t S, int64_t D, const float* samples, 
     return MC_OK;
 }
 
+// Host evaluations of the samplers' Box-Muller and uniform log (philox.h:
+// the same code the kernels run), for the CPU tests against libm / the oracle.
+extern "C" int mc_box_muller_host(const uint32_t* words, int64_t n, float* out) {
+    if (n < 0 || (n > 0 && (!words || !out))) return fail(MC_ERR_INVALID, "bad arguments");
+    for (int64_t i = 0; i < n; ++i) mc_box_muller(words[2 * i], words[2 * i + 1], &out[2 * i], &out[2 * i + 1]);
+    return MC_OK;
+}
+extern "C" int mc_log_unit_host(const double* x, int64_t n, double* out) {
+    if (n < 0 || (n > 0 && (!x || !out))) return fail(MC_ERR_INVALID, "bad arguments");
+    for (int64_t i = 0; i < n; ++i) out[i] = mc_log_unit(x[i]);
+    return MC_OK;
+}
+
 extern "C" const char* mc_last_error(void) { return g_last_error.c_str(); }
 extern "C" int32_t mc_abi_version(void) { return MC_ABI_VERSION; }

@@ -122,7 +122,7 @@ k_hmc(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, flo
         const float H1 = -lpn + 0.5f * G.sum(kp1);
         const float ratio = -(H1 - H0);
         const mc_u32x4 ru = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_ACCEPT, 0, 0);
-        const float logu = mc_logf_ref(mc_u01_f32(ru.x));
+        const float logu = mc_logf_u01(mc_u01_f32(ru.x));
         const bool accepted = logu < ratio;
         if (accepted && L > 0) {
             float* t;

@@ -1111,7 +1111,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             const float ratio = -(H1 - H0);
             const mc_u32x4 ru = mc_draw(cfg.seed, (uint32_t)(cfg.chain_offset + cc[c]),
                                         (uint32_t)it, MC_RNG_TAG_ACCEPT, 0, 0);
-            const float logu = mc_logf_ref(mc_u01_f32(ru.x));
+            const float logu = mc_logf_u01(mc_u01_f32(ru.x));
             const bool accepted = logu < ratio;
             acc[c] = accepted;
             nacc[c] += accepted ? 1 : 0;

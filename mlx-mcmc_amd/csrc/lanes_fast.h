@@ -140,18 +140,38 @@ MC_DEV void lf_moments(const float* xv, int len, int lmin4, f2 th, f2& s1, f2& s
         a2[1] = pk_fma(d1, d1, a2[1]);
     };
     int u4 = 0;
-    for (; u4 + 4 <= lmin4; u4 += 4) {
-        f2 a[4][2];
+    // 16 elements per round; the next round's LDS loads are issued before
+    // this round's arithmetic (software pipelined over two register sets that
+    // alternate, so no copies: a lone wave per SIMD — fewer slices — does not
+    // wait for the load latency)
+    if (lmin4 >= 4) {
+        float4 A[4], B[4];
+        auto load = [&](float4 (&X)[4], int g) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 v = *(const float4*)(xv + (u4 + q) * 256);
-            a[q][0] = (f2){v.x, v.y};
-            a[q][1] = (f2){v.z, v.w};
-        }
+            for (int q = 0; q < 4; ++q) X[q] = *(const float4*)(xv + (g + q) * 256);
+        };
+        auto round = [&](const float4 (&X)[4]) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            pair(a[q][0]);
-            pair(a[q][1]);
+            for (int q = 0; q < 4; ++q) {
+                pair((f2){X[q].x, X[q].y});
+                pair((f2){X[q].z, X[q].w});
+            }
+        };
+        // (the prefetch index is clamped to the last full round: the loads
+        // are unconditional, so the register sets never need copies)
+        const int last = lmin4 - 4;
+        load(A, 0);
+        for (;;) {
+            const bool more_b = u4 + 8 <= lmin4;
+            load(B, min(u4 + 4, last));
+            round(A);
+            u4 += 4;
+            if (!more_b) break;
+            const bool more_a = u4 + 8 <= lmin4;
+            load(A, min(u4 + 4, last));
+            round(B);
+            u4 += 4;
+            if (!more_a) break;
         }
     }
     // the lane's remaining full groups (a lane-varying count), then its last
@@ -691,8 +711,11 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 bool ready = true;  // (bitwise: lane masks, no branches)
 #pragma unroll
                 for (int ps = 0; ps < NPASS; ++ps) {
-                    vals[ps] = __uint_as_float((uint32_t)y[ps]);
-                    ready = ready & (((need >> ps) & 1u) == 0u | (uint32_t)(y[ps] >> 32) == epoch);
+                    const bool nd = ((need >> ps) & 1u) != 0u;
+                    // a pass this lane does not need stays 0: the 16-lane slice
+                    // sums run over every column (S < 16 leaves columns idle)
+                    vals[ps] = nd ? __uint_as_float((uint32_t)y[ps]) : 0.0f;
+                    ready = ready & (!nd | ((uint32_t)(y[ps] >> 32) == epoch));
                 }
                 return ready;
             };
@@ -783,7 +806,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             const float ratio = -(H1 - H0);
             const mc_u32x4 ru = mc_draw(cfg.seed, (uint32_t)(cfg.chain_offset + cc[c]),
                                         (uint32_t)it, MC_RNG_TAG_ACCEPT, 0, 0);
-            const float logu = mc_logf_ref(mc_u01_f32(ru.x));
+            const float logu = mc_logf_u01(mc_u01_f32(ru.x));
             const bool accepted = logu < ratio;
             acc[c] = accepted;
             nacc[c] += accepted ? 1 : 0;

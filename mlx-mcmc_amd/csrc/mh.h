@@ -64,7 +64,7 @@ k_mh(DevCtx P, RunArgs A, float scale, mc_chain_scalars* scal, float* st_q, floa
         const float lpn = eval_lp_grad<WPC, true>(P, qB, nullptr, G, S);
         const float ratio = lpn - lp;
         const mc_u32x4 ru = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_ACCEPT, 0, 0);
-        const float logu = mc_logf_ref(mc_u01_f32(ru.x));
+        const float logu = mc_logf_u01(mc_u01_f32(ru.x));
         const bool accepted = logu < ratio;
         if (accepted) {
             float* t = qA;

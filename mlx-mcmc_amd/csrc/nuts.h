@@ -169,7 +169,7 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
 
         // slice variable (nuts.py:234-237)
         const mc_u32x4 rs = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_SLICE, 0, 0);
-        const double log_u = (double)(-H0) + (double)mc_logf_ref(mc_u01_f32(rs.x));
+        const double log_u = (double)(-H0) + (double)mc_logf_u01(mc_u01_f32(rs.x));
         double logu;
         if (cfg.slice_mode == 0) {
             const float x = (float)log_u;

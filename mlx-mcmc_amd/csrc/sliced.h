@@ -926,7 +926,7 @@ k_hmc_sl(SlCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 const uint32_t chain_id = (uint32_t)(cfg.chain_offset + min(c, C - 1));
                 const mc_u32x4 ru =
                     mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_ACCEPT, 0, 0);
-                const float logu = mc_logf_ref(mc_u01_f32(ru.x));
+                const float logu = mc_logf_u01(mc_u01_f32(ru.x));
                 const bool accepted = logu < ratio;
                 acc = accepted && L > 0;
                 if (acc) cs[CS_LP * NB + b] = lpn;

@@ -176,3 +176,37 @@ def test_oracle_nuts_fixture_replay_and_dual_averaging():
     np.testing.assert_array_equal(r.trace["leaves"], fx["leaves"][0])
     np.testing.assert_array_equal(r.samples, fx["samples"][0])
     assert fx["depth"].max() >= 5
+
+
+def test_box_muller_and_unit_log_match_libm():
+    """The samplers' Box-Muller (philox.h mc_box_muller: fdlibm-style log and
+    sincospi restricted to the uniforms' range) against the oracle's numpy
+    formula (oracle/philox.py box_muller) and libm, on the host build of the
+    same code (mc_box_muller_host / mc_log_unit_host)."""
+    import ctypes
+
+    from mlx_mcmc_amd import _lib
+    from oracle import philox as R
+
+    lib = _lib.load()
+    rng = np.random.default_rng(5)
+    n = 400_000
+    w = rng.integers(0, 2 ** 32, size=(n, 2), dtype=np.uint64).astype(np.uint32)
+    w[:64, 0] = np.arange(64)                       # u1 at the smallest values
+    w[64:128, 1] = 2 ** 32 - 1 - np.arange(64)      # angles next to 2 pi
+    out = np.zeros((n, 2), np.float32)
+    assert lib.mc_box_muller_host(w.ctypes.data_as(ctypes.c_void_p), n,
+                                  out.ctypes.data_as(ctypes.c_void_p)) == 0
+    z0, z1 = R.box_muller(w[:, 0], w[:, 1])
+    ref = np.stack([z0, z1], axis=1)
+    diff = out != ref
+    # differences only where the oracle's own angle rounding (2 pi u2 in f64)
+    # moves a value next to a zero of sin / cos: tiny values, a few f32 ulp
+    assert diff.sum() <= 16, diff.sum()
+    assert np.all(np.abs(out[diff] - ref[diff]) <= 1e-6 * np.maximum(np.abs(ref[diff]), 1e-3))
+    x = R.u01_f64(w[:, 0])
+    lg = np.zeros(n)
+    assert lib.mc_log_unit_host(x.ctypes.data_as(ctypes.c_void_p), n,
+                                lg.ctypes.data_as(ctypes.c_void_p)) == 0
+    ulps = np.abs(lg - np.log(x)) / np.spacing(np.abs(np.log(x)))
+    assert ulps.max() <= 1.0, ulps.max()
