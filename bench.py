@@ -157,7 +157,7 @@ def cpu_single(G, N, L, step_size, budget_s, chain=0):
             qp, pp = M.leapfrog(qp, pp, step_size)
             steps += 1
         H1 = M.hamiltonian(qp, pp)
-        if R.logf_ref(R.uniform(0, chain, iters, R.TAG_ACCEPT)) < -(H1 - H0):
+        if R.logf_u01(R.uniform(0, chain, iters, R.TAG_ACCEPT)) < -(H1 - H0):
             q = qp
         iters += 1
     dt = time.perf_counter() - t0

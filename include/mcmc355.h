@@ -316,10 +316,10 @@ int mc_debug_lanes_forms(int on);
  * skipping the register-only one.  Trees agree up to fp32 summation order. */
 int mc_debug_nuts_variant(int variant);
 /* Test hooks (host code, no device): the samplers' Box-Muller pair from two
- * Philox words per pair (words [n][2] -> out [n][2] f32) and their double
- * log of a uniform in [2^-40, 1] (philox.h mc_box_muller / mc_log_unit).   */
+ * Philox words per pair (words [n][2] -> out [n][2] f32) and their f32 log
+ * of a uniform in (0, 1] (philox.h mc_box_muller / mc_logf_unit).         */
 int mc_box_muller_host(const uint32_t* words, int64_t n, float* out);
-int mc_log_unit_host(const double* x, int64_t n, double* out);
+int mc_logf_unit_host(const float* x, int64_t n, float* out);
 /* After a sliced mc_hmc_run: MC_OK, or MC_ERR_TIMEOUT if an exchange timed
  * out (the launch then left its chains' state unchanged or partial).
  * Synchronises the stream.  Always MC_OK for an unsliced program.         */

@@ -2622,9 +2622,9 @@ extern "C" int mc_box_muller_host(const uint32_t* words, int64_t n, float* out) 
     for (int64_t i = 0; i < n; ++i) mc_box_muller(words[2 * i], words[2 * i + 1], &out[2 * i], &out[2 * i + 1]);
     return MC_OK;
 }
-extern "C" int mc_log_unit_host(const double* x, int64_t n, double* out) {
+extern "C" int mc_logf_unit_host(const float* x, int64_t n, float* out) {
     if (n < 0 || (n > 0 && (!x || !out))) return fail(MC_ERR_INVALID, "bad arguments");
-    for (int64_t i = 0; i < n; ++i) out[i] = mc_log_unit(x[i]);
+    for (int64_t i = 0; i < n; ++i) out[i] = mc_logf_unit(x[i]);
     return MC_OK;
 }
 

@@ -13,12 +13,14 @@
 // Transforms (identical in oracle/philox.py):
 //   uniform f32 in (0,1):   ((w >> 9) + 0.5) * 2^-23          (exact in f32)
 //   uniform f64 in (0,1):   (w + 0.5) * 2^-32                  (exact in f64)
-//   normal pair:            double Box-Muller on two f64 uniforms, each
-//                           result rounded once to f32 (device: sincospi).
-// Doing Box-Muller and every log/exp that feeds a decision in double and
-// rounding once makes the GPU and the CPU oracle agree bit-for-bit except when
-// a double result lies within ~1 ulp(f64) of an f32 rounding boundary
-// (probability ~1e-8 per value).
+//   normal pair:            Box-Muller in f32 from IEEE operations only
+//                           (mc_box_muller below): bit-identical on host,
+//                           device and in the NumPy oracle;
+//   log of an accept / slice uniform: mc_logf_unit (the same f32 log).
+// Other f32 log / exp values that feed a decision (dual averaging) are
+// evaluated in double and rounded once (mc_logf_ref / mc_expf_ref): GPU and
+// oracle agree except when a double result lies within ~1 ulp(f64) of an f32
+// rounding boundary (probability ~1e-8 per value).
 #pragma once
 #include <stdint.h>
 #include <math.h>
@@ -72,80 +74,69 @@ MC_HD double mc_u01_f64(uint32_t w) {
     return ((double)w + 0.5) * 2.3283064365386962890625e-10;  // 2^-32
 }
 
-// Box-Muller's double log and sincospi, restricted to the arguments the
-// uniforms produce (the device math library's general versions handle every
-// special case and cost ~90 / ~60 VALU; these ~40 each, and the samplers draw
-// 3 normals and 2 accept logs per lane and iteration):
-//   mc_log_unit(x), x in [2^-40, 1]: fdlibm's e_log.c reduction and minimax
-//     polynomial (k ln2 + log(1 + f), f in [sqrt(2)/2 - 1, sqrt(2) - 1),
-//     < 1 ulp);
-//   mc_sincospi_unit(x), x in [0, 2): sin / cos(pi x) from the quadrant
-//     n = rint(2x) (exact: x has <= 33 significant bits) and fdlibm's
-//     __kernel_sin / __kernel_cos on pi (x - n / 2), |.| <= pi / 4 (< 1 ulp).
-// Both use only IEEE +, -, *, / (built with -ffp-contract=off: no FMA), so
-// host and device agree bit for bit; tests/test_golden.py checks them
-// against libm.
-MC_HD double mc_log_unit(double x) {
-    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
-    const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
-                 Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
-                 Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
-                 Lg7 = 1.479819860511658591e-01;
+// Box-Muller in single precision from IEEE operations only (+, -, *, /,
+// correctly rounded sqrt; built with -ffp-contract=off), so that host, device
+// and the NumPy oracle (oracle/philox.py: the same operations in float32)
+// produce the same bits:
+//   u = (float(w) + 0.5) 2^-32  (w rounded to f32 once, then exact steps);
+//   mc_logf_unit(u), u in (0, 1]: FreeBSD msun e_logf.c's reduction and
+//     minimax polynomial (k ln2 + log(1 + f), f in [sqrt(2)/2 - 1, sqrt(2) - 1));
+//   mc_sincospif_unit(x), x in [0, 2]: quadrant n = rint(2x), r = x - n/2
+//     (exact), Taylor polynomials of sin / cos on pi r, |pi r| <= pi/4.
+// Each normal is within a few ulp(f32) of the exact transform of its
+// uniforms (tests/test_golden.py).  A double-precision transform costs ~3x
+// the VALU: 3.6 % of the bench kernel's time on MI355X (three normals per
+// lane and iteration, profiles/r3/ab).
+MC_HD float mc_logf_unit(float x) {
+    const float ln2_hi = 0x1.62e300p-1f, ln2_lo = 0x1.2fefa2p-17f;  // (exact f32 values)
+    const float Lg1 = 0x1.555554p-1f, Lg2 = 0x1.999c26p-2f, Lg3 = 0x1.23d3dcp-2f,
+                Lg4 = 0x1.f13c4cp-3f;
     int k;
-    double m = frexp(x, &k);                 // x = m 2^k, m in [0.5, 1)
-    if (m < 0.70710678118654752440) {        // m in [sqrt(2)/2, sqrt(2))
-        m = m * 2.0;
+    float m = frexpf(x, &k);                 // x = m 2^k, m in [0.5, 1)
+    if (m < 0x1.6a09e6p-1f) {               // m in [sqrt(2)/2, sqrt(2))
+        m = m * 2.0f;
         k -= 1;
     }
-    const double f = m - 1.0;                // exact
-    const double s = f / (2.0 + f);
-    const double dk = (double)k;
-    const double z = s * s, w = z * z;
-    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
-    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
-    const double R = t2 + t1;
-    const double hfsq = 0.5 * f * f;
+    const float f = m - 1.0f;                // exact
+    const float s = f / (2.0f + f);
+    const float dk = (float)k;
+    const float z = s * s, w = z * z;
+    const float t1 = w * (Lg2 + w * Lg4);
+    const float t2 = z * (Lg1 + w * Lg3);
+    const float R = t2 + t1;
+    const float hfsq = 0.5f * f * f;
     return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
 }
-MC_HD void mc_sincospi_unit(double x, double* sp, double* cp) {
-    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-    const double n = rint(2.0 * x);          // quadrant 0..4
-    const double r = x - 0.5 * n;            // exact, |r| <= 1/4
-    const double t = r * 3.14159265358979311600e+00;
-    const double z = t * t;
-    const double v = z * t;
-    const double sr = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
-    const double sn = t + v * (S1 + z * sr);
-    const double cr = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
-    const double hz = 0.5 * z;
-    const double w = 1.0 - hz;
-    const double cs = w + (((1.0 - w) - hz) + z * cr);
+MC_HD void mc_sincospif_unit(float x, float* sp, float* cp) {
+    const float S1 = -0x1.555556p-3f, S2 = 0x1.111112p-7f, S3 = -0x1.a01a02p-13f,
+                S4 = 0x1.71de3ap-19f;  // f32(-1/3!), f32(1/5!), ...
+    const float C1 = 0x1.555556p-5f, C2 = -0x1.6c16c2p-10f, C3 = 0x1.a01a02p-16f,
+                C4 = -0x1.27e4fcp-22f;  // f32(1/4!), f32(-1/6!), ...
+    const float n = rintf(2.0f * x);         // quadrant 0..4
+    const float r = x - 0.5f * n;            // exact, |r| <= 1/4
+    const float t = r * 0x1.921fb6p+1f;     // f32(pi)
+    const float z = t * t;
+    const float sn = t + (t * z) * (S1 + z * (S2 + z * (S3 + z * S4)));
+    const float cs = (1.0f - 0.5f * z) + (z * z) * (C1 + z * (C2 + z * (C3 + z * C4)));
     const int q = ((int)n) & 3;
     *sp = q == 0 ? sn : (q == 1 ? cs : (q == 2 ? -sn : -cs));
     *cp = q == 0 ? cs : (q == 1 ? -sn : (q == 2 ? -cs : sn));
 }
+MC_HD float mc_u01_boxf(uint32_t w) { return ((float)w + 0.5f) * 0x1p-32f; }
 
-// Device only.  cos / sin of 2 pi u2 through sincospi(2 u2) (2 u2 is exact):
-// one call, no Payne-Hanek reduction; the f64 values agree with the oracle's
-// numpy cos / sin(2 pi u2) to ~1 ulp(f64), so the f32 results are identical
-// except within ~1 ulp(f64) of an f32 rounding boundary.
+// The normal pair of two Philox words.
 MC_HD void mc_box_muller(uint32_t a, uint32_t b, float* z0, float* z1) {
-    const double u1 = mc_u01_f64(a);
-    const double u2 = mc_u01_f64(b);
-    const double r = sqrt(-2.0 * mc_log_unit(u1));
-    double s, c;
-    mc_sincospi_unit(2.0 * u2, &s, &c);
-    *z0 = (float)(r * c);
-    *z1 = (float)(r * s);
+    const float u1 = mc_u01_boxf(a);
+    const float u2 = mc_u01_boxf(b);
+    const float r = sqrtf(-2.0f * mc_logf_unit(u1));
+    float s, c;
+    mc_sincospif_unit(2.0f * u2, &s, &c);
+    *z0 = r * c;
+    *z1 = r * s;
 }
 
 // f32 log / exp "as IEEE would round them": evaluated in double, rounded once.
 MC_HD float mc_logf_ref(float x) { return (float)log((double)x); }
-// The same for a uniform in (0, 1] (accept / slice draws): mc_log_unit.
-MC_HD float mc_logf_u01(float u) { return (float)mc_log_unit((double)u); }
+// The log of an accept / slice uniform in (0, 1]: mc_logf_unit.
+MC_HD float mc_logf_u01(float u) { return mc_logf_unit(u); }
 MC_HD float mc_expf_ref(float x) { return (float)exp((double)x); }

@@ -75,12 +75,67 @@ def u01_f64(w):
     return (np.asarray(w, np.uint32).astype(np.float64) + 0.5) * 2.0 ** -32
 
 
+F32 = np.float32
+_fx = float.fromhex
+# mlx-mcmc_amd/csrc/philox.h mc_logf_unit / mc_sincospif_unit constants (exact f32)
+_LN2_HI, _LN2_LO = F32(_fx("0x1.62e300p-1")), F32(_fx("0x1.2fefa2p-17"))
+_LG = [F32(_fx(h)) for h in ("0x1.555554p-1", "0x1.999c26p-2", "0x1.23d3dcp-2", "0x1.f13c4cp-3")]
+_SQRT_HALF = F32(_fx("0x1.6a09e6p-1"))
+_S = [F32(_fx(h)) for h in ("-0x1.555556p-3", "0x1.111112p-7", "-0x1.a01a02p-13",
+                            "0x1.71de3ap-19")]
+_C = [F32(_fx(h)) for h in ("0x1.555556p-5", "-0x1.6c16c2p-10", "0x1.a01a02p-16",
+                            "-0x1.27e4fcp-22")]
+_PI = F32(_fx("0x1.921fb6p+1"))
+
+
+def u01_boxf(w):
+    """(float32(w) + 0.5) * 2^-32 (philox.h mc_u01_boxf)."""
+    return (np.asarray(w, np.uint32).astype(np.float32) + F32(0.5)) * F32(2.0 ** -32)
+
+
+def logf_unit(x):
+    """philox.h mc_logf_unit: float32 log of x in (0, 1], the same IEEE
+    operations in the same order (FreeBSD msun e_logf.c's reduction and
+    polynomial)."""
+    x = np.asarray(x, np.float32)
+    m, k = np.frexp(x)
+    small = m < _SQRT_HALF
+    m = np.where(small, m * F32(2.0), m).astype(np.float32)
+    k = np.where(small, k - 1, k)
+    f = m - F32(1.0)
+    s = f / (F32(2.0) + f)
+    dk = k.astype(np.float32)
+    z = s * s
+    w = z * z
+    t1 = w * (_LG[1] + w * _LG[3])
+    t2 = z * (_LG[0] + w * _LG[2])
+    R = t2 + t1
+    hfsq = F32(0.5) * f * f
+    return (dk * _LN2_HI - ((hfsq - (s * (hfsq + R) + dk * _LN2_LO)) - f)).astype(np.float32)
+
+
+def sincospif_unit(x):
+    """philox.h mc_sincospif_unit: float32 (sin, cos)(pi x), x in [0, 2]."""
+    x = np.asarray(x, np.float32)
+    n = np.rint(F32(2.0) * x).astype(np.float32)
+    r = x - F32(0.5) * n
+    t = r * _PI
+    z = t * t
+    sn = t + (t * z) * (_S[0] + z * (_S[1] + z * (_S[2] + z * _S[3])))
+    cs = (F32(1.0) - F32(0.5) * z) + (z * z) * (_C[0] + z * (_C[1] + z * (_C[2] + z * _C[3])))
+    q = n.astype(np.int64) & 3
+    s_out = np.select([q == 0, q == 1, q == 2], [sn, cs, -sn], -cs).astype(np.float32)
+    c_out = np.select([q == 0, q == 1, q == 2], [cs, -sn, -cs], sn).astype(np.float32)
+    return s_out, c_out
+
+
 def box_muller(a, b):
-    u1 = u01_f64(a)
-    u2 = u01_f64(b)
-    r = np.sqrt(-2.0 * np.log(u1))
-    t = 6.283185307179586 * u2
-    return (r * np.cos(t)).astype(np.float32), (r * np.sin(t)).astype(np.float32)
+    """philox.h mc_box_muller: the float32 pair of two words (bit-identical)."""
+    u1 = u01_boxf(a)
+    u2 = u01_boxf(b)
+    r = np.sqrt(F32(-2.0) * logf_unit(u1)).astype(np.float32)
+    s, c = sincospif_unit(F32(2.0) * u2)
+    return (r * c).astype(np.float32), (r * s).astype(np.float32)
 
 
 def normals4(words):
@@ -106,6 +161,11 @@ def proposal_noise(seed, chain, it, D):
 
 def uniform(seed, chain, it, tag, sub=0, index=0, word=0):
     return u01_f32(draw(seed, chain, it, tag, sub, index)[..., word])
+
+
+def logf_u01(u):
+    """float32 log of an accept / slice uniform (philox.h mc_logf_u01)."""
+    return np.float32(logf_unit(np.float32(u)))
 
 
 def logf_ref(x):

@@ -144,7 +144,7 @@ def hmc(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_siz
         pp = -pp  # hmc.py:136 (no effect on H)
         H_prop = M.hamiltonian(qp, pp)
         ratio = F32(-(H_prop - H_init))
-        log_u = R.logf_ref(R.uniform(seed, chain, it, R.TAG_ACCEPT))
+        log_u = R.logf_u01(R.uniform(seed, chain, it, R.TAG_ACCEPT))
         accepted = bool(log_u < ratio)
         if record:
             trace["accepted"].append(accepted)
@@ -197,7 +197,7 @@ def metropolis_hastings(log_prob_fn, initial_params, num_samples=1000, proposal_
         lpp = M.logp(qp)
         with np.errstate(invalid="ignore", over="ignore"):
             ratio = F32(lpp - lp)
-        log_u = R.logf_ref(R.uniform(random_seed, chain, i, R.TAG_ACCEPT))
+        log_u = R.logf_u01(R.uniform(random_seed, chain, i, R.TAG_ACCEPT))
         accepted = bool(log_u < ratio)
         if accepted:
             q, lp = qp, lpp
@@ -307,7 +307,7 @@ def nuts(log_prob_fn, initial_params, num_samples=1000, num_warmup=1000, step_si
         r = R.momentum(seed, chain, it, M.D)
         H0 = M.hamiltonian(theta, r)
         U = R.uniform(seed, chain, it, R.TAG_SLICE)
-        log_u = float(F32(-H0)) + float(R.logf_ref(U))
+        log_u = float(F32(-H0)) + float(R.logf_u01(U))
         logu = _slice_log_u(log_u, slice_mode)
         theta_minus = theta_plus = theta
         r_minus = r_plus = r

@@ -40,7 +40,7 @@ def _run(chain):
     r = S.hmc(lp, init, seed=0, chain=chain, record=True, **TRACE)
     n = TRACE["num_warmup"] + TRACE["num_samples"]
     out = {"samples": r.samples,
-           "log_u": np.array([R.logf_ref(R.uniform(0, chain, i, R.TAG_ACCEPT)) for i in range(n)],
+           "log_u": np.array([R.logf_u01(R.uniform(0, chain, i, R.TAG_ACCEPT)) for i in range(n)],
                              np.float32)}
     for k in ("accepted", "ratio", "step_size", "energy"):
         out[k] = np.asarray(r.trace[k])

@@ -66,7 +66,7 @@ def _run(job):
     out = {"samples": r.samples, "step_size": r.step_size, "accept_rate": r.accept_rate}
     if kind == "trace":
         n = cfg["num_warmup"] + cfg["num_samples"]
-        out["log_u"] = np.array([R.logf_ref(R.uniform(0, chain, i, R.TAG_ACCEPT))
+        out["log_u"] = np.array([R.logf_u01(R.uniform(0, chain, i, R.TAG_ACCEPT))
                                  for i in range(n)], np.float32)
         for k in ("accepted", "ratio", "step_size", "energy"):
             out["t_" + k] = np.asarray(r.trace[k])

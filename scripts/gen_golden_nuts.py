@@ -64,7 +64,7 @@ def _run(job):
     r = S.nuts(lp, init, seed=SEED, chain=chain, **cfg)
     n = cfg["num_warmup"] + cfg["num_samples"]
     out = {k: np.asarray(r.trace[k], np.float64) for k in KEYS}
-    out["log_u"] = np.array([R.logf_ref(R.uniform(SEED, chain, i, R.TAG_SLICE))
+    out["log_u"] = np.array([R.logf_u01(R.uniform(SEED, chain, i, R.TAG_SLICE))
                              for i in range(n)], np.float32)
     out["samples"] = r.samples
     return name, chain, out

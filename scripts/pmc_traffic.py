@@ -4,7 +4,9 @@ profiles/pmc_traffic.json (read by bench.py for roofline.traffic).
 HBM bytes per launch of the dominant kernel = (2 * FETCH_SIZE + WRITE_SIZE) * 1024:
 FETCH_SIZE and WRITE_SIZE are kilobytes; on gfx950 FETCH_SIZE counts half the
 bytes of wide streaming reads (MI355X_MICROARCH.md, HBM section), so it is
-doubled.  Usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> <shape>"""
+doubled.  Usage: python scripts/pmc_traffic.py <fetch_dir> <write_dir> <shape> <iters per launch> [label]
+Records are keyed "<shape>@<iters per launch>" (bench.py pmc_traffic): a
+launch's fixed bytes (the slice blocks, once per launch) do not scale."""
 import csv
 import glob
 import json
@@ -37,7 +39,9 @@ def main():
     wk = sum(w.values()) / max(len(w), 1)
     out_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
-    data[shape] = {
+    key = f"{shape}@{ipl}"
+    data.pop(shape, None)  # (round-2 records were keyed by shape alone)
+    data[key] = {
         "kernel": kern,
         "dispatches": [len(f), len(w)],
         "iters_per_launch": ipl,
@@ -45,9 +49,10 @@ def main():
         "write_kb_per_launch": wk,
         "hbm_bytes_per_launch": (2.0 * fk + wk) * 1024.0,
         "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction)",
+        "profile": sys.argv[5] if len(sys.argv) > 5 else "",
     }
     json.dump(data, open(out_path, "w"), indent=1)
-    print(json.dumps(data[shape]))
+    print(json.dumps(data[key]))
 
 
 if __name__ == "__main__":

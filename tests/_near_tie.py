@@ -55,5 +55,5 @@ def log_u(seed, chain, n_iter):
     """f32 log U of the accept draws (the shared Philox stream, oracle/philox.py)."""
     from oracle import philox as R
 
-    return np.array([R.logf_ref(R.uniform(seed, chain, i, R.TAG_ACCEPT)) for i in range(n_iter)],
+    return np.array([R.logf_u01(R.uniform(seed, chain, i, R.TAG_ACCEPT)) for i in range(n_iter)],
                     np.float32)

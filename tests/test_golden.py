@@ -148,7 +148,7 @@ def test_large_trace_fixture_is_mixed():
     from oracle import philox as R
 
     c = int(fx["chains"][2])
-    assert fx["log_u"][2][5] == R.logf_ref(R.uniform(0, c, 5, R.TAG_ACCEPT))
+    assert fx["log_u"][2][5] == R.logf_u01(R.uniform(0, c, 5, R.TAG_ACCEPT))
 
 
 def test_oracle_nuts_fixture_replay_and_dual_averaging():
@@ -178,11 +178,13 @@ def test_oracle_nuts_fixture_replay_and_dual_averaging():
     assert fx["depth"].max() >= 5
 
 
-def test_box_muller_and_unit_log_match_libm():
-    """The samplers' Box-Muller (philox.h mc_box_muller: fdlibm-style log and
-    sincospi restricted to the uniforms' range) against the oracle's numpy
-    formula (oracle/philox.py box_muller) and libm, on the host build of the
-    same code (mc_box_muller_host / mc_log_unit_host)."""
+def test_box_muller_and_unit_log_host_bit_exact():
+    """The samplers' Box-Muller and uniform log (philox.h mc_box_muller /
+    mc_logf_unit: IEEE float32 operations only) on the host build of the same
+    code (mc_box_muller_host / mc_logf_unit_host) are bit-identical to the
+    oracle's NumPy float32 restatement (oracle/philox.py box_muller /
+    logf_unit), edge words included, and within a few ulp of the exact
+    transform of the same uniforms."""
     import ctypes
 
     from mlx_mcmc_amd import _lib
@@ -192,21 +194,27 @@ def test_box_muller_and_unit_log_match_libm():
     rng = np.random.default_rng(5)
     n = 400_000
     w = rng.integers(0, 2 ** 32, size=(n, 2), dtype=np.uint64).astype(np.uint32)
-    w[:64, 0] = np.arange(64)                       # u1 at the smallest values
-    w[64:128, 1] = 2 ** 32 - 1 - np.arange(64)      # angles next to 2 pi
+    w[:256, 0] = np.arange(256)                     # u1 at the smallest values
+    w[256:512, 0] = 2 ** 32 - 1 - np.arange(256)    # u1 -> 1 (r -> 0)
+    w[512:4608, 1] = (np.arange(4096) * (2 ** 32 // 4096)).astype(np.uint32)  # quadrant edges
     out = np.zeros((n, 2), np.float32)
     assert lib.mc_box_muller_host(w.ctypes.data_as(ctypes.c_void_p), n,
                                   out.ctypes.data_as(ctypes.c_void_p)) == 0
     z0, z1 = R.box_muller(w[:, 0], w[:, 1])
-    ref = np.stack([z0, z1], axis=1)
-    diff = out != ref
-    # differences only where the oracle's own angle rounding (2 pi u2 in f64)
-    # moves a value next to a zero of sin / cos: tiny values, a few f32 ulp
-    assert diff.sum() <= 16, diff.sum()
-    assert np.all(np.abs(out[diff] - ref[diff]) <= 1e-6 * np.maximum(np.abs(ref[diff]), 1e-3))
-    x = R.u01_f64(w[:, 0])
-    lg = np.zeros(n)
-    assert lib.mc_log_unit_host(x.ctypes.data_as(ctypes.c_void_p), n,
-                                lg.ctypes.data_as(ctypes.c_void_p)) == 0
-    ulps = np.abs(lg - np.log(x)) / np.spacing(np.abs(np.log(x)))
-    assert ulps.max() <= 1.0, ulps.max()
+    np.testing.assert_array_equal(out[:, 0], z0)
+    np.testing.assert_array_equal(out[:, 1], z1)
+    # accuracy against the exact transform of the same f32 uniforms
+    u1 = R.u01_boxf(w[:, 0]).astype(np.float64)
+    u2 = R.u01_boxf(w[:, 1]).astype(np.float64)
+    r = np.sqrt(-2.0 * np.log(u1))
+    for got, ex in ((z0, r * np.cos(2 * np.pi * u2)), (z1, r * np.sin(2 * np.pi * u2))):
+        big = np.abs(ex) > 1e-3
+        ulp = np.abs(got[big] - ex[big]) / np.spacing(np.abs(ex[big]).astype(np.float32))
+        assert ulp.max() <= 4.0, ulp.max()
+    u = R.u01_f32(w[:, 0])
+    lg = np.zeros(n, np.float32)
+    assert lib.mc_logf_unit_host(u.ctypes.data_as(ctypes.c_void_p), n,
+                                 lg.ctypes.data_as(ctypes.c_void_p)) == 0
+    np.testing.assert_array_equal(lg, R.logf_unit(u))
+    ex = np.log(u.astype(np.float64))
+    assert (np.abs(lg - ex) / np.spacing(np.abs(ex).astype(np.float32))).max() <= 1.0
