@@ -122,13 +122,8 @@ MC_DEV f2 lf_hi_minus(f2 xy, f2 th) {
 // parameter th) for both chains, packed FP32: d = x - th, s1 += d,
 // s2 = fma(d, d, s2), with the even and odd elements in separate packed
 // accumulators (two independent dependency chains each).
-MC_DEV void lf_moments(const float* xv, int len, int lmin4, f2 th, f2& s1, f2& s2) {
+MC_DEV void lf_moments(const float* xv, int len, int lmin4, int lmax, f2 th, f2& s1, f2& s2) {
     f2 a1[2] = {{0.f, 0.f}, {0.f, 0.f}}, a2[2] = {{0.f, 0.f}, {0.f, 0.f}};
-    auto elem = [&](float x, int hh) {
-        const f2 d = (f2){x, x} - th;
-        a1[hh] += d;
-        a2[hh] = pk_fma(d, d, a2[hh]);
-    };
     // a register pair's elements broadcast by swizzle (op_sel on the pair,
     // no copy of the odd register)
     auto pair = [&](f2 xy) {
@@ -174,23 +169,27 @@ MC_DEV void lf_moments(const float* xv, int len, int lmin4, f2 th, f2& s1, f2& s
             if (!more_a) break;
         }
     }
-    // the lane's remaining full groups (a lane-varying count), then its last
-    // partial group: elements in the accumulators of their parity, no
-    // per-element accumulator select
-    const int len4 = len >> 2;
-    for (; u4 < len4; ++u4) {
+    // the groups every lane holds in full (uniform), then the ragged end:
+    // element e of the lanes with more elements (e < lmax, uniform bounds),
+    // masked per lane (the tile is padded to whole groups, so every load is
+    // in bounds); no exec-masked loop, no per-lane branch
+    for (; u4 < lmin4; ++u4) {
         const float4 a = *(const float4*)(xv + u4 * 256);
-        elem(a.x, 0);
-        elem(a.y, 1);
-        elem(a.z, 0);
-        elem(a.w, 1);
+        pair((f2){a.x, a.y});
+        pair((f2){a.z, a.w});
     }
-    const int rem = len & 3;
-    if (rem) {
-        const float4 a = *(const float4*)(xv + u4 * 256);
-        elem(a.x, 0);
-        if (rem > 1) elem(a.y, 1);
-        if (rem > 2) elem(a.z, 0);
+    const f2 z = {0.f, 0.f};
+    for (int e = 4 * lmin4; e < lmax; e += 4) {
+        const float4 a = *(const float4*)(xv + (e >> 2) * 256);
+        const float x[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (e + k >= lmax) break;  // (uniform)
+            f2 d = (f2){x[k], x[k]} - th;
+            d = (e + k < len) ? d : z;
+            a1[k & 1] += d;
+            a2[k & 1] = pk_fma(d, d, a2[k & 1]);
+        }
     }
     s1 = a1[0] + a1[1];
     s2 = a2[0] + a2[1];
@@ -379,13 +378,14 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     // per slot: the swept term's run (data pointer, length, full float4
     // groups of every lane) and the direct term's presence
     const float* xv[RS];
-    int len[RS], lmin4[RS];
+    int len[RS], lmin4[RS], lmax[RS];
     f2 cnt[RS];
     bool pdir[RS];
 #pragma unroll
     for (int r = 0; r < RS; ++r) {
         len[r] = 0;
         lmin4[r] = 0;
+        lmax[r] = 0;
         xv[r] = sd;
         if (SW && r < tt[0].nslot) {
             len[r] = ((const int32_t*)sd)[tt[0].len_off + r * 64 + j];
@@ -393,6 +393,13 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             xv[r] = sd + tt[0].doff[0] + tt[0].toff[r] + 4 * j;
         }
         cnt[r] = bc2((float)len[r]);
+        // the slot's longest run (uniform: a wave max, once per launch)
+        {
+            int m = len[r];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) m = max(m, __shfl_xor(m, o));
+            lmax[r] = __builtin_amdgcn_readfirstlane(m);
+        }
         pdir[r] = DIR && r < tt[nsweep].nslot &&
                   ((const int32_t*)sd)[tt[nsweep].len_off + r * 64 + j] > 0;
     }
@@ -411,7 +418,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         for (int r = 0; r < RS; ++r) {
             s1[r] = (f2){0.f, 0.f};
             s2[r] = (f2){0.f, 0.f};
-            if (len[r] > 0) lf_moments(xv[r], len[r], lmin4[r], q[r], s1[r], s2[r]);
+            if (len[r] > 0) lf_moments(xv[r], len[r], lmin4[r], lmax[r], q[r], s1[r], s2[r]);
         }
     };
 
