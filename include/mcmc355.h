@@ -76,7 +76,11 @@ typedef enum {
     MC_DIST_HALFNORMAL  = 1,  /* halfnormal.py:34-63   (value, -, scale)     */
     MC_DIST_EXPONENTIAL = 2,  /* exponential.py:48-71  (value, -, rate)      */
     MC_DIST_GAMMA       = 3,  /* gamma.py:40-88        (value, alpha, beta)  */
-    MC_DIST_BETA        = 4   /* beta.py:37-91         (value, alpha, beta)  */
+    MC_DIST_BETA        = 4,  /* beta.py:37-91         (value, alpha, beta)  */
+    MC_DIST_IDENTITY    = 5   /* weight * sum_i value_i   (value, -, -):  a   */
+                              /* parameter expression added to the log      */
+                              /* density (the Jacobian of a reparameterised */
+                              /* parameter, `lp + log_sigma`)               */
 } mc_dist_kind;
 
 typedef enum {
@@ -88,12 +92,24 @@ typedef enum {
     MC_OP_GATHER  = 5   /* q[param_offset + index[pool_offset + i]] (int32)  */
 } mc_operand_kind;
 
+/* An elementwise transform of a parameter operand (PSCALAR / PVEC / GATHER),
+ * applied in f32 before the term reads it, its derivative applied to the
+ * operand's cotangent as mx.grad's VJPs do (exp: c * exp(x); log: c / x):
+ * `Normal(mu, mx.exp(log_sigma))`, `Normal(0, 1).log_prob(mx.log(x))`.      */
+typedef enum {
+    MC_XF_NONE = 0,
+    MC_XF_EXP  = 1,
+    MC_XF_LOG  = 2
+} mc_transform_kind;
+
 typedef struct mc_operand {
     int32_t kind;          /* mc_operand_kind                               */
     int32_t param_offset;  /* PSCALAR / PVEC / GATHER                       */
     int64_t pool_offset;   /* DATA: float pool; GATHER: index pool          */
     float   value;         /* CONST                                         */
-    int32_t reserved;
+    int32_t transform;     /* mc_transform_kind (parameter operands only;   */
+                           /* was `reserved`: zero-initialised callers get  */
+                           /* MC_XF_NONE)                                   */
 } mc_operand;
 
 typedef struct mc_term {

@@ -38,6 +38,7 @@ MC_DIST_HALFNORMAL = 1
 MC_DIST_EXPONENTIAL = 2
 MC_DIST_GAMMA = 3
 MC_DIST_BETA = 4
+MC_DIST_IDENTITY = 5
 
 # mc_series_stats fields (include/mcmc355.h)
 MC_ST_ESS, MC_ST_MEAN, MC_ST_M2, MC_ST_HMEAN0, MC_ST_HMEAN1, MC_ST_HM2_0, MC_ST_HM2_1 = range(7)
@@ -49,6 +50,10 @@ MC_OP_PSCALAR = 2
 MC_OP_DATA = 3
 MC_OP_PVEC = 4
 MC_OP_GATHER = 5
+
+MC_XF_NONE = 0
+MC_XF_EXP = 1
+MC_XF_LOG = 2
 
 MC_RNG_TAG_MOMENTUM = 1
 MC_RNG_TAG_ACCEPT = 2
@@ -65,7 +70,7 @@ class McOperand(ctypes.Structure):
         ("param_offset", ctypes.c_int32),
         ("pool_offset", ctypes.c_int64),
         ("value", ctypes.c_float),
-        ("reserved", ctypes.c_int32),
+        ("transform", ctypes.c_int32),
     ]
 
 

@@ -25,8 +25,17 @@ constant or scalar parameter, ``x`` a data array, a parameter vector / slice
 or an injective gather, ``a`` a constant, scalar parameter, data array,
 parameter vector or injective gather — linear regression ``Normal(a + b * x,
 sigma)``, non-centred hierarchies ``Normal(mu + tau * z, sigma_j)``.  It is
-accepted as a Normal ``loc`` only (mc_affine in include/mcmc355.h); anything
-else (two products, ``mx.log(sigma)``, a product of two parameters used as a
+accepted as a Normal ``loc`` only (mc_affine in include/mcmc355.h).
+
+Reparameterised models: ``mx.exp(p)`` / ``mx.log(p)`` of a parameter (or a
+slice / element / gather of one) is a *transformed* parameter operand
+(mc_transform_kind), usable wherever a parameter is — ``Normal(mu,
+mx.exp(log_sigma))``, ``HalfNormal(1).log_prob(mx.exp(log_tau))``,
+``mu + mx.exp(log_tau) * z``, ``Normal(0, 1).log_prob(mx.log(x))``; and a
+parameter expression added to a log density (``lp + log_sigma``, the
+Jacobian of the transform; ``lp - mx.log(x)``; ``mx.sum(log_x)``) is an
+*identity* term ``weight * sum_i value_i`` (MC_DIST_IDENTITY).  Anything else
+(two products, exp of an expression, a product of two parameters used as a
 scale ...) raises ``TraceError``.
 """
 from __future__ import annotations
@@ -59,13 +68,22 @@ class Param:
 
     __array_priority__ = 1000  # make NumPy defer to our operators
 
-    def __init__(self, name: str, offset: int, shape: Tuple[int, ...], view=None):
+    def __init__(self, name: str, offset: int, shape: Tuple[int, ...], view=None, xf: int = 0):
         self.name = name
         self.offset = offset          # flat offset of the base parameter
         self.base_shape = shape
         # view: None (whole param), ('elem', flat_index), ('slice', start, len),
         # ('gather', int32 index array relative to `offset`)
         self.view = view
+        self.xf = xf  # mc_transform_kind: mx.exp / mx.log of the parameter (view)
+
+    def transformed(self, xf: int, fn: str) -> "Param":
+        """mx.exp / mx.log of this parameter (view): elementwise, so it commutes
+        with the view."""
+        if self.xf:
+            raise TraceError(f"mx.{fn} of a transformed parameter: one mx.exp / mx.log of a "
+                             "parameter traces; " + _UNSUPPORTED)
+        return Param(self.name, self.offset, self.base_shape, self.view, xf)
 
     @property
     def shape(self) -> Tuple[int, ...]:
@@ -106,13 +124,13 @@ class Param:
                 i += length
             if not 0 <= i < length:
                 raise IndexError(f"index {idx} out of range for parameter '{self.name}'")
-            return Param(self.name, self.offset, self.base_shape, ("elem", base + i))
+            return Param(self.name, self.offset, self.base_shape, ("elem", base + i), self.xf)
         if isinstance(idx, slice):
             start, stop, step = idx.indices(length)
             if step != 1:
                 raise TraceError("strided parameter slices are not supported")
             return Param(self.name, self.offset, self.base_shape,
-                         ("slice", base + start, max(0, stop - start)))
+                         ("slice", base + start, max(0, stop - start)), self.xf)
         arr = np.asarray(idx)
         if arr.dtype.kind not in "iu":
             raise TraceError("parameters can only be gathered by an integer index array")
@@ -121,7 +139,7 @@ class Param:
         if arr.size and (arr.min() < 0 or arr.max() >= length):
             raise IndexError(f"gather index out of range for parameter '{self.name}'")
         return Param(self.name, self.offset, self.base_shape,
-                     ("gather", (base + arr).astype(np.int32).ravel(), arr.shape))
+                     ("gather", (base + arr).astype(np.int32).ravel(), arr.shape), self.xf)
 
     def _unsupported(self, *a, **k):
         raise TraceError(f"arithmetic on traced parameter '{self.name}': " + _UNSUPPORTED)
@@ -133,12 +151,18 @@ class Param:
     __rmul__ = __mul__
 
     def __add__(self, other):
+        if isinstance(other, LogProbExpr):
+            return other + self
         return Affine.lift(self) + other
 
     def __radd__(self, other):
+        if isinstance(other, LogProbExpr):
+            return other + self
         return Affine.lift(self) + other
 
     def __sub__(self, other):
+        if isinstance(other, LogProbExpr):
+            return (-other) + self
         return Affine.lift(self) + (-1.0) * other if not isinstance(other, Affine) else \
             Affine.lift(self) + other * -1.0
 
@@ -158,7 +182,8 @@ class Param:
     __bool__ = __int__ = __float__
 
     def __repr__(self):
-        return f"Param({self.name}, view={self.view})"
+        xf = {1: "exp ", 2: "log "}.get(self.xf, "")
+        return f"Param({xf}{self.name}, view={self.view})"
 
 
 def _is_slope(x) -> bool:
@@ -205,7 +230,7 @@ class Affine:
         else:
             raise TraceError("a product of two vectors: only loc + slope * x (slope a constant "
                              "or scalar parameter) traces; " + _UNSUPPORTED)
-        if isinstance(x, Param) and x.shape == ():
+        if isinstance(x, Param) and x.shape == () and isinstance(slope, Param):
             raise TraceError("a product of two scalar parameters: " + _UNSUPPORTED)
         if not isinstance(x, Param) and not isinstance(slope, Param):
             raise TraceError("a constant product outside a parameter expression")
@@ -213,7 +238,7 @@ class Affine:
 
     def __add__(self, other):
         if isinstance(other, LogProbExpr):
-            raise TraceError("adding a parameter expression to a log density: " + _UNSUPPORTED)
+            return other + self
         o = Affine.lift(other)
         if self.x is not None and o.x is not None:
             raise TraceError("a sum of two products (a + b*x + c*z): only loc + slope * x "
@@ -243,6 +268,8 @@ class Affine:
     __radd__ = __add__
 
     def __sub__(self, other):
+        if isinstance(other, LogProbExpr):
+            return (-other) + self
         if isinstance(other, Param):
             return self + Affine.product(-1.0, other)
         if isinstance(other, Affine):
@@ -282,18 +309,19 @@ class Operand:
     data: Optional[np.ndarray] = None    # float32, DATA
     index: Optional[np.ndarray] = None   # int32,   GATHER
     shape: Tuple[int, ...] = ()
+    transform: int = 0                   # mc_transform_kind (parameter operands)
 
     def key(self):
         if self.kind == _lib.MC_OP_CONST:
             return ("c", float(np.float32(self.value)))
         if self.kind == _lib.MC_OP_PSCALAR:
-            return ("p", self.param_offset)
+            return ("p", self.param_offset, self.transform)
         if self.kind == _lib.MC_OP_PVEC:
-            return ("v", self.param_offset, self.shape)
+            return ("v", self.param_offset, self.shape, self.transform)
         if self.kind == _lib.MC_OP_DATA:
             return ("d", id(self.data))
         if self.kind == _lib.MC_OP_GATHER:
-            return ("g", self.param_offset, id(self.index))
+            return ("g", self.param_offset, id(self.index), self.transform)
         return ("n",)
 
 
@@ -304,15 +332,19 @@ def to_operand(x) -> Operand:
     """Classify a distribution argument."""
     if isinstance(x, Param):
         v = x.view
+        xf = x.xf
         if v is None:
             if x.base_shape == ():
-                return Operand(_lib.MC_OP_PSCALAR, param_offset=x.offset)
-            return Operand(_lib.MC_OP_PVEC, param_offset=x.offset, shape=x.base_shape)
+                return Operand(_lib.MC_OP_PSCALAR, param_offset=x.offset, transform=xf)
+            return Operand(_lib.MC_OP_PVEC, param_offset=x.offset, shape=x.base_shape,
+                           transform=xf)
         if v[0] == "elem":
-            return Operand(_lib.MC_OP_PSCALAR, param_offset=x.offset + v[1])
+            return Operand(_lib.MC_OP_PSCALAR, param_offset=x.offset + v[1], transform=xf)
         if v[0] == "slice":
-            return Operand(_lib.MC_OP_PVEC, param_offset=x.offset + v[1], shape=(v[2],))
-        return Operand(_lib.MC_OP_GATHER, param_offset=x.offset, index=v[1], shape=tuple(v[2]))
+            return Operand(_lib.MC_OP_PVEC, param_offset=x.offset + v[1], shape=(v[2],),
+                           transform=xf)
+        return Operand(_lib.MC_OP_GATHER, param_offset=x.offset, index=v[1], shape=tuple(v[2]),
+                       transform=xf)
     if isinstance(x, LogProbExpr):
         raise TraceError("a log density cannot be a distribution argument: " + _UNSUPPORTED)
     if isinstance(x, Affine):
@@ -381,8 +413,8 @@ class LogProbExpr:
                 raise TraceError(f"shape mismatch {self.shape} vs {other.shape}")
             terms = list(self.terms) + [_scaled(t, sign) for t in other.terms]
             return LogProbExpr(terms, self.const + sign * other.const, self.shape)
-        if isinstance(other, Param):
-            raise TraceError("adding a raw parameter to a log density: " + _UNSUPPORTED)
+        if isinstance(other, (Param, Affine)):
+            return self._combine(identity_expr(other), sign)
         c = _scalar_const(other)
         if self.shape != ():
             raise TraceError("adding a constant to an unsummed vector log density")
@@ -423,6 +455,40 @@ class LogProbExpr:
         return f"LogProbExpr({len(self.terms)} terms, shape={self.shape})"
 
 
+def identity_expr(x) -> LogProbExpr:
+    """A parameter expression added to a log density (``lp + log_sigma``,
+    ``lp - mx.log(x)``): identity terms ``weight * value`` (MC_DIST_IDENTITY),
+    unsummed — ``mx.sum`` reduces it like any log density.  Accepted: a
+    parameter or view, transformed or not, times a constant, plus a constant."""
+    const = 0.0
+    weight = 1.0
+    if isinstance(x, Affine):
+        if x.x is None:
+            raise TraceError("adding a parameter loc expression to a log density: "
+                             + _UNSUPPORTED)
+        if isinstance(x.slope, Param):
+            raise TraceError("adding a product of parameters to a log density: " + _UNSUPPORTED)
+        if x.loc is not None:
+            loc = np.asarray(_to_numpy(x.loc))
+            if isinstance(x.loc, Param) or loc.dtype == object or loc.size != 1:
+                raise TraceError("adding a sum of a parameter and a vector to a log density: "
+                                 + _UNSUPPORTED)
+            const = float(loc.reshape(()))
+        weight = float(np.asarray(_to_numpy(x.slope)).reshape(()))
+        x = x.x
+    if not isinstance(x, Param):
+        raise TraceError("adding this expression to a log density: " + _UNSUPPORTED)
+    op = to_operand(x)
+    n, shape = broadcast_n("identity", [op])
+    if op.kind == _lib.MC_OP_GATHER and op.shape == ():
+        op.shape = (1,)
+    if const and shape != ():
+        raise TraceError("adding a parameter vector plus a constant to a log density: "
+                         + _UNSUPPORTED)
+    term = Term(_lib.MC_DIST_IDENTITY, op, NONE_OPERAND, NONE_OPERAND, n, weight)
+    return LogProbExpr([term], const, shape)
+
+
 def _scaled(t: Term, c: float) -> Term:
     return Term(t.dist, t.value, t.loc, t.scale, t.n, t.weight * c, t.aff)
 
@@ -446,6 +512,9 @@ def make_term(dist: int, dist_name: str, value, loc, scale) -> LogProbExpr:
                              + _UNSUPPORTED)
         loc_op, slope_op, x_op = loc.operands()
         if x_op is not None:
+            if x_op.kind == _lib.MC_OP_PSCALAR:
+                raise TraceError("a constant times a scalar parameter as a Normal loc: "
+                                 + _UNSUPPORTED)
             aff = (slope_op, x_op)
     else:
         loc_op = NONE_OPERAND if loc is None else to_operand(loc)
@@ -615,6 +684,7 @@ def _build_pools(model: TracedModel) -> None:
             co.kind = o.kind
             co.param_offset = o.param_offset
             co.value = o.value
+            co.transform = o.transform
             if o.kind == _lib.MC_OP_DATA:
                 co.pool_offset = nd
                 data_parts.append(o.data.astype(np.float32))

@@ -41,8 +41,10 @@ def array(x, dtype=None):
 def sum(x, axis=None, keepdims=False):  # noqa: A001 - mirrors mx.sum
     if isinstance(x, _trace.LogProbExpr):
         return x.sum(axis)
-    if isinstance(x, _trace.Param):
-        raise _trace.TraceError("mx.sum of a raw parameter: " + _trace._UNSUPPORTED)
+    if isinstance(x, (_trace.Param, _trace.Affine)):
+        # a parameter expression summed into a log density (`mx.sum(log_x)`,
+        # the Jacobian of a vector reparameterisation): identity terms
+        return _trace.identity_expr(x).sum(axis)
     return np.sum(np.asarray(x), axis=axis, keepdims=keepdims)
 
 
@@ -56,8 +58,23 @@ def _concrete(name, fn):
     return f
 
 
-log = _concrete("log", np.log)
-exp = _concrete("exp", np.exp)
+def _transform(name, xf, fn):
+    """mx.exp / mx.log: of a traced parameter (or view) a transformed parameter
+    operand (mc_transform_kind); of concrete arrays the NumPy f32 value."""
+    def f(x, *a, **k):
+        if isinstance(x, _trace.Param) and not a and not k:
+            return x.transformed(xf, name)
+        if _trace.is_symbolic(x, *a):
+            raise _trace.TraceError(f"mx.{name} of a traced expression (only of a parameter or "
+                                    "a view of one): " + _trace._UNSUPPORTED)
+        return fn(np.asarray(_trace._to_numpy(x)), *a, **k)
+
+    f.__name__ = name
+    return f
+
+
+log = _transform("log", 2, np.log)
+exp = _transform("exp", 1, np.exp)
 sqrt = _concrete("sqrt", np.sqrt)
 abs = _concrete("abs", np.abs)  # noqa: A001
 mean = _concrete("mean", np.mean)

@@ -349,12 +349,26 @@ static bool has_affine(const mc_program* p) {
         if (t.affine) return true;
     return false;
 }
+// Transformed parameter operands and identity terms (the reparameterised
+// models of mc_transform_kind) run on the chain-per-workgroup kernels.
+static bool has_transform(const mc_program* p) {
+    for (const DevTerm& t : p->raw) {
+        if (t.dist == MC_DIST_IDENTITY) return true;
+        for (int a = 0; a < 3; ++a)
+            if (t.op[a].xf != MC_XF_NONE) return true;
+        if (t.affine && (t.ab.xf != MC_XF_NONE || t.ax.xf != MC_XF_NONE)) return true;
+    }
+    return false;
+}
 
 static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = nullptr) {
     const std::vector<DevTerm>& raw = p->raw;
     if (has_affine(p))
         return fail(MC_ERR_UNSUPPORTED, "affine loc operands run on the chain-per-workgroup "
                     "kernels (not sliceable)");
+    if (has_transform(p))
+        return fail(MC_ERR_UNSUPPORTED, "transformed parameter operands (mx.exp / mx.log) and "
+                    "identity terms run on the chain-per-workgroup kernels (not sliceable)");
     const std::vector<float>& dp = p->h_data;
     const std::vector<int32_t>& ip = p->h_index;
     const int D = p->D;
@@ -1081,7 +1095,7 @@ static int64_t program_elements(const mc_program* p) {
 // stay unsliced (a per-step exchange costs more than the whole evaluation).
 static constexpr int64_t kLrAutoMinElements = 2048;
 static int auto_slices(const mc_program* p) {
-    if (has_affine(p)) return 1;
+    if (has_affine(p) || has_transform(p)) return 1;
     const int64_t n = program_elements(p);
     if (n >= 65536) return 16;
     if (n >= 16384) return 8;
@@ -1264,7 +1278,7 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
 
     for (int32_t t = 0; t < n_terms; ++t) {
         const mc_term& src = terms[t];
-        if (src.dist < MC_DIST_NORMAL || src.dist > MC_DIST_BETA)
+        if (src.dist < MC_DIST_NORMAL || src.dist > MC_DIST_IDENTITY)
             return fail(MC_ERR_INVALID, "term %d: unknown distribution %d", t, src.dist);
         if (src.n < 1) return fail(MC_ERR_INVALID, "term %d: n must be >= 1", t);
         const int64_t n = src.n;
@@ -1302,13 +1316,27 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
             d.pool = o.pool_offset;
             d.cval = o.value;
             d.unique = 1;
+            d.xf = o.transform;
+            if (o.transform < MC_XF_NONE || o.transform > MC_XF_LOG)
+                return fail(MC_ERR_INVALID, "term %d op %d: unknown transform %d", t, a,
+                            o.transform);
+            if (o.transform != MC_XF_NONE && o.kind != MC_OP_PSCALAR && o.kind != MC_OP_PVEC &&
+                o.kind != MC_OP_GATHER)
+                return fail(MC_ERR_INVALID, "term %d op %d: a transform applies to parameter "
+                            "operands only", t, a);
             const bool need =
-                !(a == 1 && (src.dist == MC_DIST_HALFNORMAL || src.dist == MC_DIST_EXPONENTIAL));
+                !(a == 1 && (src.dist == MC_DIST_HALFNORMAL || src.dist == MC_DIST_EXPONENTIAL)) &&
+                !(src.dist == MC_DIST_IDENTITY && (a == 1 || a == 2));
             if (!need) {
                 if (o.kind != MC_OP_NONE && o.kind != MC_OP_CONST)
-                    return fail(MC_ERR_INVALID, "term %d: %s takes no loc operand", t,
-                                src.dist == MC_DIST_HALFNORMAL ? "HalfNormal" : "Exponential");
+                    return fail(MC_ERR_INVALID, "term %d: %s takes no %s operand", t,
+                                src.dist == MC_DIST_HALFNORMAL
+                                    ? "HalfNormal"
+                                    : (src.dist == MC_DIST_EXPONENTIAL ? "Exponential"
+                                                                       : "an identity term"),
+                                a == 1 ? "loc" : "scale");
                 d.kind = MC_OP_NONE;
+                d.xf = MC_XF_NONE;
                 continue;
             }
             switch (o.kind) {

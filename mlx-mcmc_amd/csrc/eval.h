@@ -112,7 +112,7 @@ MC_DEV DevOperand load_op(const MC_CONST DevOperand* p) {
     o.cval = p->cval;
     o.unique = p->unique;
     o.slot = p->slot;
-    o.pad = 0;
+    o.xf = p->xf;
     return o;
 }
 
@@ -341,6 +341,15 @@ MC_DEV ElemOut elem_beta(float v, float a, float b, float lbeta) {
     return o;
 }
 
+// An identity term (MC_DIST_IDENTITY): the value itself, cotangent 1.
+MC_DEV ElemOut elem_identity(float v) {
+    ElemOut o;
+    o.lp = v;
+    o.dv = 1.0f;
+    o.dm = o.ds = 0.0f;
+    return o;
+}
+
 // Every distribution: logs = f32 log of operand slot 2 (scale / rate / beta;
 // unused by Beta), lg = the gammaln normaliser (Gamma, Beta; see lgamma_norm).
 MC_DEV ElemOut elem_eval(int dist, float c0, float v, float m, float s, float logs, float lg) {
@@ -349,6 +358,7 @@ MC_DEV ElemOut elem_eval(int dist, float c0, float v, float m, float s, float lo
         case MC_DIST_HALFNORMAL: return elem_halfnormal(c0, v, s, logs);
         case MC_DIST_EXPONENTIAL: return elem_exponential(v, s, logs);
         case MC_DIST_GAMMA: return elem_gamma(v, m, s, logs, lg);
+        case MC_DIST_IDENTITY: return elem_identity(v);
         default: return elem_beta(v, m, s, lg);
     }
 }
@@ -374,8 +384,24 @@ MC_DEV bool is_vec(int kind) {
     return kind == MC_OP_DATA || kind == MC_OP_PVEC || kind == MC_OP_GATHER;
 }
 
+// Transformed parameter operands (mc_transform_kind): the f32 value a term
+// reads, and the VJP applied to its cotangent c as mx.grad's would be
+// (exp: c * exp(x), from the forward value y; log: c / x).
+MC_DEV float xf_apply(int xf, float x) {
+    return xf == MC_XF_EXP ? expf(x) : (xf == MC_XF_LOG ? logf(x) : x);
+}
+MC_DEV float xf_chain(int xf, float c, float x, float y) {
+    return xf == MC_XF_EXP ? c * y : (xf == MC_XF_LOG ? c / x : c);
+}
+// A PSCALAR operand's cotangent partial through its transform.
+MC_DEV float xf_chain_scalar(const DevOperand& o, float c, const float* q) {
+    if (o.xf == MC_XF_NONE) return c;
+    const float x = q[o.poff];
+    return xf_chain(o.xf, c, x, xf_apply(o.xf, x));
+}
+
 MC_DEV float uniform_value(const DevOperand& o, const float* q) {
-    if (o.kind == MC_OP_PSCALAR) return q[o.poff];
+    if (o.kind == MC_OP_PSCALAR) return xf_apply(o.xf, q[o.poff]);
     if (o.kind == MC_OP_CONST) return o.cval;
     return 0.0f;
 }
@@ -447,7 +473,9 @@ MC_DEV void strided_uscale(const DevTerm& T, const DevCtx& P, const float* q, fl
     M.neg = M.neg || neg;
 }
 
-MC_DEV int fast_kind(int kind) {
+MC_DEV int fast_kind(const DevOperand& o) {
+    const int kind = o.kind;
+    if (o.xf != MC_XF_NONE && is_vec(kind)) return -1;  // transformed vector: generic path
     return kind == MC_OP_DATA ? 1 : (kind == MC_OP_PVEC ? 2 : (is_vec(kind) ? -1 : 0));
 }
 
@@ -456,9 +484,9 @@ MC_DEV float fetch(const DevOperand& o, int64_t i, float uni, const float* q, co
         case MC_OP_DATA:
             return P.data[o.pool + i];
         case MC_OP_PVEC:
-            return q[o.poff + i];
+            return xf_apply(o.xf, q[o.poff + i]);
         case MC_OP_GATHER:
-            return q[o.poff + P.index[o.pool + i]];
+            return xf_apply(o.xf, q[o.poff + P.index[o.pool + i]]);
         default:
             return uni;
     }
@@ -466,17 +494,23 @@ MC_DEV float fetch(const DevOperand& o, int64_t i, float uni, const float* q, co
 
 // Accumulate a per-element cotangent for operand o (never the primary).
 MC_DEV void accum(const DevOperand& o, int64_t i, float c, float& scalar_part, float* g,
-                  const DevCtx& P) {
+                  const float* q, const DevCtx& P) {
     switch (o.kind) {
         case MC_OP_PSCALAR:
-            scalar_part += c;
+            scalar_part += c;  // (its transform: at the slot flush, xf_chain_scalar)
             break;
-        case MC_OP_PVEC:
-            g[o.poff + i] += c;
+        case MC_OP_PVEC: {
+            const int64_t j = o.poff + i;
+            if (o.xf != MC_XF_NONE) c = xf_chain(o.xf, c, q[j], xf_apply(o.xf, q[j]));
+            g[j] += c;
             break;
-        case MC_OP_GATHER:
-            g[o.poff + P.index[o.pool + i]] += c;
+        }
+        case MC_OP_GATHER: {
+            const int64_t j = o.poff + P.index[o.pool + i];
+            if (o.xf != MC_XF_NONE) c = xf_chain(o.xf, c, q[j], xf_apply(o.xf, q[j]));
+            g[j] += c;
             break;
+        }
         default:
             break;
     }
@@ -509,16 +543,16 @@ MC_DEV void strided_generic(const DevTerm& T, const DevCtx& P, const float* q, f
         const float lg = lgv ? lgamma_norm(T.dist, m, s) : ulg;
         const ElemOut e = elem_eval(T.dist, T.c0, v, m, s, logs, lg);
         if (mask & PASS_LP) lp_acc += w * e.lp;
-        if (mask & PASS_VALUE) accum(T.op[0], i, w * e.dv, pv, g, P);
+        if (mask & PASS_VALUE) accum(T.op[0], i, w * e.dv, pv, g, q, P);
         if (mask & PASS_LOC) {
             const float cm = w * e.dm;
-            accum(T.op[1], i, cm, pm, g, P);
+            accum(T.op[1], i, cm, pm, g, q, P);
             if (aff) {
                 pb += cm * xa;
-                accum(T.ax, i, cm * ub, dummy, g, P);
+                accum(T.ax, i, cm * ub, dummy, g, q, P);
             }
         }
-        if (mask & PASS_SCALE) accum(T.op[2], i, w * e.ds, ps, g, P);
+        if (mask & PASS_SCALE) accum(T.op[2], i, w * e.ds, ps, g, q, P);
     }
 }
 
@@ -657,7 +691,7 @@ MC_DEV float seg_fetch(const DevOperand& o, int64_t e, float uni, float prim, bo
         case MC_OP_DATA:
             return P.data[o.pool + e];
         case MC_OP_GATHER:
-            return q[o.poff + P.index[o.pool + e]];
+            return xf_apply(o.xf, q[o.poff + P.index[o.pool + e]]);
         default:
             return uni;
     }
@@ -683,6 +717,7 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
     const float w = T.weight;
     const bool aff = T.affine != 0;  // loc = (gathered) loc + slope * x, x data (tiled)
     const float ub = aff ? uniform_value(T.ab, q) : 0.0f;
+    const int prim_xf = a == 0 ? T.op[0].xf : (a == 1 ? T.op[1].xf : T.op[2].xf);
     for (int t = wave; t < T.ntiles; t += WPC) {
         const int off = tiles[3 * t];
         const int lpad = tiles[3 * t + 1];
@@ -690,7 +725,8 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
         const bool valid = v < T.nvirt;
         const int k = valid ? lanes[2 * v] : 0;
         const int len = valid ? lanes[2 * v + 1] : 0;
-        const float th = q[prim_poff + k];
+        const float thx = q[prim_poff + k];
+        const float th = xf_apply(prim_xf, thx);
         float cp = 0.0f;
         for (int u = 0; u < lpad; ++u) {
             if (u < len) {
@@ -706,21 +742,22 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
                 if (mask & PASS_LP) lp_acc += w * o.lp;
                 if (mask & PASS_VALUE) {
                     if (a == 0) cp += w * o.dv;
-                    else accum(T.op[0], e, w * o.dv, pv, g, P);
+                    else accum(T.op[0], e, w * o.dv, pv, g, q, P);
                 }
                 if (mask & PASS_LOC) {
                     const float cm = w * o.dm;
                     if (a == 1) cp += cm;
-                    else accum(T.op[1], e, cm, pm, g, P);
+                    else accum(T.op[1], e, cm, pm, g, q, P);
                     if (aff) pb += cm * xa;
                 }
                 if (mask & PASS_SCALE) {
                     if (a == 2) cp += w * o.ds;
-                    else accum(T.op[2], e, w * o.ds, ps, g, P);
+                    else accum(T.op[2], e, w * o.ds, ps, g, q, P);
                 }
             }
         }
         if (valid && acc_prim) {
+            cp = xf_chain(prim_xf, cp, thx, th);
             if (split) vpart[v] = cp;
             else g[prim_poff + k] += cp;
         }
@@ -764,8 +801,8 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
         bool moments = false;
 
         if (T.primary < 0) {
-            const int fv = fast_kind(T.op[0].kind);
-            const int fl = normal ? fast_kind(T.op[1].kind) : 0;
+            const int fv = fast_kind(T.op[0]);
+            const int fl = normal ? fast_kind(T.op[1]) : 0;
             if (moment_dist && !scale_vec && fv >= 0 && fl >= 0 && !T.affine) {
                 moments = true;
                 const int code = normal ? (fv * 3 + fl) : (9 + fv);
@@ -797,8 +834,10 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
         } else {
             float* vpart = S.vpart;
             const int other_kind = T.primary == 1 ? T.op[0].kind : T.op[1].kind;
+            const int prim_xf = T.primary == 0 ? T.op[0].xf : (T.primary == 1 ? T.op[1].xf
+                                                                                  : T.op[2].xf);
             const bool fast = normal && !scale_vec && T.primary <= 1 && other_kind == MC_OP_DATA &&
-                              !T.affine;
+                              !T.affine && prim_xf == MC_XF_NONE;
             if (fast) {
                 moments = true;
                 if (T.primary == 1)
@@ -830,10 +869,15 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
             if (task) flush_slot_task(G, slot, x);
             else flush_slot(G, slot, x);
         };
-        if ((mask & PASS_VALUE) && T.op[0].kind == MC_OP_PSCALAR) flush(T.op[0].slot, pv);
-        if ((mask & PASS_LOC) && T.op[1].kind == MC_OP_PSCALAR) flush(T.op[1].slot, pm);
-        if ((mask & PASS_SCALE) && T.op[2].kind == MC_OP_PSCALAR) flush(T.op[2].slot, ps);
-        if ((mask & PASS_LOC) && T.affine && T.ab.kind == MC_OP_PSCALAR) flush(T.ab.slot, pb);
+        // (a transformed parameter's partial through its VJP first)
+        if ((mask & PASS_VALUE) && T.op[0].kind == MC_OP_PSCALAR)
+            flush(T.op[0].slot, xf_chain_scalar(T.op[0], pv, q));
+        if ((mask & PASS_LOC) && T.op[1].kind == MC_OP_PSCALAR)
+            flush(T.op[1].slot, xf_chain_scalar(T.op[1], pm, q));
+        if ((mask & PASS_SCALE) && T.op[2].kind == MC_OP_PSCALAR)
+            flush(T.op[2].slot, xf_chain_scalar(T.op[2], ps, q));
+        if ((mask & PASS_LOC) && T.affine && T.ab.kind == MC_OP_PSCALAR)
+            flush(T.ab.slot, xf_chain_scalar(T.ab, pb, q));
         if (!VALUE_ONLY && pass + 1 < T.npass) G.sync();  // passes exist because their writes overlap
         MC_STAMP(22);
     }

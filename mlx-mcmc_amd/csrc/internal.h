@@ -17,7 +17,7 @@ struct DevOperand {
     float cval;
     int32_t unique;
     int32_t slot;     // PSCALAR: LDS slot of its per-wave partial cotangent
-    int32_t pad;
+    int32_t xf;       // mc_transform_kind of a parameter operand (eval.h xf_*)
 };
 
 // Pass mask bits: which cotangents a sweep over the term accumulates.  Terms

@@ -19,7 +19,9 @@ checked against an answer with no Monte-Carlo error of its own:
         decays like a Gaussian, so the equally spaced rule converges
         geometrically — `quadrature_error` measures it by halving the grid).
         Means and variances of mu and theta_g follow from the conditional
-        ones by the laws of total expectation and variance.
+        ones by the laws of total expectation and variance; those of
+        (log tau, log sigma) — workloads.hierarchical_reparam's unconstrained
+        parameters — are the grid's own moments.
   gaussian_moments  configs[1] (isotropic N(0, I)) and configs[4]
         (N(0, diag(s^2)), s_i = 10^(-1.5 i / 99)): mean 0, variance s^2.
 
@@ -135,6 +137,10 @@ def hierarchical_moments(y, group, G, n_grid=161, width=10.0):
     for wk, m, vm, et, vt in cond:
         Vm += wk * (vm + (m - Em) ** 2)
         Vt += wk * (vt + (et - Et) ** 2)
+    U, V = U.ravel(), V.ravel()
+    Eu, Ev = float(np.sum(w * U)), float(np.sum(w * V))
+    log_mean = [Eu, Ev]
+    log_var = [float(np.sum(w * (U - Eu) ** 2)), float(np.sum(w * (V - Ev) ** 2))]
     Etau = float(np.sum(w * T))
     Esig = float(np.sum(w * S))
     Vtau = float(np.sum(w * (T - Etau) ** 2))
@@ -142,7 +148,8 @@ def hierarchical_moments(y, group, G, n_grid=161, width=10.0):
     mean = np.concatenate([[Em, Etau, Esig], Et])
     var = np.concatenate([[Vm, Vtau, Vsig], Vt])
     edge = max(w.reshape(n_grid, n_grid)[[0, -1], :].max(), w.reshape(n_grid, n_grid)[:, [0, -1]].max())
-    return {"mean": mean, "var": var, "mode_log_tau_sigma": x0.tolist(),
+    return {"mean": mean, "var": var, "log_tau_sigma_mean": log_mean,
+            "log_tau_sigma_var": log_var, "mode_log_tau_sigma": x0.tolist(),
             "laplace_sd_log_tau_sigma": sd.tolist(), "edge_weight": float(edge)}
 
 
@@ -152,9 +159,13 @@ def quadrature_error(y, group, G, n_grid=161):
     error bound."""
     a = hierarchical_moments(y, group, G, n_grid)
     b = hierarchical_moments(y, group, G, 2 * n_grid - 1)
-    sd = np.sqrt(b["var"])
-    return (float(np.max(np.abs(a["mean"] - b["mean"]) / np.maximum(np.abs(b["mean"]), sd))),
-            float(np.max(np.abs(a["var"] - b["var"]) / b["var"])))
+    am = np.concatenate([a["mean"], a["log_tau_sigma_mean"]])
+    bm = np.concatenate([b["mean"], b["log_tau_sigma_mean"]])
+    av = np.concatenate([a["var"], a["log_tau_sigma_var"]])
+    bv = np.concatenate([b["var"], b["log_tau_sigma_var"]])
+    sd = np.sqrt(bv)
+    return (float(np.max(np.abs(am - bm) / np.maximum(np.abs(bm), sd))),
+            float(np.max(np.abs(av - bv) / bv)))
 
 
 def gaussian_moments(scales):

@@ -5,7 +5,10 @@ test infrastructure, run here on the CPU and committed.
       For each README shape (small G=7/N=1K, medium G=97/N=10K, large
       G=997/N=100K — workloads.SHAPES, data workloads.hierarchical_data seed 0):
       exact posterior means and variances in layout order (mu, tau, sigma,
-      theta[0..G-1]), the quadrature grid, and the quadrature error measured by
+      theta[0..G-1]), the moments of (log tau, log sigma) (the unconstrained
+      parameters of workloads.hierarchical_reparam, whose layout order is
+      mu, log_tau, log_sigma, theta), the quadrature grid, and the quadrature
+      error (both sets of moments) measured by
       halving the grid spacing (relative to max(|mean|, sd) for means and to
       the variance for variances).
 
@@ -39,6 +42,8 @@ def main():
         em, ev = E.quadrature_error(y, g, G, n_grid=N_GRID)
         out["shapes"][shape] = {"G": G, "N": N, "mean": r["mean"].tolist(),
                                 "var": r["var"].tolist(),
+                                "log_tau_sigma_mean": r["log_tau_sigma_mean"],
+                                "log_tau_sigma_var": r["log_tau_sigma_var"],
                                 "mode_log_tau_sigma": r["mode_log_tau_sigma"],
                                 "laplace_sd_log_tau_sigma": r["laplace_sd_log_tau_sigma"],
                                 "edge_weight": r["edge_weight"],

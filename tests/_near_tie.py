@@ -5,18 +5,21 @@ fp32 rounding of their log ratios -(H_prop - H_init) puts them on opposite
 sides of log U.  A divergence is accepted only at such a near-tie: |log U -
 ratio| within TIE of the reference run's ratio, TIE = TIE_ULPS ulp of
 |H_init| (H is a float32 sum of the whole log density, summed in a different
-order by each kernel / by the oracle).  Reference: hmc.py:139-153."""
+order by each kernel / by the oracle).  When H is a small difference of
+large terms (a log density near zero), the rounding is that of the terms:
+`h_scale` (a bound on the magnitude of the summands) replaces |H_init| when
+it is larger.  Reference: hmc.py:139-153."""
 import numpy as np
 
 TIE_ULPS = 8
 BLOWUP = 1e3     # |log ratio| beyond which the proposal is a diverged trajectory
 
 
-def tie_bound(energy):
-    return TIE_ULPS * np.spacing(np.abs(np.float32(energy))).astype(np.float64)
+def tie_bound(energy, h_scale=0.0):
+    return TIE_ULPS * np.spacing(np.float32(max(abs(float(energy)), h_scale))).astype(np.float64)
 
 
-def compare_trace(gpu, ref, label, verbose=False):
+def compare_trace(gpu, ref, label, verbose=False, h_scale=0.0):
     """Decisions / ratios / H_init / step sizes of one chain (dicts of 1-D
     arrays: accepted, ratio, energy, step_size; ref also log_u).  Returns the
     number of leading iterations that agree (all, or up to a proven
@@ -24,7 +27,7 @@ def compare_trace(gpu, ref, label, verbose=False):
     n = len(ref["accepted"])
     worst = 0.0
     for i in range(n):
-        tie = tie_bound(ref["energy"][i])
+        tie = tie_bound(ref["energy"][i], h_scale)
         rg, rr = float(gpu["ratio"][i]), float(ref["ratio"][i])
         if not np.isfinite(rr) or rr < -BLOWUP:
             # a diverged trajectory: chaotic in its last digits, but both

@@ -92,6 +92,10 @@ def test_fixture_is_reproduced():
         r = E.hierarchical_moments(y, g, G, n_grid=81)
         np.testing.assert_allclose(r["mean"], fx[shape]["mean"], rtol=1e-10, atol=1e-12)
         np.testing.assert_allclose(r["var"], fx[shape]["var"], rtol=1e-9)
+        np.testing.assert_allclose(r["log_tau_sigma_mean"], fx[shape]["log_tau_sigma_mean"],
+                                   rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(r["log_tau_sigma_var"], fx[shape]["log_tau_sigma_var"],
+                                   rtol=1e-9)
         assert fx[shape]["quadrature_rel_error_mean"] < 1e-9
         assert fx[shape]["quadrature_rel_error_var"] < 1e-9
         assert fx[shape]["edge_weight"] < 1e-12
@@ -120,3 +124,26 @@ def test_oracle_hmc_agrees_with_exact(name, shape):
     if n > 100:     # the spread is that of independent standard normals
         assert 0.8 < np.sqrt(np.mean(zm ** 2)) < 1.3
         assert 0.8 < np.sqrt(np.mean(zv ** 2)) < 1.3
+
+
+def test_reparam_density_is_the_change_of_variables():
+    """workloads.hierarchical_reparam (the exp-transformed scales + their
+    log-Jacobian identity terms) is hierarchical's density in (mu, log tau,
+    log sigma, theta): log p_reparam(u, v) = log p(e^u, e^v) + u + v, so the
+    fixture's (log tau, log sigma) moments are its posterior's."""
+    import torch
+
+    G, N = W.SHAPES["small"]
+    a, _ = W.hierarchical(W.ns_oracle(), G, N)
+    b, _ = W.hierarchical_reparam(W.ns_oracle(), G, N)
+    rng = np.random.default_rng(3)
+    for _ in range(3):
+        mu, u, v = rng.normal(1.0, 0.3), rng.normal(0.3, 0.3), rng.normal(0.0, 0.05)
+        th = torch.tensor(rng.normal(1.0, 1.0, G), dtype=torch.float64)
+        pa = {"mu": torch.tensor(mu, dtype=torch.float64),
+              "tau": torch.tensor(np.exp(u), dtype=torch.float64),
+              "sigma": torch.tensor(np.exp(v), dtype=torch.float64), "theta": th}
+        pb = {"mu": pa["mu"], "log_tau": torch.tensor(u, dtype=torch.float64),
+              "log_sigma": torch.tensor(v, dtype=torch.float64), "theta": th}
+        with torch.no_grad():
+            np.testing.assert_allclose(float(b(pb)), float(a(pa)) + u + v, rtol=1e-12)

@@ -140,8 +140,13 @@ X3 = np.arange(3, dtype=np.float32)
     lambda p: m.Gamma(p["x"] * 2.0, 1.0).log_prob(p["x"]),      # not a Normal loc
     lambda p: mx.sum(m.Normal((p["x"] + p["x"] * X3) * 2.0, 1.0).log_prob(X3)),  # scaled affine
     lambda p: m.Normal(0, 1).log_prob(p["x"]) if p["x"] > 0 else 0,  # Python branch
-    lambda p: mx.log(p["x"]),                                   # unsupported primitive
+    lambda p: mx.log(p["x"]),                                   # a parameter, not a density
     lambda p: m.Normal(0, 1).log_prob(p["v"]),                  # unsummed vector
+    lambda p: m.Normal(0, 1).log_prob(mx.exp(mx.exp(p["x"]))),  # a transform of a transform
+    lambda p: m.Normal(0, 1).log_prob(mx.exp(p["x"] * 2.0)),    # exp of an expression
+    lambda p: m.Normal(0, 1).log_prob(p["x"]) + p["x"] * p["x"],  # a product added to lp
+    lambda p: m.Normal(0, 1).log_prob(p["x"]) + p["v"],         # unsummed vector identity
+    lambda p: mx.sum(m.Normal(2.0 * p["x"], 1.0).log_prob(X3)),  # const * scalar as a loc
 ])
 def test_unsupported_models_raise(bad):
     with pytest.raises(_trace.TraceError):
@@ -194,3 +199,70 @@ def test_scalar_param_plus_constant_loc_message():
         _trace.trace(shifted, {"mu": 0.0})
     with pytest.raises(_trace.TraceError, match="two scalar parameters"):
         _trace.trace(two, {"mu": 0.0, "nu": 0.0})
+
+
+def test_transformed_operands_and_identity_terms():
+    """Reparameterised models (include/mcmc355.h mc_transform_kind,
+    MC_DIST_IDENTITY): mx.exp / mx.log of a parameter is a transformed
+    operand wherever a parameter may stand; a parameter expression added to
+    the log density is an identity term with its constant weight."""
+    XF = {_lib.MC_XF_NONE: "", _lib.MC_XF_EXP: "exp", _lib.MC_XF_LOG: "log"}
+
+    def desc(o):
+        return (o.kind, XF[o.transform])
+
+    lp, init = W.hierarchical_reparam(W.ns_product(), *W.SHAPES["small"])
+    tm = _trace.trace(lp, init)
+    P, N, PV, G_, D = (_lib.MC_OP_PSCALAR, _lib.MC_OP_NONE, _lib.MC_OP_PVEC, _lib.MC_OP_GATHER,
+                       _lib.MC_OP_DATA)
+    C = _lib.MC_OP_CONST
+    got = [(t.dist, desc(t.value), desc(t.loc), desc(t.scale), t.weight) for t in tm.terms]
+    assert got == [
+        (_lib.MC_DIST_NORMAL, (P, ""), (C, ""), (C, ""), 1.0),
+        (_lib.MC_DIST_HALFNORMAL, (P, "exp"), (N, ""), (C, ""), 1.0),     # HalfNormal(5)(e^lt)
+        (_lib.MC_DIST_IDENTITY, (P, ""), (N, ""), (N, ""), 1.0),          # + log_tau
+        (_lib.MC_DIST_HALFNORMAL, (P, "exp"), (N, ""), (C, ""), 1.0),
+        (_lib.MC_DIST_IDENTITY, (P, ""), (N, ""), (N, ""), 1.0),
+        (_lib.MC_DIST_NORMAL, (PV, ""), (P, ""), (P, "exp"), 1.0),        # theta ~ N(mu, e^lt)
+        (_lib.MC_DIST_NORMAL, (D, ""), (G_, ""), (P, "exp"), 1.0),        # y ~ N(theta[g], e^ls)
+    ]
+    assert [tm.c_terms[k].scale.transform for k in range(len(tm.terms))][-1] == _lib.MC_XF_EXP
+    # the affine slope exp(log_tau) of the non-centred model
+    lp, init = W.eight_schools_nc_log(W.ns_product())
+    tm = _trace.trace(lp, init)
+    (t,) = [t for t in tm.terms if t.aff is not None]
+    assert desc(t.aff[0]) == (P, "exp") and desc(t.aff[1]) == (PV, "")
+    assert tm.c_affines[0].slope.transform == _lib.MC_XF_EXP
+    # a log-transformed vector value and `- mx.sum(mx.log(x))`
+    lp, init = W.lognormal(W.ns_product())
+    tm = _trace.trace(lp, init)
+    a, b = tm.terms
+    assert desc(a.value) == (PV, "log") and a.n == 20
+    assert (b.dist, desc(b.value), b.weight, b.n) == (_lib.MC_DIST_IDENTITY, (PV, "log"), -1.0, 20)
+    # forms of an identity: sign, constant weight and offset, views
+    def forms(p):
+        lp0 = m.Normal(0, 1).log_prob(p["x"])
+        return (lp0 - p["x"], -p["x"] + lp0, lp0 + 0.5 * p["x"], lp0 + (2.0 * p["x"] + 1.0),
+                lp0 + mx.sum(mx.log(p["v"][1:3])), lp0 - mx.sum(p["v"][np.array([0, 0, 2])]))
+    outs = forms({"x": _trace.Param("x", 0, ()), "v": _trace.Param("v", 1, (3,))})
+    ids = [[t for t in o.terms if t.dist == _lib.MC_DIST_IDENTITY][0] for o in outs]
+    assert [t.weight for t in ids] == [-1.0, -1.0, 0.5, 2.0, 1.0, -1.0]
+    assert outs[3].const == 1.0
+    assert desc(ids[4].value) == (PV, "log") and ids[4].value.param_offset == 2 and ids[4].n == 2
+    assert desc(ids[5].value) == (G_, "") and ids[5].n == 3
+    # a transform commutes with a view: exp(v)[1] and exp(v[1]) are one operand
+    o1 = _trace.to_operand(mx.exp(_trace.Param("v", 1, (3,)))[1])
+    o2 = _trace.to_operand(mx.exp(_trace.Param("v", 1, (3,))[1]))
+    assert o1.key() == o2.key() == ("p", 2, _lib.MC_XF_EXP)
+    # transformed and plain operands never fold together
+    y = W.simple_normal_data()
+
+    def two_scales(p):
+        lp = 0.0
+        for v in y[:3]:
+            lp = lp + m.Normal(p["mu"], p["s"]).log_prob(mx.array(v))
+        for v in y[3:6]:
+            lp = lp + m.Normal(p["mu"], mx.exp(p["s"])).log_prob(mx.array(v))
+        return lp
+    tm = _trace.trace(two_scales, {"mu": 0.0, "s": 0.0})
+    assert [(t.n, t.scale.transform) for t in tm.terms] == [(3, 0), (3, _lib.MC_XF_EXP)]

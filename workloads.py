@@ -19,7 +19,7 @@ def ns_product():
 
     return SimpleNamespace(Normal=m.Normal, HalfNormal=m.HalfNormal, Exponential=m.Exponential,
                            Gamma=m.Gamma, Beta=m.Beta, sum=mx.sum, array=mx.array,
-                           name="product")
+                           exp=mx.exp, log=mx.log, name="product")
 
 
 def ns_oracle():
@@ -27,7 +27,7 @@ def ns_oracle():
 
     return SimpleNamespace(Normal=ns.Normal, HalfNormal=ns.HalfNormal, Exponential=ns.Exponential,
                            Gamma=ns.Gamma, Beta=ns.Beta, sum=ns.sum, array=ns.array,
-                           name="oracle")
+                           exp=ns.exp, log=ns.log, name="oracle")
 
 
 # ---- config 1: examples/01_simple_normal.py:26-50 (vectorised as in
@@ -87,6 +87,31 @@ def hierarchical(ns, G=997, N=100_000, seed=0):
     init = {"mu": np.float32(gm.mean()), "tau": np.float32(gm.std()),
             "sigma": np.float32(1.0), "theta": gm}
     return log_prob, init
+
+
+def hierarchical_reparam(ns, G=997, N=100_000, seed=0):
+    """The hierarchical model with unconstrained scales: tau = exp(log_tau),
+    sigma = exp(log_sigma), the same HalfNormal priors on tau and sigma plus
+    the log-Jacobians (`lp + log_tau`), so (mu, exp(log_tau), exp(log_sigma),
+    theta) has exactly `hierarchical`'s posterior (oracle/exact.py
+    log_tau_sigma moments).  Transformed scale operands and identity terms
+    (include/mcmc355.h mc_transform_kind, MC_DIST_IDENTITY)."""
+    y, group = hierarchical_data(G, N, seed)
+
+    def log_prob(params):
+        mu, log_tau, log_sigma = params["mu"], params["log_tau"], params["log_sigma"]
+        theta = params["theta"]
+        tau, sigma = ns.exp(log_tau), ns.exp(log_sigma)
+        lp = ns.Normal(0, 10).log_prob(mu)
+        lp = lp + ns.HalfNormal(5).log_prob(tau) + log_tau
+        lp = lp + ns.HalfNormal(5).log_prob(sigma) + log_sigma
+        lp = lp + ns.sum(ns.Normal(mu, tau).log_prob(theta))
+        lp = lp + ns.sum(ns.Normal(theta[group], sigma).log_prob(y))
+        return lp
+
+    _, init = hierarchical(ns, G, N, seed)
+    return log_prob, {"mu": init["mu"], "log_tau": np.float32(np.log(init["tau"])),
+                      "log_sigma": np.float32(0.0), "theta": init["theta"]}
 
 
 def hierarchical_flops_per_step(G, N):
@@ -186,6 +211,50 @@ def eight_schools_nc(ns):
 
     return log_prob, {"mu": np.float32(4.0), "tau": np.float32(3.0),
                       "z": np.zeros(8, np.float32)}
+
+
+def eight_schools_nc_log(ns):
+    """Non-centred eight schools with tau = exp(log_tau): the affine loc's
+    slope is a transformed parameter (mu + exp(log_tau) * z), plus the
+    log-Jacobian identity term."""
+    y, sig = EIGHT_SCHOOLS_Y, EIGHT_SCHOOLS_SIGMA
+
+    def log_prob(params):
+        mu, log_tau, z = params["mu"], params["log_tau"], params["z"]
+        tau = ns.exp(log_tau)
+        lp = ns.Normal(0, 5).log_prob(mu) + ns.HalfNormal(5).log_prob(tau) + log_tau
+        lp = lp + ns.sum(ns.Normal(0, 1).log_prob(z))
+        return lp + ns.sum(ns.Normal(mu + tau * z, sig).log_prob(ns.array(y)))
+
+    return log_prob, {"mu": np.float32(4.0), "log_tau": np.float32(1.0),
+                      "z": np.zeros(8, np.float32)}
+
+
+# ---- a positive vector through mx.log: log-normal components -----------------------
+def lognormal_params(D=20):
+    m = np.linspace(-1.0, 1.0, D).astype(np.float32)
+    s = np.linspace(0.2, 0.4, D).astype(np.float32)
+    return m, s
+
+
+def lognormal(ns, D=20):
+    """x_i > 0 with log x_i ~ N(m_i, s_i), written as the change of variables
+    Normal(m, s).log_prob(log x) - sum(log x): a log-transformed parameter
+    vector as a value operand and a vector identity term.  Known answer:
+    E x_i = exp(m_i + s_i^2 / 2), Var x_i = (exp(s_i^2) - 1) exp(2 m_i + s_i^2)."""
+    m, s = lognormal_params(D)
+
+    def log_prob(params):
+        x = params["x"]
+        lp = ns.sum(ns.Normal(ns.array(m), ns.array(s)).log_prob(ns.log(x)))
+        return lp - ns.sum(ns.log(x))
+
+    return log_prob, {"x": np.exp(m).astype(np.float32)}
+
+
+def lognormal_moments(D=20):
+    m, s = (v.astype(np.float64) for v in lognormal_params(D))
+    return {"mean": np.exp(m + s * s / 2), "var": np.expm1(s * s) * np.exp(2 * m + s * s)}
 
 
 # ---- linear regression: an affine loc a + b * x over data ------------------------
