@@ -38,7 +38,12 @@
 //   * the shared parameters' own priors enter slice 0's log-p record (one
 //     add in the lane that holds the parameter, instead of a per-step
 //     readlane sum over the shared parameters after the exchange);
-//   * the kinetic-energy items K0 / K1 travel only on the first / last step.
+//   * the kinetic-energy items K0 / K1 travel only on the first / last step;
+//   * log p is evaluated, exchanged and summed on the last step only: a
+//     leapfrog step needs the gradient alone, and the Hamiltonian of the
+//     proposal (hmc.py:139-153) reads log p at the end of the trajectory, so
+//     the intermediate steps' log-p items (their terms' log / normaliser
+//     work, the records' lp pairs and their polls) were never used.
 // Results equal k_hmc_lr's up to fp32 summation order; runs are
 // bit-reproducible and independent of how chains are split over launches.
 #pragma once
@@ -86,10 +91,16 @@ MC_DEV f2 bc2(float x) { return (f2){x, x}; }
 // Reduce-scatter of 8 per-lane values over the wave: returns two registers;
 // row r of register n holds (in all 16 lanes) the wave total of value
 // 4n + {0, 2, 1, 3}[r].  A fixed tree: the same bits in every wave / slice.
+// Z01: v[0] and v[1] are zero in every lane (their totals are +0).
+template <bool Z01 = false>
 MC_DEV void lf_rs8(const float (&v)[8], float (&x)[2]) {
     float w[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {  // lanes 0-31: v[2m] sums, lanes 32-63: v[2m+1]
+        if (Z01 && m == 0) {
+            w[0] = 0.0f;
+            continue;
+        }
         const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[2 * m]),
                                                         __float_as_uint(v[2 * m + 1]), false, false);
         w[m] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
@@ -442,12 +453,13 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     const int pub_pair = (col < 2 * NRS) ? 8 * (col >> 1) + 4 * (col & 1) + lf_row(row) : -1;
     const bool pub_rec = pub_pair >= 0 && pub_pair < NV;
     // poll passes by kind: record pairs every step, K0 / K1 pairs on the first / last
-    uint32_t need_v = 0, need_k0 = 0, need_k1 = 0;
+    uint32_t need_v = 0, need_lp = 0, need_k0 = 0, need_k1 = 0;
 #pragma unroll
     for (int ps = 0; ps < NPASS; ++ps) {
         const int pr = 4 * ps + lf_row(row);
         if (X1 || !poll_lane || pr >= NPAIR) continue;
-        if (pr < NV) need_v |= 1u << ps;
+        if (pr < 2) need_lp |= 1u << ps;  // the log-p pairs: last step only
+        else if (pr < NV) need_v |= 1u << ps;
         else if (pr < NV + 2) need_k0 |= 1u << ps;
         else need_k1 |= 1u << ps;
     }
@@ -537,10 +549,11 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         sweep(M1, M2);
         for (int l = 0; l < L; ++l) {
             MC_STAMP(0);
+            const bool lst = l == L - 1;  // log p: the last step only
             // finish the swept term from its moment sums, evaluate the direct
             // term (k_hmc_lr's lr_finish; same arithmetic, both chains packed):
-            // log p partial, complete private gradients, cotangent partials of
-            // the swept scale (cs), the direct loc (cm) and scale (cd)
+            // log p partial (last step), complete private gradients, cotangent
+            // partials of the swept scale (cs), the direct loc (cm) and scale (cd)
             // (the first contribution to each sum is assigned, not added to
             // zero: x + 0 is not folded under IEEE signed zeros)
             f2 lpp = {0.f, 0.f}, cs = {0.f, 0.f}, cm = {0.f, 0.f}, cd = {0.f, 0.f};
@@ -555,45 +568,56 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 s = first ? v : s + v;
                 first = false;
             };
+            // (a shared scale's 1/s^2 is squared here from its 1/s: the
+            // holding lane's sh.iv = sh.is * sh.is, the same rounding)
             if (SW) {
                 const f2 is = SWS ? lf_sh2(sh.is, ksw) : sw_cinv;
-                const f2 iv = SWS ? lf_sh2(sh.iv, ksw) : sw_cinv2;
-                const f2 lg = SWS ? lf_sh2(sh.lg, ksw) : sw_clogs;
-                const f2 c0lg = sw_c0 - lg;
+                const f2 iv = SWS ? is * is : sw_cinv2;
 #pragma unroll
                 for (int r = 0; r < RS; ++r) {
                     const bool on = len[r] != 0;
-                    const f2 lpt = cnt[r] * c0lg - (half * M2[r]) * iv;
                     const f2 z = {0.f, 0.f};
-                    if (RS == 1) {  // one slot: an empty lane's terms are zeros
-                        lpp = on ? sw_w * lpt : z;
-                        g[r] = on ? sw_w * (M1[r] * iv) : z;
-                        cs = on ? sw_w * ((M2[r] * iv - cnt[r]) * is) : z;
-                        lpp0 = cs0 = g0r[r] = false;
+                    if (RS == 1) {
+                        // one slot: an empty lane's moment sums and count are
+                        // zeros (the sweep skips it), so are its gradient and
+                        // cotangent; its log p is selected away
+                        g[r] = sw_w * (M1[r] * iv);
+                        cs = sw_w * ((M2[r] * iv - cnt[r]) * is);
+                        cs0 = g0r[r] = false;
                     } else if (on) {
-                        acc(lpp, lpp0, sw_w * lpt);
                         acc(g[r], g0r[r], sw_w * (M1[r] * iv));
                         acc(cs, cs0, sw_w * ((M2[r] * iv - cnt[r]) * is));
+                    }
+                    if (lst) {
+                        const f2 lg = SWS ? lf_sh2(sh.lg, ksw) : sw_clogs;
+                        const f2 lpt = cnt[r] * (sw_c0 - lg) - (half * M2[r]) * iv;
+                        if (RS == 1) {
+                            lpp = on ? sw_w * lpt : z;
+                            lpp0 = false;
+                        } else if (on) {
+                            acc(lpp, lpp0, sw_w * lpt);
+                        }
                     }
                 }
             }
             if (DIR) {
                 const f2 um = DM ? lf_sh2(sh.q, kdm) : d_m;
                 const f2 is = DS ? lf_sh2(sh.is, kds) : d_cinv;
-                const f2 iv = DS ? lf_sh2(sh.iv, kds) : d_cinv2;
-                const f2 lg = DS ? lf_sh2(sh.lg, kds) : d_clogs;
-                const f2 c0lg = one * (d_c0 - lg);
+                const f2 iv = DS ? is * is : d_cinv2;
 #pragma unroll
                 for (int r = 0; r < RS; ++r) {
                     if (!pdir[r]) continue;
                     const f2 d = q[r] - um;
                     const f2 s2 = d * d;
-                    const f2 lpt = c0lg - (half * s2) * iv;
-                    acc(lpp, lpp0, d_w * lpt);
                     const f2 u = d_w * (d * iv);
                     acc(g[r], g0r[r], -u);
                     acc(cm, cm0, u);
                     acc(cd, cd0, d_w * ((s2 * iv - one) * is));
+                    if (lst) {
+                        const f2 lg = DS ? lf_sh2(sh.lg, kds) : d_clogs;
+                        const f2 lpt = one * (d_c0 - lg) - (half * s2) * iv;
+                        acc(lpp, lpp0, d_w * lpt);
+                    }
                 }
             }
             // the own prior of this lane's shared parameter (moment form with
@@ -603,13 +627,15 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             {
                 const float v = sh.q;
                 const float d = own.hn ? v : v - o_m;
-                const float d2 = d * d;
                 const bool out = own.hn && !(v >= 0.0f);
-                const float lpe = out ? -__builtin_inff() : o_c0l - (0.5f * d2) * o_cinv2;
-                const float lp_own = o_wn * lpe;
                 g_own = (out || !own.on) ? 0.0f : o_wn * -(d * o_cinv2);
-                if (own_lp0) lpp[0] += lp_own;
-                if (own_lp1) lpp[1] += lp_own;
+                if (lst) {
+                    const float d2 = d * d;
+                    const float lpe = out ? -__builtin_inff() : o_c0l - (0.5f * d2) * o_cinv2;
+                    const float lp_own = o_wn * lpe;
+                    if (own_lp0) lpp[0] += lp_own;
+                    if (own_lp1) lpp[1] += lp_own;
+                }
             }
             MC_STAMP(1);
             // wave totals, reduce-scattered: pair P = 2 slot + chain
@@ -647,7 +673,8 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     float vv[8], xx[2];
 #pragma unroll
                     for (int x = 0; x < 8; ++x) vv[x] = v[8 * qq + x];
-                    lf_rs8(vv, xx);
+                    if (qq == 0 && !lst) lf_rs8<true>(vv, xx);  // (no log-p pairs)
+                    else lf_rs8(vv, xx);
                     xr[2 * qq] = xx[0];
                     xr[2 * qq + 1] = xx[1];
                 }
@@ -671,7 +698,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 // first / last step (lanes 2, 3 of rows 0 / 1)
                 int pp = -1;
                 float pv = 0.0f;
-                if (pub_rec) {
+                if (pub_rec && (lst || pub_pair >= 2)) {  // (log-p pairs: last step)
                     pp = pub_pair;
                     pv = xr[0];
 #pragma unroll
@@ -700,7 +727,8 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             }
             // poll: pass ps reads pair 4 ps + perm[row] of slice col
             const bool kstep = (l == 0) || (l == L - 1);
-            const uint32_t need = need_v | (l == 0 ? need_k0 : 0u) | (l == L - 1 ? need_k1 : 0u);
+            const uint32_t need =
+                need_v | (l == 0 ? need_k0 : 0u) | (lst ? (need_k1 | need_lp) : 0u);
             float vals[NPASS];
 #pragma unroll
             for (int ps = 0; ps < NPASS; ++ps) vals[ps] = 0.0f;
@@ -762,8 +790,10 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 }
             }
             // totals: the slice sum (the own priors are in slice 0's record)
-            lpn[0] = rl(tot[0], 0) + lp_const;
-            lpn[1] = rl(tot[0], 16 * lf_row(1)) + lp_const;
+            if (lst) {
+                lpn[0] = rl(tot[0], 0) + lp_const;
+                lpn[1] = rl(tot[0], 16 * lf_row(1)) + lp_const;
+            }
             {
                 float gx = 0.0f;
 #pragma unroll
