@@ -1007,6 +1007,9 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 granule_store(par ? gpub[1] : gpub[0], epoch, v);
             }
             MC_STAMP(2);
+            // the sweep at a higher wave priority than the latency-bound rest of
+            // the step (k_hmc_lf: the two waves of a SIMD settle out of phase)
+            __builtin_amdgcn_s_setprio(1);
             // while the records travel: the private parameters' next position
             // (their gradients are complete) and the swept terms' sums there,
             // and the scalar terms of this step
@@ -1057,6 +1060,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 break;
             }
             MC_STAMP(3);
+            __builtin_amdgcn_s_setprio(0);
             // slice sums: a fixed 16-lane DPP tree per pair, read from the row's lane 0
             float tot[4 * NPASS];
             if constexpr (X1) {

@@ -719,6 +719,14 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 if (pp >= 0) granule_store(gline[par] + slice * 16 + pp, epoch, pv);
             }
             MC_STAMP(2);
+            // the sweep issues at a higher wave priority than the latency-bound
+            // rest of the step (slice sums, shared drift, finish, reduce-scatter,
+            // publish): the two waves of a SIMD settle out of phase, one
+            // sweeping while the other's dependent chains fill its gaps (with
+            // equal priorities the SQ's oldest-first choice kept them in step;
+            // A/B on one box 92.0 -> 100.0 M steps/s, the same with priority 1, 2
+            // or 3, and with the poll at either level, profiles/r3/ab/ab34)
+            __builtin_amdgcn_s_setprio(1);
             // while the records travel: the private parameters' next position
             // and the swept terms' sums there
             if (l + 1 < L) {
@@ -770,6 +778,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 break;
             }
             MC_STAMP(3);
+            __builtin_amdgcn_s_setprio(0);
             // slice sums: a fixed 16-lane DPP tree per pass; pair 4 ps + perm[r]
             // in row r of tot[ps]
             float tot[NPASS];
