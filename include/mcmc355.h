@@ -326,6 +326,11 @@ int mc_debug_exchange_fault(int on);
  * run time (FORM = -1) instead of its compile-time instantiations; 1 restores
  * the default.  Results agree up to fp32 summation order.                  */
 int mc_debug_lanes_forms(int on);
+/* Test hook: 0 runs every lane-resident HMC launch on the general kernel
+ * k_hmc_lr instead of the fast-form k_hmc_lf (as MC_LANES_FAST=0 in the
+ * environment); 1 restores the default.  Results agree up to fp32
+ * summation order.                                                        */
+int mc_debug_lanes_fast(int on);
 /* Test hook for k_nuts_lr's variants: -1 (default) picks the fastest variant
  * the program qualifies for; 0 forces the generic lane evaluator (SPEC 0);
  * 1 forces the specialised variant (SPEC 1) where the program qualifies,

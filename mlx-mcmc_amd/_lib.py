@@ -181,6 +181,7 @@ SIGNATURES = [
     ("mc_workspace_release", ctypes.c_int, [_VP]),
     ("mc_debug_exchange_fault", ctypes.c_int, [ctypes.c_int]),
     ("mc_debug_lanes_forms", ctypes.c_int, [ctypes.c_int]),
+    ("mc_debug_lanes_fast", ctypes.c_int, [ctypes.c_int]),
     ("mc_debug_nuts_variant", ctypes.c_int, [ctypes.c_int]),
     ("mc_box_muller_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     ("mc_logf_unit_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),

@@ -85,6 +85,10 @@ struct LanePlan {
     int fast = 0;        // fast form: only swept / direct terms and own priors (k_hmc_lf)
     int form = -1;       // the fast form's LF_* bits when every slice has the same terms
                          // and distinct shared roles (compile-time k_hmc_lf), else -1
+    int32_t shxf[kLrMaxShared] = {0, 0, 0, 0};  // transforms of the shared parameters
+    float shid[kLrMaxShared] = {0.f, 0.f, 0.f, 0.f};  // raw identity weights (k_hmc_lf)
+    int has_xf = 0;      // a shared parameter is transformed, or an identity term
+                         // (no NUTS lanes, no term interpreter)
     std::string why;     // why it does not qualify
     std::vector<LrTerm> terms;
     std::vector<float> data;
@@ -336,6 +340,8 @@ static int64_t pp_index(const DevTerm& t, int a, int64_t i, const std::vector<in
 // The parameter / element partition plan_slices computes, kept for the
 // lane-resident planner (plan_lanes).
 struct SlPartition {
+    std::vector<int> shxf;                // per shared ordinal: mc_transform_kind
+    std::vector<int> sterm_raw;           // per scalar term: LrSterm::raw bits
     std::vector<int> ppr;                 // per term: slot of its per-element parameter, or -1
     std::vector<char> shared, scalar;     // per parameter / per term
     std::vector<int> jsh;                 // per parameter: shared ordinal, or -1
@@ -350,7 +356,7 @@ static bool has_affine(const mc_program* p) {
     return false;
 }
 // Transformed parameter operands and identity terms (the reparameterised
-// models of mc_transform_kind) run on the chain-per-workgroup kernels.
+// models of mc_transform_kind).
 static bool has_transform(const mc_program* p) {
     for (const DevTerm& t : p->raw) {
         if (t.dist == MC_DIST_IDENTITY) return true;
@@ -360,15 +366,31 @@ static bool has_transform(const mc_program* p) {
     }
     return false;
 }
+// ... whose transforms all act on broadcast (PSCALAR) parameters and whose
+// identity terms are scalar: the lane-resident kernel k_hmc_lr runs them
+// (lanes.h LrCtx::shxf); anything else runs on the chain-per-workgroup kernels.
+static bool transform_on_shared_only(const mc_program* p) {
+    for (const DevTerm& t : p->raw) {
+        if (t.affine) return false;
+        for (int a = 0; a < 3; ++a)
+            if (t.op[a].xf != MC_XF_NONE && t.op[a].kind != MC_OP_PSCALAR) return false;
+        if (t.dist == MC_DIST_IDENTITY && t.op[0].kind != MC_OP_PSCALAR &&
+            t.op[0].kind != MC_OP_CONST)
+            return false;
+    }
+    return true;
+}
 
 static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = nullptr) {
     const std::vector<DevTerm>& raw = p->raw;
     if (has_affine(p))
         return fail(MC_ERR_UNSUPPORTED, "affine loc operands run on the chain-per-workgroup "
                     "kernels (not sliceable)");
-    if (has_transform(p))
-        return fail(MC_ERR_UNSUPPORTED, "transformed parameter operands (mx.exp / mx.log) and "
-                    "identity terms run on the chain-per-workgroup kernels (not sliceable)");
+    const bool xf = has_transform(p);
+    if (xf && !transform_on_shared_only(p))
+        return fail(MC_ERR_UNSUPPORTED, "transformed parameter operands (mx.exp / mx.log) of "
+                    "per-element parameters, and identity terms over them, run on the "
+                    "chain-per-workgroup kernels (not sliceable)");
     const std::vector<float>& dp = p->h_data;
     const std::vector<int32_t>& ip = p->h_index;
     const int D = p->D;
@@ -414,6 +436,36 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = n
             lidx[j] = (int)priv[s].size();
             priv[s].push_back(j);
             run += cost[j];
+        }
+    }
+    // the transform of each shared parameter: every transformed use agrees;
+    // terms that are not scalar read it through the transform only (a scalar
+    // term may also read the raw parameter: the raw bits below)
+    std::vector<int> shxf(shl.size(), MC_XF_NONE);
+    if (xf) {
+        for (const DevTerm& t : raw)
+            for (int a = 0; a < 3; ++a) {
+                const DevOperand& o = t.op[a];
+                if (o.kind != MC_OP_PSCALAR || o.xf == MC_XF_NONE) continue;
+                int& x = shxf[jsh[o.poff]];
+                if (x != MC_XF_NONE && x != o.xf)
+                    return fail(MC_ERR_UNSUPPORTED, "a broadcast parameter read through two "
+                                "different transforms (mx.exp and mx.log): not sliceable");
+                x = o.xf;
+            }
+        for (int t = 0; t < nT; ++t) {
+            bool sc = true;
+            for (int a = 0; a < 3; ++a) {
+                const int k = raw[t].op[a].kind;
+                if (k != MC_OP_CONST && k != MC_OP_PSCALAR && k != MC_OP_NONE) sc = false;
+            }
+            if (sc) continue;
+            for (int a = 0; a < 3; ++a) {
+                const DevOperand& o = raw[t].op[a];
+                if (o.kind == MC_OP_PSCALAR && o.xf != shxf[jsh[o.poff]])
+                    return fail(MC_ERR_UNSUPPORTED, "a broadcast parameter read both raw and "
+                                "through mx.exp / mx.log by per-element terms: not sliceable");
+            }
         }
     }
     P.S = S;
@@ -471,6 +523,7 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = n
     // scalar terms (only constants and broadcast parameters): evaluated once
     // per chain after every exchange, in every slice, not split into slices
     std::vector<char> scalar(nT, 0);
+    std::vector<int> sterm_raw;
     P.sterms.clear();
     for (int t = 0; t < nT; ++t) {
         bool sc = true;
@@ -484,6 +537,13 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = n
             if (raw[t].n > INT32_MAX) return fail(MC_ERR_UNSUPPORTED, "scalar term too long");
             st.niter = (int32_t)raw[t].n;  // element count
             P.sterms.push_back(st);
+            int rb = 0;
+            for (int a = 0; a < 3; ++a) {
+                const DevOperand& o = raw[t].op[a];
+                if (o.kind == MC_OP_PSCALAR && o.xf == MC_XF_NONE && shxf[jsh[o.poff]] != MC_XF_NONE)
+                    rb |= 1 << a;
+            }
+            sterm_raw.push_back(rb);
         }
     }
 
@@ -506,6 +566,8 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = n
         }
     }
     if (part) {
+        part->shxf = shxf;
+        part->sterm_raw = sterm_raw;
         part->ppr = ppr;
         part->shared = shared;
         part->scalar = scalar;
@@ -775,7 +837,12 @@ static LrCtx lrctx_of(const mc_program* p) {
     c.nitems = L.nitems;
     c.sdata_floats = L.sdata_floats;
     c.lp_const = p->lp_const;
-    for (int k = 0; k < kLrMaxShared; ++k) c.shl[k] = L.shl[k];
+    for (int k = 0; k < kLrMaxShared; ++k) {
+        c.shl[k] = L.shl[k];
+        c.shxf[k] = L.shxf[k];
+        c.shid[k] = L.shid[k];
+    }
+    c.has_xf = L.has_xf;
     return c;
 }
 
@@ -848,6 +915,8 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
     L.Dsh = SP.Dsh;
     L.nitems = SP.nitems;
     for (int k = 0; k < SP.Dsh; ++k) L.shl[k] = part.shl[k];
+    L.has_xf = has_transform(p) ? 1 : 0;
+    for (int k = 0; k < SP.Dsh; ++k) L.shxf[k] = part.shxf.empty() ? 0 : part.shxf[k];
     L.terms.assign((size_t)S * nT, LrTerm());
     L.blocks.assign(4 * (size_t)S, 0);
     L.gidx.assign((size_t)S * kLrMaxSlots * 64, -1);
@@ -1033,9 +1102,12 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
     }
     // the scalar terms, compact (LDS copy in every workgroup)
     uint32_t own_mask = 0;
-    for (const SlTerm& st : SP.sterms) {
+    int lf_generic = 0;  // scalar terms k_hmc_lf cannot take
+    for (size_t it = 0; it < SP.sterms.size(); ++it) {
+        const SlTerm& st = SP.sterms[it];
         LrSterm x;
         std::memset(&x, 0, sizeof(x));
+        x.raw = part.sterm_raw.empty() ? 0 : part.sterm_raw[it];
         x.dist = st.dist;
         x.kinds = st.kind[0] | (st.kind[1] << 4) | (st.kind[2] << 8);
         x.jsh = (st.kind[0] == SK_SHARED ? st.jsh[0] : 0) |
@@ -1050,10 +1122,17 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         x.own = st.kind[0] == SK_SHARED &&
                 (st.dist == MC_DIST_NORMAL || st.dist == MC_DIST_HALFNORMAL) &&
                 (st.kind[1] == SK_CONST || st.kind[1] == SK_NONE) && st.kind[2] == SK_CONST &&
-                !(own_mask >> st.jsh[0] & 1);
+                !(own_mask >> st.jsh[0] & 1) && !(x.raw & 1);
         if (x.own) own_mask |= 1u << st.jsh[0];
         x.cinv = st.kind[2] == SK_CONST ? 1.0f / st.cval[2] : 0.0f;
         if (!x.own) ++L.n_generic;
+        // an identity term over a raw shared parameter (its log-Jacobian):
+        // k_hmc_lf adds it in the holder lane (LrCtx::shid); k_hmc_lr runs it
+        // with the other generic scalar terms
+        const bool raw_id = st.dist == MC_DIST_IDENTITY && st.kind[0] == SK_SHARED &&
+                            ((x.raw & 1) || L.shxf[st.jsh[0]] == MC_XF_NONE);
+        if (raw_id) L.shid[st.jsh[0]] += x.wn;
+        else if (!x.own) ++lf_generic;
         L.sterms.push_back(x);
     }
     L.sdata_floats = (L.sdata_floats + 3) / 4 * 4;  // the scalar terms follow, 16-byte aligned
@@ -1061,7 +1140,7 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         kSlLdsBudget)
         return no("slice data exceed the LDS budget");
     if (L.data.empty()) L.data.assign(4, 0.0f);
-    L.fast = (!any_rest && L.n_generic == 0) ? 1 : 0;
+    L.fast = (!any_rest && lf_generic == 0) ? 1 : 0;
     L.form = L.fast ? lanes_form(L, nT) : -1;
     L.ok = 1;
     return MC_OK;
@@ -1095,7 +1174,7 @@ static int64_t program_elements(const mc_program* p) {
 // stay unsliced (a per-step exchange costs more than the whole evaluation).
 static constexpr int64_t kLrAutoMinElements = 2048;
 static int auto_slices(const mc_program* p) {
-    if (has_affine(p) || has_transform(p)) return 1;
+    if (has_affine(p) || (has_transform(p) && !transform_on_shared_only(p))) return 1;
     const int64_t n = program_elements(p);
     if (n >= 65536) return 16;
     if (n >= 16384) return 8;
@@ -1192,6 +1271,13 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
         free_lanes(LP);
         LP.why = why;
         p->note = "lane-resident kernel: " + why;
+        if (has_transform(p)) {  // the term interpreter has no transforms
+            free_slices(p->sl);
+            if (!automatic)
+                return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: %s (a program with "
+                            "transformed operands is sliced onto it only)", why.c_str());
+            return MC_OK;
+        }
         if (automatic && program_elements(p) < 16384) {  // only worth it on the lanes kernel
             free_slices(p->sl);
             if (p->slice_kernel != 1) (void)plan_lanes1(p);
@@ -1218,6 +1304,9 @@ extern "C" int mc_program_set_slice_kernel(mc_program* p, int32_t kernel) {
     }
     if (kernel == 2 && !p->lr.ok)
         return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: %s", p->lr.why.c_str());
+    if (kernel == 1 && has_transform(p))
+        return fail(MC_ERR_UNSUPPORTED, "the term interpreter does not run transformed operands "
+                    "(mx.exp / mx.log) or identity terms");
     p->slice_kernel = kernel;
     return MC_OK;
 }
@@ -2037,13 +2126,17 @@ extern "C" int mc_debug_exchange_fault(int on) {
 
 // the fast-form kernel (lanes_fast.h) for programs that qualify, unless
 // MC_LANES_FAST=0 in the environment (A/B timing against k_hmc_lr)
+static int g_lanes_fast = -1;  // mc_debug_lanes_fast; -1: MC_LANES_FAST from the environment
 static bool lanes_fast_enabled() {
-    static int on = -1;
-    if (on < 0) {
+    if (g_lanes_fast < 0) {
         const char* e = std::getenv("MC_LANES_FAST");
-        on = (e && e[0] == '0') ? 0 : 1;
+        g_lanes_fast = (e && e[0] == '0') ? 0 : 1;
     }
-    return on == 1;
+    return g_lanes_fast == 1;
+}
+extern "C" int mc_debug_lanes_fast(int on) {
+    g_lanes_fast = on ? 1 : 0;
+    return MC_OK;
 }
 
 // compile-time forms of k_hmc_lf: MC_LANES_FORM=0 in the environment or
@@ -2126,6 +2219,8 @@ static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
 template <int NB>
 static int launch_hmc_sl(const mc_program* p, const mc_run_config* cfg, void* state,
                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
+    if (has_transform(p))
+        return fail(MC_ERR_UNSUPPORTED, "the term interpreter does not run transformed operands");
     int64_t qo, go;
     mc_state_offsets(p, cfg->num_chains, &qo, &go);
     char* b = (char*)state;
@@ -2385,7 +2480,7 @@ static size_t nuts_lr_lds_bytes(const mc_program* p, int max_depth) {
            (size_t)nuts_lr_arena_floats(p->lr.rs, max_depth) * 4;
 }
 static bool use_nuts_lanes(const mc_program* p, int max_depth) {
-    return nuts_lanes_enabled() && p->sl.S < 2 && p->lr.ok && p->lr.S == 1 &&
+    return nuts_lanes_enabled() && p->sl.S < 2 && p->lr.ok && p->lr.S == 1 && !p->lr.has_xf &&
            p->slice_kernel != 1 && nuts_lr_lds_bytes(p, max_depth) <= (size_t)kSlLdsBudget;
 }
 // no broadcast parameter, no scalar term and one slice term with at most one

@@ -85,6 +85,9 @@ struct LrSterm {
     int32_t own;    // a prior of one shared parameter: value shared, Normal /
                     // HalfNormal with constant loc and scale
     float cinv;     // CONST scale: 1/scale
+    int32_t raw;    // bit a: shared operand a reads the raw parameter of a
+                    // transformed one (LrCtx::shxf; an identity term's log-Jacobian)
+    int32_t pad[3];
 };
 
 struct LrCtx {
@@ -103,6 +106,12 @@ struct LrCtx {
     int32_t sdata_floats;   // LDS floats of a slice block (the scalar terms follow)
     float lp_const;
     int32_t shl[kLrMaxShared];  // global index of shared parameter k
+    int32_t shxf[kLrMaxShared];  // its mc_transform_kind: every slice term (and
+                                 // every scalar-term operand without the raw
+                                 // bit) reads xf(q) (mx.exp(log_sigma) ...)
+    float shid[kLrMaxShared];    // k_hmc_lf: the weights of the identity terms
+                                 // over the raw parameter (its log-Jacobian)
+    int32_t has_xf;              // a transform or an identity term (k_hmc_lf)
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -195,7 +204,9 @@ struct LrPriv {
 // q = 1, p = g = 0).  Uniform reads go through readlane.
 struct LrShared {
     float q, p, g;
-    float is, iv, lg;  // 1/q, 1/q^2, f32 log q: the derived scale values
+    float v;           // the value terms read: xf(q) for a transformed parameter
+                       // (LrCtx::shxf, eval.h xf_apply), else q
+    float is, iv, lg;  // 1/v, 1/v^2, f32 log v: the derived scale values
 };
 
 // One Normal term with a broadcast scale and compile-time operand kinds
@@ -214,8 +225,8 @@ MC_DEV void lr_normal_term(const MC_CONST LrTerm* T, const float* sd, int j, LrP
     float uv[2], um[2], is[2], iv[2], lg[2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-        uv[c] = (K0 == SK_SHARED) ? rl(sh.q, 2 * j0 + c) : (K0 == SK_CONST ? T->cval[0] : 0.0f);
-        um[c] = (K1 == SK_SHARED) ? rl(sh.q, 2 * j1 + c) : (K1 == SK_CONST ? T->cval[1] : 0.0f);
+        uv[c] = (K0 == SK_SHARED) ? rl(sh.v, 2 * j0 + c) : (K0 == SK_CONST ? T->cval[0] : 0.0f);
+        um[c] = (K1 == SK_SHARED) ? rl(sh.v, 2 * j1 + c) : (K1 == SK_CONST ? T->cval[1] : 0.0f);
         is[c] = (K2 == SK_SHARED) ? rl(sh.is, 2 * j2 + c) : T->cinv;
         iv[c] = (K2 == SK_SHARED) ? rl(sh.iv, 2 * j2 + c) : T->cinv2;
         lg[c] = (K2 == SK_SHARED) ? rl(sh.lg, 2 * j2 + c) : T->clogs;
@@ -369,7 +380,7 @@ MC_DEV void lr_finish(const MC_CONST LrTerm* tt, int nsweep, int ndirect, LrPriv
         const int j1 = T->jsh[1], j2 = T->jsh[2];
         const bool shm = T->kind[1] == SK_SHARED, shs = T->kind[2] == SK_SHARED;
         const f2 w = f2s(T->weight), c0 = f2s(T->c0);
-        const f2 um = shm ? (f2){rl(sh.q, 2 * j1), rl(sh.q, 2 * j1 + 1)} : f2s(T->cval[1]);
+        const f2 um = shm ? (f2){rl(sh.v, 2 * j1), rl(sh.v, 2 * j1 + 1)} : f2s(T->cval[1]);
         const f2 is = shs ? (f2){rl(sh.is, 2 * j2), rl(sh.is, 2 * j2 + 1)} : f2s(T->cinv);
         const f2 iv = shs ? (f2){rl(sh.iv, 2 * j2), rl(sh.iv, 2 * j2 + 1)} : f2s(T->cinv2);
         const f2 lg = shs ? (f2){rl(sh.lg, 2 * j2), rl(sh.lg, 2 * j2 + 1)} : f2s(T->clogs);
@@ -413,7 +424,7 @@ MC_DEV void lr_dscale_term(const MC_CONST LrTerm* T, const float* sd, int j, LrP
     const int nslot = T->nslot;
     const f2 w = f2s(T->weight), c0 = f2s(T->c0), half = f2s(0.5f);
     const int32_t* lens = (const int32_t*)sd + T->len_off;
-    const f2 uo = ko == SK_SHARED ? (f2){rl(sh.q, 2 * jo), rl(sh.q, 2 * jo + 1)}
+    const f2 uo = ko == SK_SHARED ? (f2){rl(sh.v, 2 * jo), rl(sh.v, 2 * jo + 1)}
                                   : f2s(T->cval[oth]);
     f2 lp = {0.f, 0.f}, po = {0.f, 0.f};
 #pragma unroll
@@ -491,9 +502,9 @@ MC_DEV void lr_eval(const MC_CONST LrTerm* tt, int t0, int nact, const float* sd
         float uv[2], um[2], us[2], is[2], iv[2], lg[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            uv[c] = k0 == SK_SHARED ? rl(sh.q, 2 * j0 + c) : (k0 == SK_CONST ? T->cval[0] : 0.f);
-            um[c] = k1 == SK_SHARED ? rl(sh.q, 2 * j1 + c) : (k1 == SK_CONST ? T->cval[1] : 0.f);
-            us[c] = k2 == SK_SHARED ? rl(sh.q, 2 * j2 + c) : (k2 == SK_CONST ? T->cval[2] : 0.f);
+            uv[c] = k0 == SK_SHARED ? rl(sh.v, 2 * j0 + c) : (k0 == SK_CONST ? T->cval[0] : 0.f);
+            um[c] = k1 == SK_SHARED ? rl(sh.v, 2 * j1 + c) : (k1 == SK_CONST ? T->cval[1] : 0.f);
+            us[c] = k2 == SK_SHARED ? rl(sh.v, 2 * j2 + c) : (k2 == SK_CONST ? T->cval[2] : 0.f);
             is[c] = k2 == SK_SHARED ? rl(sh.is, 2 * j2 + c) : T->cinv;
             iv[c] = k2 == SK_SHARED ? rl(sh.iv, 2 * j2 + c) : T->cinv2;
             lg[c] = k2 == SK_SHARED ? rl(sh.lg, 2 * j2 + c) : T->clogs;
@@ -636,13 +647,17 @@ MC_DEV LrOwn lr_own_prior(int n_sterms, const LrSterm* st, int j, int nsh) {
 }
 
 MC_DEV void wave_sum8(const float (&v)[8], float (&out)[8]);
+// g_self: the cotangent of the lane's parameter's value sh.v; g_raw: of its
+// raw q (the raw-bit operands of a transformed parameter, lanes.h LrSterm).
 MC_DEV void lr_scalar_terms(int n_sterms, int n_generic, const LrSterm* st, const LrOwn& own,
-                            const LrShared& sh, int j, int nsh, float (&lp)[2], float& g_self) {
+                            const LrShared& sh, int j, int nsh, float (&lp)[2], float& g_self,
+                            float& g_raw) {
     const int xk = j >> 1;
     float lp_own = 0.0f, g_own = 0.0f;
+    g_raw = 0.0f;
     if (own.on) {
         // moment form with the constant scale's reciprocals, as the sliced terms
-        const float v = sh.q;
+        const float v = sh.v;
         const float d = own.hn ? v : v - own.m;
         const float d2 = d * d;
         const bool out = own.hn && !(v >= 0.0f);
@@ -666,8 +681,10 @@ MC_DEV void lr_scalar_terms(int n_sterms, int n_generic, const LrSterm* st, cons
         if (T.own) continue;
         const int k0 = T.kinds & 15, k1 = (T.kinds >> 4) & 15, k2 = (T.kinds >> 8) & 15;
         const int j0 = T.jsh & 15, j1 = (T.jsh >> 4) & 15, j2 = (T.jsh >> 8) & 15;
-        const float q0 = __shfl(sh.q, 2 * j0 + c), q1 = __shfl(sh.q, 2 * j1 + c);
-        const float q2 = __shfl(sh.q, 2 * j2 + c);
+        const bool r0 = T.raw & 1, r1 = (T.raw >> 1) & 1, r2 = (T.raw >> 2) & 1;
+        const float q0 = __shfl(r0 ? sh.q : sh.v, 2 * j0 + c);
+        const float q1 = __shfl(r1 ? sh.q : sh.v, 2 * j1 + c);
+        const float q2 = __shfl(r2 ? sh.q : sh.v, 2 * j2 + c);
         const float v = k0 == SK_SHARED ? q0 : (k0 == SK_CONST ? T.cval[0] : 0.f);
         const float m = k1 == SK_SHARED ? q1 : (k1 == SK_CONST ? T.cval[1] : 0.f);
         const float sc = k2 == SK_SHARED ? q2 : (k2 == SK_CONST ? T.cval[2] : 0.f);
@@ -676,11 +693,12 @@ MC_DEV void lr_scalar_terms(int n_sterms, int n_generic, const LrSterm* st, cons
             (k1 == SK_SHARED || k2 == SK_SHARED) ? lgamma_norm(T.dist, m, sc) : T.clg;
         const ElemOut e = elem_eval(T.dist, T.c0, v, m, sc, ls, lgx);
         lpg += T.wn * e.lp;
-        float y = 0.0f;
-        if (k0 == SK_SHARED && j0 == xk) y += T.wn * e.dv;
-        if (k1 == SK_SHARED && j1 == xk) y += T.wn * e.dm;
-        if (k2 == SK_SHARED && j2 == xk) y += T.wn * e.ds;
+        float y = 0.0f, yr = 0.0f;
+        if (k0 == SK_SHARED && j0 == xk) (r0 ? yr : y) += T.wn * e.dv;
+        if (k1 == SK_SHARED && j1 == xk) (r1 ? yr : y) += T.wn * e.dm;
+        if (k2 == SK_SHARED && j2 == xk) (r2 ? yr : y) += T.wn * e.ds;
         g_self += y;
+        g_raw += yr;
     }
     lp[0] += rl(lpg, 0);
     lp[1] += rl(lpg, 1);
@@ -771,6 +789,10 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     for (int k = 1; k < kLrMaxShared; ++k) xg = (xk == k) ? P.shl[k] : xg;
     const int64_t xch_id = xc ? cc[1] : cc[0];
     const bool xlive = xon && (xc ? live[1] : live[0]);
+    int xxf = P.shxf[0];  // the lane's parameter's transform
+#pragma unroll
+    for (int k = 1; k < kLrMaxShared; ++k) xxf = (xk == k) ? P.shxf[k] : xxf;
+    xxf = xon ? xxf : MC_XF_NONE;
 
     float* sd = smem;
     const int64_t* blk = P.blocks + 4 * (int64_t)slice;
@@ -803,6 +825,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     sh.q = xon ? st_q[xch_id * D + xg] : 1.0f;
     sh.g = xon ? st_g[xch_id * D + xg] : 0.0f;
     sh.p = 0.0f;
+    sh.v = xf_apply(xxf, sh.q);
     double eps[2];
     float lp[2];
     int nacc[2], ntot[2], wacc[2], wtot[2];
@@ -934,9 +957,10 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             pj = pj + xh * sh.g;
             sh.p = pj;
             sh.q = sh.q + xe * pj;
-            sh.is = 1.0f / sh.q;
-            sh.iv = 1.0f / (sh.q * sh.q);
-            sh.lg = logf(sh.q);
+            sh.v = xf_apply(xxf, sh.q);  // (mx.exp(log_sigma) ...: the terms' value)
+            sh.is = 1.0f / sh.v;
+            sh.iv = 1.0f / (sh.v * sh.v);
+            sh.lg = logf(sh.v);
         };
         LrMoments<RS> M;
         drift_private(false);
@@ -1024,8 +1048,9 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
 #pragma unroll
             for (int ps = 0; ps < NPASS; ++ps)
                 y0[ps] = (!X1 && poll_lane && 4 * ps + (j >> 4) < NPAIR) ? granule_load(gp + 4 * ps) : 0ull;
-            float slp[2] = {0.f, 0.f}, sg_self = 0.0f;
-            lr_scalar_terms(P.n_sterms, P.n_sterms_generic, sst, own, sh, j, Dsh, slp, sg_self);
+            float slp[2] = {0.f, 0.f}, sg_self = 0.0f, sg_raw = 0.0f;
+            lr_scalar_terms(P.n_sterms, P.n_sterms_generic, sst, own, sh, j, Dsh, slp, sg_self,
+                            sg_raw);
             MC_STAMP(7);
             float vals[NPASS];
             uint32_t need = 0;
@@ -1086,7 +1111,9 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
 #pragma unroll
                 for (int k = 0; k < NSH; ++k)
                     if (xk == k) gx = xc ? tot[2 + 2 * k + 1] : tot[2 + 2 * k];
-                sh.g = xon ? gx + sg_self : 0.0f;
+                // the value's cotangent through the transform's VJP, then the
+                // raw-parameter terms (eval.h xf_chain: the tape's arithmetic)
+                sh.g = xon ? xf_chain(xxf, gx + sg_self, sh.q, sh.v) + sg_raw : 0.0f;
             }
 #pragma unroll
             for (int c = 0; c < 2; ++c) {

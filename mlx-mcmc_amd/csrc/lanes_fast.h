@@ -342,6 +342,19 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     for (int k = 1; k < kLrMaxShared; ++k) xg = (xo == k) ? P.shl[k] : xg;
     const int64_t xch_id = xc ? cc[1] : cc[0];
     const bool xlive = xon && (xc ? live[1] : live[0]);
+    // a transformed shared parameter (lanes.h LrCtx::shxf) and the identity
+    // terms over its raw value: a uniform branch, so programs without them
+    // run the same instructions as before
+    const bool hxf = P.has_xf != 0;
+    int xxf = P.shxf[0];
+    float xid = P.shid[0];
+#pragma unroll
+    for (int k = 1; k < kLrMaxShared; ++k) {
+        xxf = (xo == k) ? P.shxf[k] : xxf;
+        xid = (xo == k) ? P.shid[k] : xid;
+    }
+    xxf = xon ? xxf : MC_XF_NONE;
+    xid = xon ? xid : 0.0f;
 
     LrPriv<RS> R0;  // (loaded as in k_hmc_lr, then packed per slot)
     int gk[RS];
@@ -362,6 +375,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     sh.q = xon ? st_q[xch_id * D + xg] : 1.0f;
     sh.g = xon ? st_g[xch_id * D + xg] : 0.0f;
     sh.p = 0.0f;
+    sh.v = hxf ? xf_apply(xxf, sh.q) : sh.q;
     sh.is = sh.iv = 1.0f;
     sh.lg = 0.0f;
     double eps[2];
@@ -534,14 +548,16 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             pj = pj + xh * sh.g;
             sh.p = pj;
             sh.q = sh.q + xe * pj;
+            sh.v = sh.q;
+            if (hxf) sh.v = xf_apply(xxf, sh.q);  // (mx.exp(log_sigma) ...: the terms' value)
             // the shared scale's reciprocals and log (moment form): hardware
             // v_rcp_f32 / v_log_f32 (<= 1 ulp) instead of the IEEE division
             // and logf sequences — one dependent chain of ~40 VALU on every
             // step's critical path becomes 5; the same bits in every slice,
             // so the replicas stay identical
-            sh.is = __builtin_amdgcn_rcpf(sh.q);
+            sh.is = __builtin_amdgcn_rcpf(sh.v);
             sh.iv = sh.is * sh.is;
-            sh.lg = __builtin_amdgcn_logf(sh.q) * 0.693147180559945f;  // log2 q * ln 2
+            sh.lg = __builtin_amdgcn_logf(sh.v) * 0.693147180559945f;  // log2 v * ln 2
         };
         f2 M1[RS], M2[RS];
         drift_private(false);
@@ -601,7 +617,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 }
             }
             if (DIR) {
-                const f2 um = DM ? lf_sh2(sh.q, kdm) : d_m;
+                const f2 um = DM ? lf_sh2(sh.v, kdm) : d_m;
                 const f2 is = DS ? lf_sh2(sh.is, kds) : d_cinv;
                 const f2 iv = DS ? is * is : d_cinv2;
 #pragma unroll
@@ -625,7 +641,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             // enters slice 0's record
             float g_own = 0.0f;
             {
-                const float v = sh.q;
+                const float v = sh.v;
                 const float d = own.hn ? v : v - o_m;
                 const bool out = own.hn && !(v >= 0.0f);
                 g_own = (out || !own.on) ? 0.0f : o_wn * -(d * o_cinv2);
@@ -635,6 +651,11 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     const float lp_own = o_wn * lpe;
                     if (own_lp0) lpp[0] += lp_own;
                     if (own_lp1) lpp[1] += lp_own;
+                    // the identity terms over the raw parameter (log-Jacobians)
+                    if (hxf && slice == 0 && xon) {
+                        if (xc == 0) lpp[0] += xid * sh.q;
+                        else lpp[1] += xid * sh.q;
+                    }
                 }
             }
             MC_STAMP(1);
@@ -808,7 +829,11 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
 #pragma unroll
                 for (int ps = 0; ps < NPASS_V; ++ps)
                     if (col == ps) gx = tot[ps];  // lane 16 row + P / 4 holds pair P
-                sh.g = xon ? gx + g_own : 0.0f;
+                float gt = gx + g_own;
+                // the value's cotangent through the transform's VJP, plus the
+                // raw identity terms (eval.h xf_chain: the tape's arithmetic)
+                if (hxf) gt = xf_chain(xxf, gt, sh.q, sh.v) + xid;
+                sh.g = xon ? gt : 0.0f;
             }
             if (l == 0) {
                 constexpr int p0 = NV, p1 = NV + 1;

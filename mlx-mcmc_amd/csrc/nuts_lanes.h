@@ -219,6 +219,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         }
     };
     auto derive = [&]() {
+        sh.v = sh.q;  // (NUTS programs carry no transformed parameter: api.hip use_nuts_lanes)
         sh.is = 1.0f / sh.q;
         sh.iv = 1.0f / (sh.q * sh.q);
         sh.lg = logf(sh.q);
@@ -302,10 +303,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
             lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp);
         }
         MC_STAMP(3);
-        float slp[2] = {0.f, 0.f}, sg_self = 0.0f;
+        float slp[2] = {0.f, 0.f}, sg_self = 0.0f, sg_raw = 0.0f;
         if constexpr (!REG)
             lr_scalar_terms(P.n_sterms, SPEC ? 0 : P.n_sterms_generic, sst, own, sh, j, Dsh, slp,
-                            sg_self);
+                            sg_self, sg_raw);
         MC_STAMP(18);
         if (Dsh == 0) {  // no shared cotangents: one reduction
             sh.g = 0.0f;

@@ -6,7 +6,12 @@ nuts.py:76-87); the unconstrained-scale forms `Normal(mu, mx.exp(log_sigma))`
 log-transformed positive vector `Normal(m, s).log_prob(mx.log(x)) -
 mx.sum(mx.log(x))` run on the GPU tape (eval.h xf_apply / xf_chain) and are
 checked against the CPU oracle, whose gradients are torch autograd over the
-same user model, and against known answers:
+same user model, and against known answers.  Programs whose transforms act on
+broadcast parameters only (the log-scale hierarchical model) also run on the
+lane-resident kernels — the fast form k_hmc_lf (lanes_fast.h: the shared
+value xf(q) beside q, the identity terms' weights in the holder lane) and the
+general k_hmc_lr (lanes.h LrCtx::shxf) — sliced or not, and are checked
+against the tape kernel and the oracle there:
 
   * tape log p within 2e-6 of sum |lp| (f32 summation order), gradients
     rtol 1e-4 (the device's expf / logf are not the CPU's: <= 2 ulp each);
@@ -45,8 +50,6 @@ def test_transform_tape_matches_autograd(gpu, model):
 
     lp_fn, init = MODELS[model](W.ns_product())
     prog = _trace.compile_model(lp_fn, init)
-    assert prog.num_slices == 1 and prog.slice_kernel == "unsliced"   # the tape kernels
-    assert "transformed" in prog.kernel_note or "affine" in prog.kernel_note
     olp, oinit = MODELS[model](W.ns_oracle())
     M = S.EagerModel(olp, oinit)
     rng = np.random.default_rng(11)
@@ -75,9 +78,32 @@ def test_transform_logp_at_negative_log_argument_is_nan(gpu):
     assert np.isnan(lp.cpu().numpy()[0])
 
 
-@pytest.mark.parametrize("model,seed", [("hier_reparam", 0), ("hier_reparam", 1),
-                                        ("lognormal", 0)])
-def test_transform_hmc_trace_matches_oracle(gpu, model, seed):
+def test_transform_kernel_selection(gpu):
+    """Broadcast-parameter transforms: the lane-resident kernels (the fast form
+    included; not the term interpreter, not NUTS lanes); transforms of
+    per-element parameters and affine programs: the tape kernels, with the
+    reason in the kernel note."""
+    from mlx_mcmc_amd import _lib, _trace
+
+    big = _trace.compile_model(*W.hierarchical_reparam(W.ns_product(), *W.SHAPES["large"]))
+    assert big.num_slices == 16 and big.slice_kernel == "lanes" and big.lanes_fast
+    assert big.kernel_note == ""
+    with pytest.raises(_lib.EngineError, match="interpreter"):
+        big.set_slice_kernel("interpreter")
+    assert big.slice_kernel == "lanes"
+    small = _trace.compile_model(*MODELS["hier_reparam"](W.ns_product()))
+    assert small.num_slices == 1 and small.slice_kernel == "lanes"
+    assert small.nuts_kernel(10) == "tape"
+    for name, why in (("eight_schools_nc_log", "affine"), ("lognormal", "transformed")):
+        prog = _trace.compile_model(*MODELS[name](W.ns_product()))
+        assert prog.slice_kernel == "unsliced" and why in prog.kernel_note, prog.kernel_note
+
+
+@pytest.mark.parametrize("model,seed,slices", [("hier_reparam", 0, 0), ("hier_reparam", 1, 0),
+                                               ("hier_reparam", 0, 1), ("lognormal", 0, 0)])
+def test_transform_hmc_trace_matches_oracle(gpu, model, seed, slices):
+    """slices = 0: the automatic plan (k_hmc_lr with one slice for the
+    log-scale hierarchical model, the tape for the log-normal); 1: the tape."""
     import mlx_mcmc_amd as m
 
     lp, init = MODELS[model](W.ns_product())
@@ -91,8 +117,9 @@ def test_transform_hmc_trace_matches_oracle(gpu, model, seed):
     kw = dict(num_samples=40, num_warmup=40, step_size=eps, num_leapfrog_steps=10,
               adapt_step_size=False)
     s, rate, info = m.hmc(lp, init, key=m.random.key(seed), progress=False, return_info=True,
-                          return_trace=True, **kw)
-    assert info.extra["kernel"] == "unsliced"
+                          return_trace=True, num_slices=slices, **kw)
+    want = "lanes" if (model == "hier_reparam" and slices == 0) else "unsliced"
+    assert info.extra["kernel"] == want
     ref = S.hmc(olp, init, seed=seed, **kw)
     n = len(ref.trace["accepted"])
     tr = info.trace
@@ -106,6 +133,48 @@ def test_transform_hmc_trace_matches_oracle(gpu, model, seed):
     k = max(0, same - 40)
     first = np.asarray(s[list(init)[0]]).reshape(kw["num_samples"], -1)  # layout offset 0
     np.testing.assert_allclose(first[:k], ref.samples[:k, :first.shape[1]], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape,kernel", [("medium", "fast"), ("large", "fast"),
+                                          ("large", "general")])
+def test_transform_lanes_match_tape(gpu, shape, kernel):
+    """The log-scale hierarchical model sliced onto k_hmc_lf / k_hmc_lr (4 /
+    16 slices) against the tape kernel k_hmc on the same chains, with the
+    reference's warmup rule acting (mixed decisions): decisions, ratios and
+    H_init equal until a proven near-tie (tests/_near_tie.py), step sizes
+    bit-identical, draws within rtol 1e-4 before it."""
+    import mlx_mcmc_amd as m
+    from _near_tie import compare_trace
+    from mlx_mcmc_amd import _lib
+
+    lp, init = W.hierarchical_reparam(W.ns_product(), *W.SHAPES[shape])
+    kw = dict(num_samples=15, num_warmup=15, step_size=3e-3, num_leapfrog_steps=20,
+              key=m.random.key(3), num_chains=16, progress=False, return_info=True,
+              return_trace=True)
+    a, _, ia = m.hmc(lp, init, num_slices=1, **kw)
+    if kernel == "general":
+        _lib.load().mc_debug_lanes_fast(0)
+    try:
+        b, _, ib = m.hmc(lp, init, **kw)
+    finally:
+        _lib.load().mc_debug_lanes_fast(1)
+    assert ia.extra["kernel"] == "unsliced" and ib.extra["kernel"] == "lanes"
+    acc = ia.trace["accepted"].astype(bool)
+    assert 0 < acc.mean() < 1, "the regime must mix accepts and rejects"
+    full = 0
+    for c in range(16):
+        ref = {"accepted": ia.trace["accepted"][c], "ratio": ia.trace["accept_stat"][c],
+               "energy": ia.trace["energy"][c], "step_size": ia.trace["step_size"][c],
+               "log_u": log_u(3, c, 30)}
+        got = {"accepted": ib.trace["accepted"][c], "ratio": ib.trace["accept_stat"][c],
+               "energy": ib.trace["energy"][c], "step_size": ib.trace["step_size"][c]}
+        same = compare_trace(got, ref, f"{shape} chain {c}")
+        full += same == 30
+        ns = max(0, same - 15)
+        for k in a:
+            np.testing.assert_allclose(b[k][c, :ns], a[k][c, :ns], rtol=1e-4, atol=1e-5)
+    print(f"{shape}: {full} of 16 chains agree over all 30 iterations")
+    assert full >= 10, "most chains agree over the whole run (the rest to a proven near-tie)"
 
 
 def test_transform_nuts_trace_matches_oracle(gpu):
@@ -142,27 +211,46 @@ def test_transform_mh_trace_matches_oracle(gpu):
     np.testing.assert_allclose(s["x"], ref.samples, rtol=1e-5, atol=1e-6)
 
 
-def test_hier_reparam_posterior_within_one_percent(gpu):
-    """The small hierarchical shape in (mu, log tau, log sigma, theta): its
-    exact moments are the fixture's (log tau, log sigma) grid moments and the
+# shape -> (slices, step size, leapfrog steps, chains, warmup, samples, batch)
+REPARAM = {"small_tape": ("small", 1, 0.02, 50, 1024, 1000, 20000, 2000),
+           "small": ("small", 0, 0.02, 50, 1024, 1000, 20000, 2000),
+           "large": ("large", 0, 2e-3, 20, 256, 1000, 60000, 3000),
+           "large_general": ("large", 0, 2e-3, 20, 256, 1000, 60000, 3000)}
+
+
+@pytest.mark.parametrize("case", list(REPARAM))
+def test_hier_reparam_posterior_within_one_percent(gpu, case):
+    """The hierarchical model in (mu, log tau, log sigma, theta): its exact
+    moments are the fixture's (log tau, log sigma) grid moments and the
     (mu, theta) ones (tests/test_exact_posterior.py pins the change of
-    variables)."""
+    variables).  small_tape: the tape kernel k_hmc; small / large: the
+    automatic plan, the lane-resident kernels with one / 16 slices (k_hmc_lf;
+    large_general: k_hmc_lr)."""
     from mlx_mcmc_amd import _trace
 
+    shape, slices, eps, L, C, Wm, S_, batch = REPARAM[case]
     with open(os.path.join(GOLD, "posterior_exact.json")) as f:
-        ex = json.load(f)["shapes"]["small"]
+        ex = json.load(f)["shapes"][shape]
     mean = np.array(ex["mean"])
     var = np.array(ex["var"])
     mean[1:3] = ex["log_tau_sigma_mean"]
     var[1:3] = ex["log_tau_sigma_var"]
-    lp, init = W.hierarchical_reparam(W.ns_product(), *W.SHAPES["small"])
-    prog = _trace.compile_model(lp, init)
-    g = stream_moments(prog, "hmc", 1024, prog.layout.flatten(init), step_size=0.02,
-                       num_warmup=1000, num_samples=20000, batch=2000, num_leapfrog_steps=50)
-    print(f"hier reparam small: kernel {prog.slice_kernel}, accept "
+    from mlx_mcmc_amd import _lib
+
+    lp, init = W.hierarchical_reparam(W.ns_product(), *W.SHAPES[shape])
+    prog = _trace.compile_model(lp, init, slices=slices)
+    assert prog.slice_kernel == ("unsliced" if slices == 1 else "lanes")
+    if case == "large_general":
+        _lib.load().mc_debug_lanes_fast(0)  # k_hmc_lr instead of k_hmc_lf
+    try:
+        g = stream_moments(prog, "hmc", C, prog.layout.flatten(init), step_size=eps,
+                           num_warmup=Wm, num_samples=S_, batch=batch, num_leapfrog_steps=L)
+    finally:
+        _lib.load().mc_debug_lanes_fast(1)
+    print(f"hier reparam {case}: kernel {prog.slice_kernel} ({prog.num_slices} slices), accept "
           f"{g['accept_rate'].mean():.3f} (min {g['accept_rate'].min():.3f})")
     assert g["accept_rate"].min() > 0.5
-    check_within_one_percent(g, {"mean": mean, "var": var}, label="hierarchical small (log scales)",
+    check_within_one_percent(g, {"mean": mean, "var": var}, label=f"hierarchical {case} (log scales)",
                              z=Z)
 
 
