@@ -77,10 +77,12 @@ typedef enum {
     MC_DIST_EXPONENTIAL = 2,  /* exponential.py:48-71  (value, -, rate)      */
     MC_DIST_GAMMA       = 3,  /* gamma.py:40-88        (value, alpha, beta)  */
     MC_DIST_BETA        = 4,  /* beta.py:37-91         (value, alpha, beta)  */
-    MC_DIST_IDENTITY    = 5   /* weight * sum_i value_i   (value, -, -):  a   */
+    MC_DIST_IDENTITY    = 5,  /* weight * sum_i value_i   (value, -, -):  a   */
                               /* parameter expression added to the log      */
                               /* density (the Jacobian of a reparameterised */
                               /* parameter, `lp + log_sigma`)               */
+    MC_DIST_EXPR        = 6   /* weight * sum_i root_i of an elementwise     */
+                              /* expression (mc_expr, mc_program_create_expr) */
 } mc_dist_kind;
 
 typedef enum {
@@ -137,6 +139,56 @@ typedef struct mc_affine {
     mc_operand slope, x;
 } mc_affine;
 
+/* Expression terms (MC_DIST_EXPR).  The reference differentiates ANY MLX
+ * expression of the parameters (hmc.py:53-67 mx.grad over the user's
+ * log_prob, nuts.py:76-87); the fused terms above cover the distribution
+ * shapes, and an expression term covers everything else that is elementwise:
+ *     weight * sum_i root_i
+ * where the term's nodes form a DAG evaluated per broadcast element i in f32
+ * (MLX's elementwise ops, each rounded once) and differentiated in reverse
+ * mode with the VJPs mx.grad uses.  Node k's arguments are nodes of the same
+ * term with smaller indices (a, b, c; -1 = unused); the last node is the
+ * root.  Leaves are mc_operands: CONST, PSCALAR, DATA, PVEC or GATHER
+ * (transform MC_XF_NONE — mx.exp / mx.log are nodes here).  Vector leaves
+ * have the term's length n.  Every non-injective GATHER leaf of a term must
+ * use the same index values (e.g. alpha[g] + beta[g] * x): the term is then
+ * evaluated per group run (segmented, deterministic); anything else is
+ * strided.  A term holds at most MC_EXPR_MAX_NODES nodes.                 */
+#define MC_EXPR_MAX_NODES 32
+typedef enum {
+    MC_EX_LEAF    = 0,   /* the node's operand                               */
+    MC_EX_ADD     = 1,   /* a + b                                            */
+    MC_EX_SUB     = 2,   /* a - b                                            */
+    MC_EX_MUL     = 3,   /* a * b                                            */
+    MC_EX_DIV     = 4,   /* a / b                                            */
+    MC_EX_NEG     = 5,   /* -a                                               */
+    MC_EX_EXP     = 6,   /* exp a                                            */
+    MC_EX_LOG     = 7,   /* log a                                            */
+    MC_EX_SQRT    = 8,   /* sqrt a                                           */
+    MC_EX_SQUARE  = 9,   /* a * a                                            */
+    MC_EX_POW     = 10,  /* a ** b                                           */
+    MC_EX_ABS     = 11,  /* |a|                                              */
+    MC_EX_LOG1P   = 12,  /* log(1 + a)                                       */
+    MC_EX_TANH    = 13,  /* tanh a                                           */
+    MC_EX_SIGMOID = 14,  /* 1 / (1 + exp(-a))                                */
+    MC_EX_NORMAL_LP      = 15,  /* Normal(b, c).log_prob(a)  normal.py:49-56 */
+    MC_EX_HALFNORMAL_LP  = 16,  /* HalfNormal(c).log_prob(a) halfnormal.py:43-63 */
+    MC_EX_EXPONENTIAL_LP = 17,  /* Exponential(c).log_prob(a) exponential.py:48-71 */
+    MC_EX_WHERE   = 18   /* a != 0 ? b : c, a a CONST / DATA leaf (mx.where  */
+                         /* over a data mask; no cotangent through a)        */
+} mc_expr_op;
+
+typedef struct mc_expr_node {
+    int32_t    op;         /* mc_expr_op                                    */
+    int32_t    a, b, c;    /* argument nodes (index within the term), or -1 */
+    mc_operand leaf;       /* MC_EX_LEAF                                    */
+} mc_expr_node;
+
+/* The nodes of one expression term: nodes[first .. first + count). */
+typedef struct mc_expr {
+    int32_t first, count;
+} mc_expr;
+
 typedef struct mc_program mc_program;
 
 /* Build a program.  data / index are HOST arrays; the library copies them to
@@ -158,6 +210,19 @@ int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
                              const float* data, int64_t n_data,
                              const int32_t* index, int64_t n_index,
                              mc_program** out);
+/* mc_program_create_affine with expression terms: a term whose dist is
+ * MC_DIST_EXPR names exprs[k] through its `affine` field (k + 1) and leaves
+ * value / loc / scale MC_OP_NONE.  Expression programs run on the
+ * chain-per-workgroup kernels (k_hmc, k_nuts, k_mh, mc_logp_grad); the
+ * sliced planners decline them.                                           */
+int mc_program_create_expr(const mc_term* terms, int32_t n_terms,
+                           const mc_affine* affines, int32_t n_affines,
+                           const mc_expr* exprs, int32_t n_exprs,
+                           const mc_expr_node* nodes, int32_t n_nodes,
+                           int32_t n_params, float lp_const,
+                           const float* data, int64_t n_data,
+                           const int32_t* index, int64_t n_index,
+                           mc_program** out);
 int mc_program_destroy(mc_program* prog);
 int32_t mc_program_num_params(const mc_program* prog);
 /* The launch geometry the engine picked: waves per chain (1, 4 or 16).     */

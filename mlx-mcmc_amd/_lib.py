@@ -39,6 +39,13 @@ MC_DIST_EXPONENTIAL = 2
 MC_DIST_GAMMA = 3
 MC_DIST_BETA = 4
 MC_DIST_IDENTITY = 5
+MC_DIST_EXPR = 6
+
+# mc_expr_op (expression-term nodes)
+(MC_EX_LEAF, MC_EX_ADD, MC_EX_SUB, MC_EX_MUL, MC_EX_DIV, MC_EX_NEG, MC_EX_EXP, MC_EX_LOG,
+ MC_EX_SQRT, MC_EX_SQUARE, MC_EX_POW, MC_EX_ABS, MC_EX_LOG1P, MC_EX_TANH, MC_EX_SIGMOID,
+ MC_EX_NORMAL_LP, MC_EX_HALFNORMAL_LP, MC_EX_EXPONENTIAL_LP, MC_EX_WHERE) = range(19)
+MC_EXPR_MAX_NODES = 32
 
 # mc_series_stats fields (include/mcmc355.h)
 MC_ST_ESS, MC_ST_MEAN, MC_ST_M2, MC_ST_HMEAN0, MC_ST_HMEAN1, MC_ST_HM2_0, MC_ST_HM2_1 = range(7)
@@ -92,6 +99,25 @@ class McAffine(ctypes.Structure):
     _fields_ = [
         ("slope", McOperand),
         ("x", McOperand),
+    ]
+
+
+class McExprNode(ctypes.Structure):
+    """mc_expr_node: op, argument nodes a, b, c (-1 unused), the leaf operand."""
+    _fields_ = [
+        ("op", ctypes.c_int32),
+        ("a", ctypes.c_int32),
+        ("b", ctypes.c_int32),
+        ("c", ctypes.c_int32),
+        ("leaf", McOperand),
+    ]
+
+
+class McExpr(ctypes.Structure):
+    """mc_expr: nodes[first .. first + count) of one expression term."""
+    _fields_ = [
+        ("first", ctypes.c_int32),
+        ("count", ctypes.c_int32),
     ]
 
 
@@ -156,6 +182,11 @@ SIGNATURES = [
       _VP, ctypes.c_int64, _VP, ctypes.c_int64, ctypes.POINTER(_VP)]),
     ("mc_program_create_affine", ctypes.c_int,
      [ctypes.POINTER(McTerm), ctypes.c_int32, ctypes.POINTER(McAffine), ctypes.c_int32,
+      ctypes.c_int32, ctypes.c_float, _VP, ctypes.c_int64, _VP, ctypes.c_int64,
+      ctypes.POINTER(_VP)]),
+    ("mc_program_create_expr", ctypes.c_int,
+     [ctypes.POINTER(McTerm), ctypes.c_int32, ctypes.POINTER(McAffine), ctypes.c_int32,
+      ctypes.POINTER(McExpr), ctypes.c_int32, ctypes.POINTER(McExprNode), ctypes.c_int32,
       ctypes.c_int32, ctypes.c_float, _VP, ctypes.c_int64, _VP, ctypes.c_int64,
       ctypes.POINTER(_VP)]),
     ("mc_program_destroy", ctypes.c_int, [_VP]),

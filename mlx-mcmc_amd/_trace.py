@@ -34,9 +34,20 @@ mx.exp(log_sigma))``, ``HalfNormal(1).log_prob(mx.exp(log_tau))``,
 ``mu + mx.exp(log_tau) * z``, ``Normal(0, 1).log_prob(mx.log(x))``; and a
 parameter expression added to a log density (``lp + log_sigma``, the
 Jacobian of the transform; ``lp - mx.log(x)``; ``mx.sum(log_x)``) is an
-*identity* term ``weight * sum_i value_i`` (MC_DIST_IDENTITY).  Anything else
-(two products, exp of an expression, a product of two parameters used as a
-scale ...) raises ``TraceError``.
+*identity* term ``weight * sum_i value_i`` (MC_DIST_IDENTITY).
+
+Everything else that is elementwise — two predictors ``a + b1 * x1 + b2 *
+x2``, ``exp`` of an expression, products and quotients of parameters,
+``mx.sqrt`` / ``mx.square`` / ``**`` / ``mx.log1p`` / ``mx.tanh`` /
+``mx.sigmoid`` / ``mx.abs``, ``mx.where`` over a data mask, Normal /
+HalfNormal / Exponential whose arguments are such expressions, and any such
+expression summed into the log density — traces to an *expression* term
+(``Expr``, MC_DIST_EXPR): a DAG of f32 elementwise ops evaluated and
+differentiated per element by the chain-per-workgroup kernels (eval.h
+eval_expr), as mx.grad differentiates the reference's MLX graph.  Gamma /
+Beta with expression arguments, indexing an expression, reductions other
+than a full ``mx.sum`` and Python branches on traced values raise
+``TraceError``.
 """
 from __future__ import annotations
 
@@ -144,35 +155,65 @@ class Param:
     def _unsupported(self, *a, **k):
         raise TraceError(f"arithmetic on traced parameter '{self.name}': " + _UNSUPPORTED)
 
-    # affine arithmetic (a + b * x): see Affine
+    # affine arithmetic (a + b * x, the fast fused paths): see Affine; any
+    # other elementwise arithmetic builds an expression (Expr)
     def __mul__(self, other):
-        return Affine.product(self, other)
+        if isinstance(other, Expr):
+            return Expr.binary(_lib.MC_EX_MUL, self, other)
+        return _affine_or_expr(lambda: Affine.product(self, other), _lib.MC_EX_MUL, self, other)
 
-    __rmul__ = __mul__
+    def __rmul__(self, other):
+        if isinstance(other, Expr):
+            return Expr.binary(_lib.MC_EX_MUL, other, self)
+        return _affine_or_expr(lambda: Affine.product(other, self), _lib.MC_EX_MUL, other, self)
 
     def __add__(self, other):
         if isinstance(other, LogProbExpr):
             return other + self
-        return Affine.lift(self) + other
+        if isinstance(other, Expr):
+            return Expr.binary(_lib.MC_EX_ADD, self, other)
+        return _affine_or_expr(lambda: Affine.lift(self) + other, _lib.MC_EX_ADD, self, other)
 
     def __radd__(self, other):
         if isinstance(other, LogProbExpr):
             return other + self
-        return Affine.lift(self) + other
+        if isinstance(other, Expr):
+            return Expr.binary(_lib.MC_EX_ADD, other, self)
+        return _affine_or_expr(lambda: Affine.lift(self) + other, _lib.MC_EX_ADD, other, self)
 
     def __sub__(self, other):
         if isinstance(other, LogProbExpr):
             return (-other) + self
-        return Affine.lift(self) + (-1.0) * other if not isinstance(other, Affine) else \
-            Affine.lift(self) + other * -1.0
+        if isinstance(other, Expr):
+            return Expr.binary(_lib.MC_EX_SUB, self, other)
+        return _affine_or_expr(
+            lambda: (Affine.lift(self) + (-1.0) * other if not isinstance(other, Affine) else
+                     Affine.lift(self) + other * -1.0), _lib.MC_EX_SUB, self, other)
 
     def __rsub__(self, other):
-        return Affine.product(-1.0, self) + other
+        if isinstance(other, Expr):
+            return Expr.binary(_lib.MC_EX_SUB, other, self)
+        return _affine_or_expr(lambda: Affine.product(-1.0, self) + other, _lib.MC_EX_SUB,
+                               other, self)
 
     def __neg__(self):
         return Affine.product(-1.0, self)
 
-    __truediv__ = __rtruediv__ = __pow__ = __abs__ = _unsupported
+    def __truediv__(self, other):
+        return Expr.binary(_lib.MC_EX_DIV, self, other)
+
+    def __rtruediv__(self, other):
+        return Expr.binary(_lib.MC_EX_DIV, other, self)
+
+    def __pow__(self, other):
+        return Expr.binary(_lib.MC_EX_POW, self, other)
+
+    def __rpow__(self, other):
+        return Expr.binary(_lib.MC_EX_POW, other, self)
+
+    def __abs__(self):
+        return Expr.unary(_lib.MC_EX_ABS, self)
+
     __lt__ = __le__ = __gt__ = __ge__ = _unsupported
 
     def __float__(self):
@@ -190,7 +231,7 @@ def _is_slope(x) -> bool:
     """A constant or a scalar parameter (an affine slope)."""
     if isinstance(x, Param):
         return x.shape == ()
-    if isinstance(x, (Affine, LogProbExpr)):
+    if isinstance(x, (Affine, LogProbExpr, Expr)):
         return False
     try:
         return np.asarray(_to_numpy(x)).size == 1 and np.asarray(_to_numpy(x)).ndim == 0
@@ -200,7 +241,7 @@ def _is_slope(x) -> bool:
 
 def _is_term_operand(x) -> bool:
     """Something to_operand accepts (a parameter or view, data, a constant)."""
-    return not isinstance(x, (Affine, LogProbExpr))
+    return not isinstance(x, (Affine, LogProbExpr, Expr))
 
 
 class Affine:
@@ -239,6 +280,18 @@ class Affine:
     def __add__(self, other):
         if isinstance(other, LogProbExpr):
             return other + self
+        if isinstance(other, Expr):
+            return Expr.binary(_lib.MC_EX_ADD, self, other)
+        return _affine_or_expr(lambda: self._add(other), _lib.MC_EX_ADD, self, other)
+
+    def __radd__(self, other):
+        if isinstance(other, LogProbExpr):
+            return other + self
+        if isinstance(other, Expr):
+            return Expr.binary(_lib.MC_EX_ADD, other, self)
+        return _affine_or_expr(lambda: self._add(other), _lib.MC_EX_ADD, other, self)
+
+    def _add(self, other):
         o = Affine.lift(other)
         if self.x is not None and o.x is not None:
             raise TraceError("a sum of two products (a + b*x + c*z): only loc + slope * x "
@@ -265,24 +318,47 @@ class Affine:
         prod = self if self.x is not None else o
         return Affine(loc, prod.slope, prod.x)
 
-    __radd__ = __add__
-
     def __sub__(self, other):
         if isinstance(other, LogProbExpr):
             return (-other) + self
+        if isinstance(other, (Affine, Expr)):
+            return Expr.binary(_lib.MC_EX_SUB, self, other)
         if isinstance(other, Param):
-            return self + Affine.product(-1.0, other)
-        if isinstance(other, Affine):
-            raise TraceError("subtracting an affine expression: " + _UNSUPPORTED)
-        return self + (-np.asarray(_to_numpy(other), np.float32))
+            return _affine_or_expr(lambda: self._add(Affine.product(-1.0, other)),
+                                   _lib.MC_EX_SUB, self, other)
+        return _affine_or_expr(lambda: self._add(-np.asarray(_to_numpy(other), np.float32)),
+                               _lib.MC_EX_SUB, self, other)
 
     def __rsub__(self, other):
-        raise TraceError("subtracting an affine expression: " + _UNSUPPORTED)
+        return Expr.binary(_lib.MC_EX_SUB, other, self)
+
+    def __mul__(self, other):
+        return Expr.binary(_lib.MC_EX_MUL, self, other)
+
+    def __rmul__(self, other):
+        return Expr.binary(_lib.MC_EX_MUL, other, self)
+
+    def __truediv__(self, other):
+        return Expr.binary(_lib.MC_EX_DIV, self, other)
+
+    def __rtruediv__(self, other):
+        return Expr.binary(_lib.MC_EX_DIV, other, self)
+
+    def __pow__(self, other):
+        return Expr.binary(_lib.MC_EX_POW, self, other)
+
+    def __rpow__(self, other):
+        return Expr.binary(_lib.MC_EX_POW, other, self)
+
+    def __neg__(self):
+        return Expr.unary(_lib.MC_EX_NEG, self)
+
+    def __abs__(self):
+        return Expr.unary(_lib.MC_EX_ABS, self)
 
     def _unsupported(self, *a, **k):
         raise TraceError("this operation on a traced parameter expression: " + _UNSUPPORTED)
 
-    __mul__ = __rmul__ = __truediv__ = __rtruediv__ = __pow__ = __neg__ = __abs__ = _unsupported
     __getitem__ = __lt__ = __le__ = __gt__ = __ge__ = _unsupported
 
     def __float__(self):
@@ -299,6 +375,176 @@ class Affine:
 
     def __repr__(self):
         return f"Affine({self.loc!r} + {self.slope!r} * {self.x!r})"
+
+
+def _affine_or_expr(build, op, a, b):
+    """The affine form when it exists (the fused fast paths), else an Expr."""
+    try:
+        return build()
+    except TraceError:
+        return Expr.binary(op, a, b)
+
+
+def _bshape(name: str, shapes) -> Tuple[int, ...]:
+    """Elementwise broadcast: scalars and one common shape."""
+    vec = [tuple(s) for s in shapes if tuple(s) != ()]
+    for s in vec[1:]:
+        if s != vec[0]:
+            raise TraceError(f"{name}: cannot broadcast shapes {vec} (operands must be scalars "
+                             "or share one shape)")
+    return vec[0] if vec else ()
+
+
+class Expr:
+    """A traced elementwise expression (MC_DIST_EXPR nodes, include/mcmc355.h
+    mc_expr_node): op an MC_EX_* code, args its argument Exprs; a leaf holds
+    a parameter (view, untransformed), a data array or a constant."""
+
+    __array_priority__ = 1000
+
+    def __init__(self, op: int, args=(), leaf=None, shape: Tuple[int, ...] = ()):
+        self.op = op
+        self.args = tuple(args)
+        self.leaf = leaf
+        self.shape = tuple(shape)
+
+    # -- construction --------------------------------------------------------
+    @staticmethod
+    def of(x) -> "Expr":
+        if isinstance(x, Expr):
+            return x
+        if isinstance(x, LogProbExpr):
+            raise TraceError("a log density inside a parameter expression (only + / - / scalar * "
+                             "combine log densities): " + _UNSUPPORTED)
+        if isinstance(x, Param):
+            if x.xf:
+                raw = Param(x.name, x.offset, x.base_shape, x.view, 0)
+                op = _lib.MC_EX_EXP if x.xf == _lib.MC_XF_EXP else _lib.MC_EX_LOG
+                return Expr(op, [Expr.of(raw)], shape=raw.shape)
+            return Expr(_lib.MC_EX_LEAF, leaf=x, shape=x.shape)
+        if isinstance(x, Affine):
+            if x.x is None:
+                return Expr.of(x.loc if x.loc is not None else 0.0)
+            prod = Expr.binary(_lib.MC_EX_MUL, x.slope, x.x)
+            return prod if x.loc is None else Expr.binary(_lib.MC_EX_ADD, x.loc, prod)
+        arr = np.asarray(_to_numpy(x))
+        if arr.dtype == object:
+            raise TraceError("unsupported value in a parameter expression: " + _UNSUPPORTED)
+        arr = arr.astype(np.float32)
+        if arr.ndim == 0:
+            return Expr(_lib.MC_EX_LEAF, leaf=float(arr), shape=())
+        return Expr(_lib.MC_EX_LEAF, leaf=np.ascontiguousarray(arr), shape=arr.shape)
+
+    @staticmethod
+    def unary(op: int, a) -> "Expr":
+        ea = Expr.of(a)
+        return Expr(op, [ea], shape=ea.shape)
+
+    @staticmethod
+    def binary(op: int, a, b) -> "Expr":
+        ea, eb = Expr.of(a), Expr.of(b)
+        return Expr(op, [ea, eb], shape=_bshape("expression", [ea.shape, eb.shape]))
+
+    @staticmethod
+    def where(mask, a, b) -> "Expr":
+        m = np.asarray(_to_numpy(mask))
+        if m.dtype == object:
+            raise TraceError("mx.where over a traced condition (the mask must be data): "
+                             + _UNSUPPORTED)
+        em = Expr.of(m.astype(np.float32))
+        ea, eb = Expr.of(a), Expr.of(b)
+        e = Expr(_lib.MC_EX_WHERE, [em, ea, eb],
+                 shape=_bshape("mx.where", [em.shape, ea.shape, eb.shape]))
+        return e
+
+    # -- arithmetic ------------------------------------------------------------
+    def __add__(self, other):
+        if isinstance(other, LogProbExpr):
+            return other + self
+        return Expr.binary(_lib.MC_EX_ADD, self, other)
+
+    def __radd__(self, other):
+        if isinstance(other, LogProbExpr):
+            return other + self
+        return Expr.binary(_lib.MC_EX_ADD, other, self)
+
+    def __sub__(self, other):
+        if isinstance(other, LogProbExpr):
+            return (-other) + self
+        return Expr.binary(_lib.MC_EX_SUB, self, other)
+
+    def __rsub__(self, other):
+        return Expr.binary(_lib.MC_EX_SUB, other, self)
+
+    def __mul__(self, other):
+        return Expr.binary(_lib.MC_EX_MUL, self, other)
+
+    def __rmul__(self, other):
+        return Expr.binary(_lib.MC_EX_MUL, other, self)
+
+    def __truediv__(self, other):
+        return Expr.binary(_lib.MC_EX_DIV, self, other)
+
+    def __rtruediv__(self, other):
+        return Expr.binary(_lib.MC_EX_DIV, other, self)
+
+    def __pow__(self, other):
+        return Expr.binary(_lib.MC_EX_POW, self, other)
+
+    def __rpow__(self, other):
+        return Expr.binary(_lib.MC_EX_POW, other, self)
+
+    def __neg__(self):
+        return Expr.unary(_lib.MC_EX_NEG, self)
+
+    def __abs__(self):
+        return Expr.unary(_lib.MC_EX_ABS, self)
+
+    def _unsupported(self, *a, **k):
+        raise TraceError("this operation on a traced expression: " + _UNSUPPORTED)
+
+    __getitem__ = __lt__ = __le__ = __gt__ = __ge__ = _unsupported
+
+    def __float__(self):
+        raise TraceError("float() of a traced expression (a Python branch on a parameter value "
+                         "cannot be traced): " + _UNSUPPORTED)
+
+    __bool__ = __int__ = __float__
+
+    @property
+    def size(self) -> int:
+        return int(np.prod(self.shape)) if self.shape else 1
+
+    def __repr__(self):
+        if self.op == _lib.MC_EX_LEAF:
+            return f"Expr(leaf {self.leaf!r})"
+        return f"Expr(op {self.op}, {len(self.args)} args, shape={self.shape})"
+
+
+def expr_term(root: Expr) -> "LogProbExpr":
+    """An expression summed into a log density: weight * sum_i root_i."""
+    n = root.size
+    return LogProbExpr([Term(_lib.MC_DIST_EXPR, NONE_OPERAND, NONE_OPERAND, NONE_OPERAND, n,
+                             1.0, None, root)], 0.0, root.shape)
+
+
+_EXPR_DIST = {"Normal": _lib.MC_EX_NORMAL_LP, "HalfNormal": _lib.MC_EX_HALFNORMAL_LP,
+              "Exponential": _lib.MC_EX_EXPONENTIAL_LP}
+
+
+def dist_expr(dist_name: str, value, loc, scale) -> "LogProbExpr":
+    """Distribution.log_prob over expression arguments (MC_EX_*_LP node)."""
+    op = _EXPR_DIST.get(dist_name)
+    if op is None:
+        raise TraceError(f"{dist_name} with parameter-expression arguments (only Normal, "
+                         "HalfNormal and Exponential take them): " + _UNSUPPORTED)
+    ev, es = Expr.of(value), Expr.of(scale)
+    if op == _lib.MC_EX_NORMAL_LP:
+        el = Expr.of(loc)
+        root = Expr(op, [ev, el, es], shape=_bshape(dist_name, [ev.shape, el.shape, es.shape]))
+    else:
+        root = Expr(op, [ev, None, es], shape=_bshape(dist_name, [ev.shape, es.shape]))
+    return expr_term(root)
 
 
 @dataclass
@@ -347,9 +593,8 @@ def to_operand(x) -> Operand:
                        transform=xf)
     if isinstance(x, LogProbExpr):
         raise TraceError("a log density cannot be a distribution argument: " + _UNSUPPORTED)
-    if isinstance(x, Affine):
-        raise TraceError("a parameter expression (loc + slope * x) is accepted as a Normal "
-                         "loc only: " + _UNSUPPORTED)
+    if isinstance(x, (Affine, Expr)):
+        raise TraceError("a parameter expression is not a fused-term operand: " + _UNSUPPORTED)
     try:
         import torch
 
@@ -367,7 +612,7 @@ def to_operand(x) -> Operand:
 
 
 def is_symbolic(*xs) -> bool:
-    return any(isinstance(x, (Param, LogProbExpr, Affine)) for x in xs)
+    return any(isinstance(x, (Param, LogProbExpr, Affine, Expr)) for x in xs)
 
 
 @dataclass
@@ -379,6 +624,7 @@ class Term:
     n: int
     weight: float = 1.0
     aff: Optional[Tuple[Operand, Operand]] = None  # affine loc: (slope, x)
+    expr: Optional["Expr"] = None                   # MC_DIST_EXPR: the root node
 
 
 def broadcast_n(dist_name: str, ops: List[Operand]) -> Tuple[int, Tuple[int, ...]]:
@@ -414,7 +660,13 @@ class LogProbExpr:
             terms = list(self.terms) + [_scaled(t, sign) for t in other.terms]
             return LogProbExpr(terms, self.const + sign * other.const, self.shape)
         if isinstance(other, (Param, Affine)):
-            return self._combine(identity_expr(other), sign)
+            try:
+                ident = identity_expr(other)
+            except TraceError:
+                ident = expr_term(Expr.of(other))
+            return self._combine(ident, sign)
+        if isinstance(other, Expr):
+            return self._combine(expr_term(other), sign)
         c = _scalar_const(other)
         if self.shape != ():
             raise TraceError("adding a constant to an unsummed vector log density")
@@ -490,11 +742,11 @@ def identity_expr(x) -> LogProbExpr:
 
 
 def _scaled(t: Term, c: float) -> Term:
-    return Term(t.dist, t.value, t.loc, t.scale, t.n, t.weight * c, t.aff)
+    return Term(t.dist, t.value, t.loc, t.scale, t.n, t.weight * c, t.aff, t.expr)
 
 
 def _scalar_const(x) -> float:
-    if isinstance(x, (Param, LogProbExpr)):
+    if isinstance(x, (Param, LogProbExpr, Affine, Expr)):
         raise TraceError(_UNSUPPORTED)
     arr = np.asarray(x)
     if arr.dtype == object or arr.size != 1:
@@ -503,6 +755,20 @@ def _scalar_const(x) -> float:
 
 
 def make_term(dist: int, dist_name: str, value, loc, scale) -> LogProbExpr:
+    if any(isinstance(x, Expr) for x in (value, loc, scale)):
+        return dist_expr(dist_name, value, loc, scale)
+    try:
+        return _make_fused_term(dist, dist_name, value, loc, scale)
+    except TraceError:
+        # arguments the fused terms do not take (an affine value or scale, a
+        # transformed parameter times a parameter ...): an expression term
+        if dist_name not in _EXPR_DIST or not any(
+                isinstance(x, (Param, Affine)) for x in (value, loc, scale)):
+            raise
+        return dist_expr(dist_name, value, loc, scale)
+
+
+def _make_fused_term(dist: int, dist_name: str, value, loc, scale) -> LogProbExpr:
     aff = None
     if isinstance(loc, Param) and dist_name == "Normal":
         loc_op = to_operand(loc)
@@ -639,6 +905,10 @@ class TracedModel:
     c_terms: object = None
     c_affines: object = None
     n_affines: int = 0
+    c_exprs: object = None
+    c_nodes: object = None
+    n_exprs: int = 0
+    n_nodes: int = 0
 
 
 def trace(log_prob_fn, initial_params: dict) -> TracedModel:
@@ -646,8 +916,9 @@ def trace(log_prob_fn, initial_params: dict) -> TracedModel:
     sym = {name: Param(name, off, shp)
            for name, shp, off in zip(layout.names, layout.shapes, layout.offsets)}
     out = log_prob_fn(sym)
-    if isinstance(out, Param):
-        raise TraceError("log_prob returned a parameter, not a log density")
+    if isinstance(out, (Param, Affine, Expr)) and tuple(out.shape) == ():
+        # a scalar parameter expression returned as the log density itself
+        out = expr_term(Expr.of(out))
     if not isinstance(out, LogProbExpr):
         raise TraceError("log_prob did not build its value from Normal / HalfNormal terms: "
                          + _UNSUPPORTED)
@@ -669,11 +940,19 @@ def _build_pools(model: TracedModel) -> None:
     affs = [t for t in model.terms if t.aff is not None]
     aarr = (_lib.McAffine * max(1, len(affs)))()
     na = 0
+    exprs: List[Tuple[int, int]] = []
+    nodes: List[tuple] = []   # (op, a, b, c, Operand or None)
     for k, t in enumerate(model.terms):
         ct = arr[k]
         ct.dist = t.dist
         ct.n = t.n
         ct.weight = t.weight
+        if t.dist == _lib.MC_DIST_EXPR:
+            first = len(nodes)
+            nodes.extend(_linearize(t.expr, t.n))
+            exprs.append((first, len(nodes) - first))
+            ct.affine = len(exprs)
+            continue
         slots = [(ct, "value", t.value), (ct, "loc", t.loc), (ct, "scale", t.scale)]
         if t.aff is not None:
             ct.affine = na + 1
@@ -693,11 +972,85 @@ def _build_pools(model: TracedModel) -> None:
                 co.pool_offset = ni
                 index_parts.append(o.index.astype(np.int32))
                 ni += o.index.size
+    carr = (_lib.McExprNode * max(1, len(nodes)))()
+    index_ids: Dict[bytes, int] = {}   # one pool copy per gather index
+    for k, (op, a, b, c, o) in enumerate(nodes):
+        cn = carr[k]
+        cn.op, cn.a, cn.b, cn.c = op, a, b, c
+        if o is None:
+            continue
+        co = cn.leaf
+        co.kind = o.kind
+        co.param_offset = o.param_offset
+        co.value = o.value
+        co.transform = 0
+        if o.kind == _lib.MC_OP_DATA:
+            co.pool_offset = nd
+            data_parts.append(o.data.astype(np.float32))
+            nd += o.data.size
+        elif o.kind == _lib.MC_OP_GATHER:
+            ik = o.index.tobytes()
+            if ik not in index_ids:
+                index_ids[ik] = ni
+                index_parts.append(o.index.astype(np.int32))
+                ni += o.index.size
+            co.pool_offset = index_ids[ik]
+    xarr = (_lib.McExpr * max(1, len(exprs)))()
+    for k, (first, count) in enumerate(exprs):
+        xarr[k].first, xarr[k].count = first, count
+    model.c_exprs, model.c_nodes = xarr, carr
+    model.n_exprs, model.n_nodes = len(exprs), len(nodes)
     model.data = (np.concatenate(data_parts) if data_parts else np.zeros(0, np.float32))
     model.index = (np.concatenate(index_parts) if index_parts else np.zeros(0, np.int32))
     model.c_terms = arr
     model.c_affines = aarr
     model.n_affines = na
+
+
+def _linearize(root: Expr, n: int) -> List[tuple]:
+    """Post-order node list of an expression term (arguments before their
+    users, the root last); identical leaves share one node."""
+    out: List[tuple] = []
+    memo: Dict[int, int] = {}
+    leaves: Dict[tuple, int] = {}
+
+    def leaf_operand(e: Expr) -> Operand:
+        x = e.leaf
+        if isinstance(x, Param):
+            op = to_operand(x)
+            if op.kind == _lib.MC_OP_GATHER and op.shape == ():
+                op.shape = (1,)
+            return op
+        if isinstance(x, np.ndarray):
+            if x.size == 1 and n > 1 and x.shape == ():
+                return Operand(_lib.MC_OP_CONST, value=float(x))
+            return Operand(_lib.MC_OP_DATA, data=x.ravel(), shape=x.shape)
+        return Operand(_lib.MC_OP_CONST, value=float(x))
+
+    def visit(e: Expr) -> int:
+        if id(e) in memo:
+            return memo[id(e)]
+        if e.op == _lib.MC_EX_LEAF:
+            o = leaf_operand(e)
+            key = (("g", o.param_offset, o.index.tobytes()) if o.kind == _lib.MC_OP_GATHER
+                   else o.key())
+            if key in leaves:
+                memo[id(e)] = leaves[key]
+                return leaves[key]
+            out.append((e.op, -1, -1, -1, o))
+            leaves[key] = memo[id(e)] = len(out) - 1
+            return len(out) - 1
+        ids = [visit(a) if a is not None else -1 for a in e.args]
+        ids += [-1] * (3 - len(ids))
+        out.append((e.op, ids[0], ids[1], ids[2], None))
+        memo[id(e)] = len(out) - 1
+        return len(out) - 1
+
+    visit(root)
+    if len(out) > _lib.MC_EXPR_MAX_NODES:
+        raise TraceError(f"an expression term of {len(out)} nodes (at most "
+                         f"{_lib.MC_EXPR_MAX_NODES}): split the log density into several sums")
+    return out
 
 
 class Program:
@@ -711,8 +1064,9 @@ class Program:
         h = ctypes.c_void_p()
         data = np.ascontiguousarray(model.data, np.float32)
         index = np.ascontiguousarray(model.index, np.int32)
-        _lib.check(lib.mc_program_create_affine(
-            model.c_terms, len(model.terms), model.c_affines, model.n_affines, self.D,
+        _lib.check(lib.mc_program_create_expr(
+            model.c_terms, len(model.terms), model.c_affines, model.n_affines, model.c_exprs,
+            model.n_exprs, model.c_nodes, model.n_nodes, self.D,
             model.lp_const, data.ctypes.data_as(ctypes.c_void_p), data.size,
             index.ctypes.data_as(ctypes.c_void_p), index.size, ctypes.byref(h)))
         self.handle = h

@@ -1,11 +1,15 @@
 """``mx``-compatible array namespace for user models: ``import mlx_mcmc_amd.core as mx``.
 
-Models written for the reference (``import mlx.core as mx``) use a handful of
-``mx`` calls inside ``log_prob`` — ``mx.sum``, ``mx.array`` — and a few more on
-the returned samples (``mx.mean``, ``mx.std``, ``mx.all``, ``mx.allclose``) and
-``mx.random.key``.  Inside a traced ``log_prob`` these build the term program
-(_trace.py); on concrete arrays they are ordinary NumPy float32 operations on
-the host (post-processing only: sampling itself runs in the HIP kernels).
+Models written for the reference (``import mlx.core as mx``) use ``mx`` calls
+inside ``log_prob`` — ``mx.sum``, ``mx.array``, elementwise math (``mx.exp``,
+``mx.log``, ``mx.sqrt``, ``mx.square``, ``mx.power``, ``mx.abs``,
+``mx.log1p``, ``mx.tanh``, ``mx.sigmoid``, ``mx.where`` over a data mask) —
+and a few more on the returned samples (``mx.mean``, ``mx.std``, ``mx.all``,
+``mx.allclose``) and ``mx.random.key``.  Inside a traced ``log_prob`` these
+build the term program (_trace.py: fused terms, or expression terms for
+general elementwise arithmetic); on concrete arrays they are ordinary NumPy
+float32 operations on the host (post-processing only: sampling itself runs in
+the HIP kernels).
 """
 from __future__ import annotations
 
@@ -43,8 +47,14 @@ def sum(x, axis=None, keepdims=False):  # noqa: A001 - mirrors mx.sum
         return x.sum(axis)
     if isinstance(x, (_trace.Param, _trace.Affine)):
         # a parameter expression summed into a log density (`mx.sum(log_x)`,
-        # the Jacobian of a vector reparameterisation): identity terms
-        return _trace.identity_expr(x).sum(axis)
+        # the Jacobian of a vector reparameterisation): identity terms, or an
+        # expression term when the sum is of a more general expression
+        try:
+            return _trace.identity_expr(x).sum(axis)
+        except _trace.TraceError:
+            return _trace.expr_term(_trace.Expr.of(x)).sum(axis)
+    if isinstance(x, _trace.Expr):
+        return _trace.expr_term(x).sum(axis)
     return np.sum(np.asarray(x), axis=axis, keepdims=keepdims)
 
 
@@ -58,25 +68,70 @@ def _concrete(name, fn):
     return f
 
 
-def _transform(name, xf, fn):
+def _transform(name, xf, op, fn):
     """mx.exp / mx.log: of a traced parameter (or view) a transformed parameter
-    operand (mc_transform_kind); of concrete arrays the NumPy f32 value."""
+    operand (mc_transform_kind, the fused fast paths); of any other traced
+    expression an expression node; of concrete arrays the NumPy f32 value."""
     def f(x, *a, **k):
-        if isinstance(x, _trace.Param) and not a and not k:
+        if isinstance(x, _trace.Param) and not x.xf and not a and not k:
             return x.transformed(xf, name)
         if _trace.is_symbolic(x, *a):
-            raise _trace.TraceError(f"mx.{name} of a traced expression (only of a parameter or "
-                                    "a view of one): " + _trace._UNSUPPORTED)
+            return _trace.Expr.unary(op, x)
         return fn(np.asarray(_trace._to_numpy(x)), *a, **k)
 
     f.__name__ = name
     return f
 
 
-log = _transform("log", 2, np.log)
-exp = _transform("exp", 1, np.exp)
-sqrt = _concrete("sqrt", np.sqrt)
-abs = _concrete("abs", np.abs)  # noqa: A001
+def _elementwise(name, op, fn):
+    """An elementwise mx function: an expression node of a traced value, the
+    NumPy f32 value of a concrete one."""
+    def f(x):
+        if _trace.is_symbolic(x):
+            return _trace.Expr.unary(op, x)
+        return fn(np.asarray(_trace._to_numpy(x), np.float32))
+
+    f.__name__ = name
+    return f
+
+
+def _sigmoid(x):
+    return (np.float32(1) / (np.float32(1) + np.exp(-x))).astype(np.float32)
+
+
+log = _transform("log", 2, _trace._lib.MC_EX_LOG, np.log)
+exp = _transform("exp", 1, _trace._lib.MC_EX_EXP, np.exp)
+sqrt = _elementwise("sqrt", _trace._lib.MC_EX_SQRT, np.sqrt)
+square = _elementwise("square", _trace._lib.MC_EX_SQUARE, np.square)
+abs = _elementwise("abs", _trace._lib.MC_EX_ABS, np.abs)  # noqa: A001
+log1p = _elementwise("log1p", _trace._lib.MC_EX_LOG1P, np.log1p)
+tanh = _elementwise("tanh", _trace._lib.MC_EX_TANH, np.tanh)
+sigmoid = _elementwise("sigmoid", _trace._lib.MC_EX_SIGMOID, _sigmoid)
+negative = _elementwise("negative", _trace._lib.MC_EX_NEG, np.negative)
+
+
+def power(a, b):
+    if _trace.is_symbolic(a, b):
+        return _trace.Expr.binary(_trace._lib.MC_EX_POW, a, b)
+    return np.power(np.asarray(_trace._to_numpy(a), np.float32),
+                    np.asarray(_trace._to_numpy(b), np.float32))
+
+
+def _binary(name, op, fn):
+    def f(a, b):
+        if _trace.is_symbolic(a, b):
+            return _trace.Expr.binary(op, a, b)
+        return fn(np.asarray(_trace._to_numpy(a), np.float32),
+                  np.asarray(_trace._to_numpy(b), np.float32))
+
+    f.__name__ = name
+    return f
+
+
+add = _binary("add", _trace._lib.MC_EX_ADD, np.add)
+subtract = _binary("subtract", _trace._lib.MC_EX_SUB, np.subtract)
+multiply = _binary("multiply", _trace._lib.MC_EX_MUL, np.multiply)
+divide = _binary("divide", _trace._lib.MC_EX_DIV, np.divide)
 mean = _concrete("mean", np.mean)
 std = _concrete("std", np.std)
 var = _concrete("var", np.var)
@@ -88,8 +143,11 @@ isinf = _concrete("isinf", np.isinf)
 
 
 def where(cond, a, b):
-    if _trace.is_symbolic(cond, a, b):
-        raise _trace.TraceError("mx.where of traced values: " + _trace._UNSUPPORTED)
+    if _trace.is_symbolic(cond):
+        raise _trace.TraceError("mx.where over a traced condition (a Python-free branch on a "
+                                "parameter value; the mask must be data): " + _trace._UNSUPPORTED)
+    if _trace.is_symbolic(a, b):
+        return _trace.Expr.where(cond, a, b)
     return np.where(cond, a, b)
 
 

@@ -111,6 +111,8 @@ struct mc_program {
     int64_t max_n = 0;
     std::vector<DevTerm> terms;
     DevTerm* d_terms = nullptr;
+    std::vector<DevExprNode> nodes;  // expression-term nodes (DevTerm::expr_base)
+    DevExprNode* d_nodes = nullptr;
     float* d_data = nullptr;
     int32_t* d_index = nullptr;
     // terms as validated (before the chain-per-workgroup tiling) and the host
@@ -129,6 +131,7 @@ struct mc_program {
 static DevCtx ctx_of(const mc_program* p) {
     DevCtx c;
     c.terms = p->d_terms;
+    c.nodes = p->d_nodes;
     c.n_terms = (int32_t)p->terms.size();
     c.D = p->D;
     c.lp_const = p->lp_const;
@@ -168,11 +171,15 @@ static int choose_wpc(int64_t max_n) {
 // chain group of T threads has ~2T lanes of work even for few, long groups;
 // with >= 2T segments nothing is split and each lane writes its group's
 // gradient directly.
-static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<int32_t>& ipool,
-                          int T) {
-    const int a = dt.primary;
+// prim_pool: index-pool offset of the sorted primary index; others: the
+// term's other vector operands, tiled beside it (DATA copied, PVEC turned
+// into identity gathers, GATHER indices copied); allow_split: long runs may be
+// split into virtual segments (expression terms keep whole runs).
+static int build_segments_ops(DevTerm& dt, int64_t prim_pool, const std::vector<DevOperand*>& others,
+                              bool allow_split, std::vector<float>& dpool,
+                              std::vector<int32_t>& ipool, int T) {
     const int64_t n = dt.n;
-    const int64_t ip = dt.op[a].pool;
+    const int64_t ip = prim_pool;
     std::vector<int64_t> sstart;
     std::vector<int32_t> sk;
     for (int64_t i = 0; i < n; ++i)
@@ -184,8 +191,8 @@ static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<in
     sstart.push_back(n);
     // split only when there are fewer groups than lanes (then ~T virtual
     // segments, one tile per wave); otherwise each lane owns whole groups
-    const int64_t Lt = (G >= (int64_t)T) ? INT64_MAX
-                                         : std::max<int64_t>(1, (n + T - 1) / T);
+    const int64_t Lt = (G >= (int64_t)T || !allow_split) ? INT64_MAX
+                                                         : std::max<int64_t>(1, (n + T - 1) / T);
     struct V {
         int32_t k;
         int64_t start;
@@ -235,9 +242,9 @@ static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<in
         lanes[2 * v + 1] = vs[v].len;
     }
     // parameter slices become identity gathers so that they can be tiled too
-    for (int b = 0; b < 3; ++b) {
-        DevOperand& d = dt.op[b];
-        if (b == a || d.kind != MC_OP_PVEC) continue;
+    for (DevOperand* dp : others) {
+        DevOperand& d = *dp;
+        if (d.kind != MC_OP_PVEC) continue;
         const int64_t base = (int64_t)ipool.size();
         for (int64_t i = 0; i < n; ++i) ipool.push_back((int32_t)i);
         d.kind = MC_OP_GATHER;
@@ -245,10 +252,9 @@ static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<in
         d.unique = 1;
     }
     // tiled copies of every other vector operand (and an affine loc's data x)
-    for (int b = 0; b < 4; ++b) {
-        if (b == 3 && !dt.affine) break;
-        DevOperand& d = b < 3 ? dt.op[b] : dt.ax;
-        if (b == a || (d.kind != MC_OP_DATA && d.kind != MC_OP_GATHER)) continue;
+    for (DevOperand* dp : others) {
+        DevOperand& d = *dp;
+        if (d.kind != MC_OP_DATA && d.kind != MC_OP_GATHER) continue;
         if (d.kind == MC_OP_DATA) {
             while (dpool.size() % 64) dpool.push_back(0.0f);
             const int64_t base = (int64_t)dpool.size();
@@ -286,6 +292,16 @@ static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<in
     if (nv > 4 * (int64_t)T && split)
         return fail(MC_ERR_UNSUPPORTED, "internal: too many virtual segments");
     return MC_OK;
+}
+
+static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<int32_t>& ipool,
+                          int T) {
+    const int a = dt.primary;
+    std::vector<DevOperand*> others;
+    for (int b = 0; b < 3; ++b)
+        if (b != a) others.push_back(&dt.op[b]);
+    if (dt.affine) others.push_back(&dt.ax);
+    return build_segments_ops(dt, dt.op[a].pool, others, true, dpool, ipool, T);
 }
 
 // ---------------------------------------------------------------------------
@@ -355,6 +371,11 @@ static bool has_affine(const mc_program* p) {
         if (t.affine) return true;
     return false;
 }
+static bool has_expr(const mc_program* p) {
+    for (const DevTerm& t : p->raw)
+        if (t.dist == MC_DIST_EXPR) return true;
+    return false;
+}
 // Transformed parameter operands and identity terms (the reparameterised
 // models of mc_transform_kind).
 static bool has_transform(const mc_program* p) {
@@ -383,6 +404,9 @@ static bool transform_on_shared_only(const mc_program* p) {
 
 static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = nullptr) {
     const std::vector<DevTerm>& raw = p->raw;
+    if (has_expr(p))
+        return fail(MC_ERR_UNSUPPORTED, "expression terms run on the chain-per-workgroup "
+                    "kernels (not sliceable)");
     if (has_affine(p))
         return fail(MC_ERR_UNSUPPORTED, "affine loc operands run on the chain-per-workgroup "
                     "kernels (not sliceable)");
@@ -1174,7 +1198,8 @@ static int64_t program_elements(const mc_program* p) {
 // stay unsliced (a per-step exchange costs more than the whole evaluation).
 static constexpr int64_t kLrAutoMinElements = 2048;
 static int auto_slices(const mc_program* p) {
-    if (has_affine(p) || (has_transform(p) && !transform_on_shared_only(p))) return 1;
+    if (has_expr(p) || has_affine(p) || (has_transform(p) && !transform_on_shared_only(p)))
+        return 1;
     const int64_t n = program_elements(p);
     if (n >= 65536) return 16;
     if (n >= 16384) return 8;
@@ -1349,9 +1374,244 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
                                         int32_t n_params, float lp_const, const float* data,
                                         int64_t n_data, const int32_t* index, int64_t n_index,
                                         mc_program** out) {
+    if (n_terms < 0 || (n_terms > 0 && !terms)) return fail(MC_ERR_INVALID, "bad term array");
+    for (int32_t t = 0; t < n_terms; ++t)
+        if (terms[t].dist == MC_DIST_EXPR)
+            return fail(MC_ERR_INVALID, "term %d: expression terms need mc_program_create_expr", t);
+    return mc_program_create_expr(terms, n_terms, affines, n_affines, nullptr, 0, nullptr, 0,
+                                  n_params, lp_const, data, n_data, index, n_index, out);
+}
+
+// Validate and lay out one expression term (MC_DIST_EXPR): its nodes are
+// appended to `gnodes` (dt.expr_base ..), a non-injective gather orders the
+// term into the segment-tiled layout (build_segments_ops, whole runs), and
+// vector leaves with overlapping parameter ranges deposit in different passes.
+static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, int32_t n_exprs,
+                           const mc_expr_node* nodes, int32_t n_nodes, int32_t n_params,
+                           std::vector<float>& dpool, std::vector<int32_t>& ipool,
+                           std::vector<DevExprNode>& gnodes, DevTerm& dt, int wpc) {
+    if (src.affine < 1 || src.affine > n_exprs)
+        return fail(MC_ERR_INVALID, "term %d: expression index %d out of range", t, src.affine);
+    if (src.value.kind != MC_OP_NONE || src.loc.kind != MC_OP_NONE || src.scale.kind != MC_OP_NONE)
+        return fail(MC_ERR_INVALID, "term %d: an expression term takes no value / loc / scale", t);
+    const mc_expr& ex = exprs[src.affine - 1];
+    if (ex.count < 1 || ex.count > kExMaxNodes)
+        return fail(MC_ERR_UNSUPPORTED, "term %d: an expression holds 1 .. %d nodes (got %d)", t,
+                    kExMaxNodes, ex.count);
+    if (ex.first < 0 || (int64_t)ex.first + ex.count > n_nodes)
+        return fail(MC_ERR_INVALID, "term %d: expression nodes out of range", t);
+    const int64_t n = src.n;
+    const int nn = ex.count;
+    std::vector<DevExprNode> en(nn);
+    std::vector<int> nonunique;  // non-injective gather leaves
+    for (int k = 0; k < nn; ++k) {
+        const mc_expr_node& s = nodes[ex.first + k];
+        DevExprNode& d = en[k];
+        std::memset(&d, 0, sizeof(d));
+        d.op = s.op;
+        d.a = s.a;
+        d.b = s.b;
+        d.c = s.c;
+        d.leaf.kind = MC_OP_NONE;
+        d.leaf.slot = -1;
+        if (s.op < MC_EX_LEAF || s.op > MC_EX_WHERE)
+            return fail(MC_ERR_INVALID, "term %d node %d: unknown op %d", t, k, s.op);
+        if (s.op == MC_EX_LEAF) {
+            const mc_operand& o = s.leaf;
+            d.leaf.kind = o.kind;
+            d.leaf.poff = o.param_offset;
+            d.leaf.pool = o.pool_offset;
+            d.leaf.cval = o.value;
+            d.leaf.unique = 1;
+            d.leaf.xf = MC_XF_NONE;
+            if (o.transform != MC_XF_NONE)
+                return fail(MC_ERR_INVALID, "term %d node %d: expression leaves take no transform "
+                            "(exp / log are nodes)", t, k);
+            switch (o.kind) {
+                case MC_OP_CONST:
+                    break;
+                case MC_OP_PSCALAR:
+                    if (o.param_offset < 0 || o.param_offset >= n_params)
+                        return fail(MC_ERR_INVALID, "term %d node %d: param %d out of range", t, k,
+                                    o.param_offset);
+                    break;
+                case MC_OP_DATA:
+                    if (o.pool_offset < 0 || o.pool_offset + n > (int64_t)dpool.size())
+                        return fail(MC_ERR_INVALID, "term %d node %d: data range out of pool", t, k);
+                    break;
+                case MC_OP_PVEC:
+                    if (o.param_offset < 0 || (int64_t)o.param_offset + n > n_params)
+                        return fail(MC_ERR_INVALID, "term %d node %d: param slice out of range", t,
+                                    k);
+                    break;
+                case MC_OP_GATHER: {
+                    if (o.pool_offset < 0 || o.pool_offset + n > (int64_t)ipool.size())
+                        return fail(MC_ERR_INVALID, "term %d node %d: index range out of pool", t,
+                                    k);
+                    std::vector<int32_t> v(ipool.begin() + o.pool_offset,
+                                           ipool.begin() + o.pool_offset + n);
+                    for (int32_t x : v)
+                        if (x < 0 || (int64_t)o.param_offset + x >= n_params)
+                            return fail(MC_ERR_INVALID,
+                                        "term %d node %d: gather index %d out of range", t, k, x);
+                    std::sort(v.begin(), v.end());
+                    d.leaf.unique = (std::adjacent_find(v.begin(), v.end()) == v.end()) ? 1 : 0;
+                    if (!d.leaf.unique) nonunique.push_back(k);
+                    break;
+                }
+                default:
+                    return fail(MC_ERR_INVALID, "term %d node %d: bad leaf kind %d", t, k, o.kind);
+            }
+            d.a = d.b = d.c = -1;
+            continue;
+        }
+        // arity: which arguments the op reads
+        bool ua = true, ub = false, uc = false;
+        switch (s.op) {
+            case MC_EX_ADD: case MC_EX_SUB: case MC_EX_MUL: case MC_EX_DIV: case MC_EX_POW:
+                ub = true;
+                break;
+            case MC_EX_NORMAL_LP: case MC_EX_WHERE:
+                ub = uc = true;
+                break;
+            case MC_EX_HALFNORMAL_LP: case MC_EX_EXPONENTIAL_LP:
+                uc = true;
+                break;
+            default:
+                break;
+        }
+        auto arg_ok = [&](int x, bool used) { return used ? (x >= 0 && x < k) : x == -1; };
+        if (!arg_ok(s.a, ua) || !arg_ok(s.b, ub) || !arg_ok(s.c, uc))
+            return fail(MC_ERR_INVALID, "term %d node %d: bad arguments (%d, %d, %d) for op %d", t,
+                        k, s.a, s.b, s.c, s.op);
+        if (s.op == MC_EX_WHERE && !(en[s.a].op == MC_EX_LEAF &&
+                                     (en[s.a].leaf.kind == MC_OP_CONST ||
+                                      en[s.a].leaf.kind == MC_OP_DATA)))
+            return fail(MC_ERR_UNSUPPORTED, "term %d node %d: a where mask must be data or a "
+                        "constant", t, k);
+        // the distribution nodes' f32 normalisers (elem_normal / elem_halfnormal)
+        if (s.op == MC_EX_NORMAL_LP) d.leaf.cval = dist_c0(MC_DIST_NORMAL);
+        if (s.op == MC_EX_HALFNORMAL_LP) d.leaf.cval = dist_c0(MC_DIST_HALFNORMAL);
+    }
+    dt.dist = MC_DIST_EXPR;
+    dt.n = n;
+    dt.weight = src.weight;
+    dt.affine = 0;
+    dt.wave_task = -1;
+    dt.primary = -1;
+    // a non-injective gather: every such leaf through the same index values
+    int64_t prim_pool = -1;
+    if (!nonunique.empty()) {
+        const int64_t p0 = en[nonunique[0]].leaf.pool;
+        for (int k : nonunique) {
+            const int64_t pk = en[k].leaf.pool;
+            if (pk != p0 && !std::equal(ipool.begin() + pk, ipool.begin() + pk + n,
+                                        ipool.begin() + p0))
+                return fail(MC_ERR_UNSUPPORTED, "term %d: an expression gathers through two "
+                            "different non-injective index arrays", t);
+            en[k].prim = 1;
+        }
+        prim_pool = p0;
+        dt.primary = 0;  // (a flag for expression terms: segmented)
+    }
+    // passes: accumulating vector leaves with overlapping parameter ranges
+    // deposit in different sweeps (ranges before any tiling)
+    {
+        std::vector<std::vector<std::pair<int64_t, int64_t>>> pr;  // per pass
+        for (int k = 0; k < nn; ++k) {
+            DevExprNode& d = en[k];
+            if (d.op != MC_EX_LEAF || !is_acc_vec(d.leaf.kind)) continue;
+            int64_t lo, hi;
+            if (d.leaf.kind == MC_OP_PVEC) {
+                lo = d.leaf.poff;
+                hi = d.leaf.poff + n - 1;
+            } else {
+                const int32_t* ix = ipool.data() + d.leaf.pool;
+                lo = d.leaf.poff + *std::min_element(ix, ix + n);
+                hi = d.leaf.poff + *std::max_element(ix, ix + n);
+            }
+            int placed = -1;
+            for (size_t ps = 0; ps < pr.size() && placed < 0; ++ps) {
+                bool clash = false;
+                for (auto& r : pr[ps])
+                    if (!(hi < r.first || r.second < lo)) clash = true;
+                if (!clash) placed = (int)ps;
+            }
+            if (placed < 0) {
+                placed = (int)pr.size();
+                pr.emplace_back();
+            }
+            pr[placed].push_back({lo, hi});
+            d.pass = placed;
+        }
+        dt.npass = std::max<int>(1, (int)pr.size());
+    }
+    if (prim_pool >= 0) {
+        // order the term by the index (stable), then tile it by runs
+        bool sorted = true;
+        for (int64_t i = 1; i < n && sorted; ++i) sorted = ipool[prim_pool + i - 1] <= ipool[prim_pool + i];
+        if (!sorted) {
+            std::vector<int64_t> perm(n);
+            std::iota(perm.begin(), perm.end(), 0);
+            std::stable_sort(perm.begin(), perm.end(), [&](int64_t x, int64_t y) {
+                return ipool[prim_pool + x] < ipool[prim_pool + y];
+            });
+            std::map<std::pair<int, int64_t>, int64_t> moved;  // (kind, old pool) -> new pool
+            for (int k = 0; k < nn; ++k) {
+                DevOperand& d = en[k].leaf;
+                if (en[k].op != MC_EX_LEAF) continue;
+                if (d.kind == MC_OP_DATA || d.kind == MC_OP_GATHER) {
+                    const auto key = std::make_pair((int)d.kind, d.pool);
+                    auto it = moved.find(key);
+                    if (it != moved.end()) {
+                        d.pool = it->second;
+                        continue;
+                    }
+                    int64_t base;
+                    if (d.kind == MC_OP_DATA) {
+                        base = (int64_t)dpool.size();
+                        for (int64_t i = 0; i < n; ++i) dpool.push_back(dpool[d.pool + perm[i]]);
+                    } else {
+                        base = (int64_t)ipool.size();
+                        for (int64_t i = 0; i < n; ++i) ipool.push_back(ipool[d.pool + perm[i]]);
+                    }
+                    moved[key] = base;
+                    d.pool = base;
+                } else if (d.kind == MC_OP_PVEC) {
+                    const int64_t base = (int64_t)ipool.size();
+                    for (int64_t i = 0; i < n; ++i) ipool.push_back((int32_t)perm[i]);
+                    d.kind = MC_OP_GATHER;
+                    d.pool = base;
+                    d.unique = 1;
+                }
+            }
+            prim_pool = en[nonunique[0]].leaf.pool;
+        }
+        std::vector<DevOperand*> others;
+        for (int k = 0; k < nn; ++k)
+            if (en[k].op == MC_EX_LEAF && !en[k].prim && is_vec_kind(en[k].leaf.kind))
+                others.push_back(&en[k].leaf);
+        const int rc = build_segments_ops(dt, prim_pool, others, false, dpool, ipool, 64 * wpc);
+        if (rc) return rc;
+    }
+    dt.expr_base = (int32_t)gnodes.size();
+    dt.expr_n = nn;
+    gnodes.insert(gnodes.end(), en.begin(), en.end());
+    return MC_OK;
+}
+
+extern "C" int mc_program_create_expr(const mc_term* terms, int32_t n_terms,
+                                      const mc_affine* affines, int32_t n_affines,
+                                      const mc_expr* exprs, int32_t n_exprs,
+                                      const mc_expr_node* nodes, int32_t n_nodes,
+                                      int32_t n_params, float lp_const, const float* data,
+                                      int64_t n_data, const int32_t* index, int64_t n_index,
+                                      mc_program** out) {
     if (!out) return fail(MC_ERR_INVALID, "out is NULL");
     if (n_affines < 0 || (n_affines > 0 && !affines))
         return fail(MC_ERR_INVALID, "bad affine array");
+    if (n_exprs < 0 || (n_exprs > 0 && !exprs)) return fail(MC_ERR_INVALID, "bad expression array");
+    if (n_nodes < 0 || (n_nodes > 0 && !nodes)) return fail(MC_ERR_INVALID, "bad node array");
     *out = nullptr;
     if (n_params <= 0) return fail(MC_ERR_INVALID, "n_params must be positive (got %d)", n_params);
     if (n_terms < 0 || (n_terms > 0 && !terms)) return fail(MC_ERR_INVALID, "bad term array");
@@ -1361,18 +1621,27 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
     std::vector<float> dpool(data, data + n_data);
     std::vector<int32_t> ipool(index, index + n_index);
     std::vector<DevTerm> dts, raws;
+    std::vector<DevExprNode> gnodes;
     int64_t max_n = 0;
     for (int32_t t = 0; t < n_terms; ++t) max_n = std::max<int64_t>(max_n, terms[t].n);
     const int wpc = choose_wpc(max_n);
 
     for (int32_t t = 0; t < n_terms; ++t) {
         const mc_term& src = terms[t];
-        if (src.dist < MC_DIST_NORMAL || src.dist > MC_DIST_IDENTITY)
+        if (src.dist < MC_DIST_NORMAL || src.dist > MC_DIST_EXPR)
             return fail(MC_ERR_INVALID, "term %d: unknown distribution %d", t, src.dist);
         if (src.n < 1) return fail(MC_ERR_INVALID, "term %d: n must be >= 1", t);
         const int64_t n = src.n;
         DevTerm dt;
         std::memset(&dt, 0, sizeof(dt));
+        if (src.dist == MC_DIST_EXPR) {
+            const int rc = build_expr_term(t, src, exprs, n_exprs, nodes, n_nodes, n_params, dpool,
+                                           ipool, gnodes, dt, wpc);
+            if (rc) return rc;
+            raws.push_back(dt);
+            dts.push_back(dt);
+            continue;
+        }
         dt.dist = src.dist;
         dt.n = n;
         dt.weight = src.weight;
@@ -1620,6 +1889,14 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
             uses.push_back({dt.ab.poff, nslot});
             ++nslot;
         }
+        if (dt.dist == MC_DIST_EXPR)
+            for (int k = 0; k < dt.expr_n; ++k) {
+                DevExprNode& d = gnodes[dt.expr_base + k];
+                if (d.op != MC_EX_LEAF || d.leaf.kind != MC_OP_PSCALAR) continue;
+                d.leaf.slot = nslot;
+                uses.push_back({d.leaf.poff, nslot});
+                ++nslot;
+            }
     }
     std::stable_sort(uses.begin(), uses.end(),
                      [](const std::pair<int32_t, int32_t>& x,
@@ -1648,6 +1925,11 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
                 if (dt.op[a].kind == MC_OP_PVEC || dt.op[a].kind == MC_OP_GATHER) vec_param = true;
             if (dt.affine && (dt.ax.kind == MC_OP_PVEC || dt.ax.kind == MC_OP_GATHER))
                 vec_param = true;
+            if (dt.dist == MC_DIST_EXPR)
+                for (int k = 0; k < dt.expr_n; ++k)
+                    if (gnodes[dt.expr_base + k].op == MC_EX_LEAF &&
+                        is_acc_vec(gnodes[dt.expr_base + k].leaf.kind))
+                        vec_param = true;
             if (dt.primary < 0 && dt.npass == 1 && dt.n <= 64 && !vec_param)
                 dt.wave_task = (next++) % wpc;
         }
@@ -1662,6 +1944,15 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
         std::vector<std::pair<int64_t, int64_t>> open_ranges;
         for (DevTerm& dt : dts) {
             std::vector<std::pair<int64_t, int64_t>> mine;
+            if (dt.dist == MC_DIST_EXPR)
+                for (int k = 0; k < dt.expr_n; ++k) {
+                    const DevExprNode& d = gnodes[dt.expr_base + k];
+                    if (d.op != MC_EX_LEAF) continue;
+                    if (d.leaf.kind == MC_OP_PVEC)
+                        mine.push_back({d.leaf.poff, d.leaf.poff + dt.n - 1});
+                    else if (d.leaf.kind == MC_OP_GATHER)
+                        mine.push_back({0, (int64_t)n_params - 1});
+                }
             for (int a = 0; a < 4; ++a) {
                 if (a == 3 && !dt.affine) break;
                 const DevOperand& d = a < 3 ? dt.op[a] : dt.ax;
@@ -1691,6 +1982,7 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
     p->wpc = wpc;
     p->terms = dts;
     p->raw = raws;
+    p->nodes = gnodes;
     p->h_data = dpool;
     p->h_index = ipool;
     hipError_t e = hipSuccess;
@@ -1698,6 +1990,12 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
         e = hipMalloc(&p->d_terms, dts.size() * sizeof(DevTerm));
         if (e == hipSuccess)
             e = hipMemcpy(p->d_terms, dts.data(), dts.size() * sizeof(DevTerm),
+                          hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess && !gnodes.empty()) {
+        e = hipMalloc(&p->d_nodes, gnodes.size() * sizeof(DevExprNode));
+        if (e == hipSuccess)
+            e = hipMemcpy(p->d_nodes, gnodes.data(), gnodes.size() * sizeof(DevExprNode),
                           hipMemcpyHostToDevice);
     }
     if (e == hipSuccess && !dpool.empty()) {
@@ -1733,6 +2031,7 @@ extern "C" int mc_program_destroy(mc_program* p) {
     free_slices(p->sl);
     free_lanes(p->lr);
     if (p->d_terms) (void)hipFree(p->d_terms);
+    if (p->d_nodes) (void)hipFree(p->d_nodes);
     if (p->d_data) (void)hipFree(p->d_data);
     if (p->d_index) (void)hipFree(p->d_index);
     delete p;

@@ -144,6 +144,8 @@ MC_DEV DevTerm load_term(const MC_CONST DevTerm* p) {
         t.ab = load_op(&p->ab);
         t.ax = load_op(&p->ax);
     }
+    t.expr_base = p->expr_base;
+    t.expr_n = p->expr_n;
     return t;
 }
 
@@ -765,6 +767,199 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
 }
 
 // ---------------------------------------------------------------------------
+// expression terms (MC_DIST_EXPR, include/mcmc355.h mc_expr_node): the
+// elementwise MLX expressions mx.grad differentiates in the reference
+// (hmc.py:53-67), one f32 rounding per op, reverse mode per element.
+// ---------------------------------------------------------------------------
+constexpr int kExMaxNodes = MC_EXPR_MAX_NODES;
+
+// Forward value of a non-leaf node (x, y, z: its argument values; c0: the
+// distribution nodes' f32 normaliser, as elem_normal / elem_halfnormal).
+MC_DEV float ex_fwd(int op, float x, float y, float z, float c0) {
+    switch (op) {
+        case MC_EX_ADD: return x + y;
+        case MC_EX_SUB: return x - y;
+        case MC_EX_MUL: return x * y;
+        case MC_EX_DIV: return x / y;
+        case MC_EX_NEG: return -x;
+        case MC_EX_EXP: return expf(x);
+        case MC_EX_LOG: return logf(x);
+        case MC_EX_SQRT: return sqrtf(x);
+        case MC_EX_SQUARE: return x * x;
+        case MC_EX_POW: return powf(x, y);
+        case MC_EX_ABS: return fabsf(x);
+        case MC_EX_LOG1P: return log1pf(x);
+        case MC_EX_TANH: return tanhf(x);
+        case MC_EX_SIGMOID: return 1.0f / (1.0f + expf(-x));
+        case MC_EX_NORMAL_LP: return elem_normal(c0, x, y, z, logf(z)).lp;
+        case MC_EX_HALFNORMAL_LP: return elem_halfnormal(c0, x, z, logf(z)).lp;
+        case MC_EX_EXPONENTIAL_LP: return elem_exponential(x, z, logf(z)).lp;
+        case MC_EX_WHERE: return x != 0.0f ? y : z;
+        default: return 0.0f;
+    }
+}
+
+// Reverse step of a non-leaf node with value v and cotangent c: the
+// cotangents of its arguments (mx.grad's VJPs: exp c*v, log c/x, sqrt
+// c/(2v), pow c*y*x^(y-1) and c*v*log x, tanh c*(1-v^2), sigmoid
+// c*v*(1-v); where: nothing to the mask, c to the branch taken).
+MC_DEV void ex_bwd(int op, float x, float y, float z, float v, float c, float c0, float& dx,
+                   float& dy, float& dz) {
+    dx = dy = dz = 0.0f;
+    switch (op) {
+        case MC_EX_ADD: dx = c; dy = c; break;
+        case MC_EX_SUB: dx = c; dy = -c; break;
+        case MC_EX_MUL: dx = c * y; dy = c * x; break;
+        case MC_EX_DIV: dx = c / y; dy = -((c * x) / (y * y)); break;
+        case MC_EX_NEG: dx = -c; break;
+        case MC_EX_EXP: dx = c * v; break;
+        case MC_EX_LOG: dx = c / x; break;
+        case MC_EX_SQRT: dx = c / (2.0f * v); break;
+        case MC_EX_SQUARE: dx = c * (2.0f * x); break;
+        case MC_EX_POW:
+            dx = c * (y * powf(x, y - 1.0f));
+            dy = c * (v * logf(x));
+            break;
+        case MC_EX_ABS: dx = x > 0.0f ? c : (x < 0.0f ? -c : 0.0f); break;
+        case MC_EX_LOG1P: dx = c / (1.0f + x); break;
+        case MC_EX_TANH: dx = c * (1.0f - v * v); break;
+        case MC_EX_SIGMOID: dx = c * (v * (1.0f - v)); break;
+        case MC_EX_NORMAL_LP: {
+            const ElemOut e = elem_normal(c0, x, y, z, logf(z));
+            dx = c * e.dv;
+            dy = c * e.dm;
+            dz = c * e.ds;
+            break;
+        }
+        case MC_EX_HALFNORMAL_LP: {
+            const ElemOut e = elem_halfnormal(c0, x, z, logf(z));
+            dx = c * e.dv;
+            dz = c * e.ds;
+            break;
+        }
+        case MC_EX_EXPONENTIAL_LP: {
+            const ElemOut e = elem_exponential(x, z, logf(z));
+            dx = c * e.dv;
+            dz = c * e.ds;
+            break;
+        }
+        case MC_EX_WHERE:
+            if (x != 0.0f) dy = c;
+            else dz = c;
+            break;
+        default: break;
+    }
+}
+
+// One expression term.  Strided (element i -> thread i mod nthr) or, with a
+// non-injective gather (T.primary >= 0), per group run of the segment-tiled
+// layout (build_segments; runs are never split for expression terms), the
+// gathered leaves read q[poff + k] and sum their cotangent in `part` over
+// the run.  Vector leaves deposit in their pass only (sweeps separated by a
+// group barrier: deterministic, no atomics); broadcast (PSCALAR) leaves sum
+// per thread and flush to their cotangent slots after pass 0.
+template <int WPC, bool VALUE_ONLY>
+MC_DEV void eval_expr(const DevTerm& T, const DevCtx& P, const float* q, float* g,
+                      const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc) {
+    const MC_CONST DevExprNode* N = cptr(P.nodes) + T.expr_base;
+    const int nn = T.expr_n;
+    const float w = T.weight;
+    const bool seg = T.primary >= 0;
+    float val[kExMaxNodes], adj[kExMaxNodes], part[kExMaxNodes];
+    const int npass = VALUE_ONLY ? 1 : T.npass;
+    for (int pass = 0; pass < npass; ++pass) {
+        for (int k = 0; k < nn; ++k) part[k] = 0.0f;
+        // element e (strided index, or tiled position), run parameter kr
+        auto element = [&](int64_t e, int kr) {
+            for (int k = 0; k < nn; ++k) {
+                const int op = N[k].op;
+                float v;
+                if (op == MC_EX_LEAF) {
+                    const int kind = N[k].leaf.kind;
+                    const int poff = N[k].leaf.poff;
+                    if (N[k].prim) {
+                        v = q[poff + kr];
+                    } else if (kind == MC_OP_CONST) {
+                        v = N[k].leaf.cval;
+                    } else if (kind == MC_OP_PSCALAR) {
+                        v = q[poff];
+                    } else if (kind == MC_OP_DATA) {
+                        v = P.data[N[k].leaf.pool + e];
+                    } else if (kind == MC_OP_PVEC) {
+                        v = q[poff + e];
+                    } else {
+                        v = q[poff + P.index[N[k].leaf.pool + e]];
+                    }
+                } else {
+                    const int a = N[k].a, b = N[k].b, c = N[k].c;
+                    v = ex_fwd(op, val[a], b >= 0 ? val[b] : 0.0f, c >= 0 ? val[c] : 0.0f,
+                               N[k].leaf.cval);
+                }
+                val[k] = v;
+            }
+            if (pass == 0) lp_acc += w * val[nn - 1];
+            if constexpr (VALUE_ONLY) return;
+            for (int k = 0; k < nn; ++k) adj[k] = 0.0f;
+            adj[nn - 1] = w;
+            for (int k = nn - 1; k >= 0; --k) {
+                const float ck = adj[k];
+                const int op = N[k].op;
+                if (op == MC_EX_LEAF) {
+                    const int kind = N[k].leaf.kind;
+                    if (kind == MC_OP_PSCALAR || N[k].prim) {
+                        part[k] += ck;
+                    } else if ((kind == MC_OP_PVEC || kind == MC_OP_GATHER) && N[k].pass == pass) {
+                        const int poff = N[k].leaf.poff;
+                        const int64_t j = kind == MC_OP_PVEC
+                                              ? (int64_t)poff + e
+                                              : (int64_t)poff + P.index[N[k].leaf.pool + e];
+                        g[j] += ck;
+                    }
+                    continue;
+                }
+                const int a = N[k].a, b = N[k].b, c = N[k].c;
+                float dx, dy, dz;
+                ex_bwd(op, val[a], b >= 0 ? val[b] : 0.0f, c >= 0 ? val[c] : 0.0f, val[k], ck,
+                       N[k].leaf.cval, dx, dy, dz);
+                adj[a] += dx;
+                if (b >= 0) adj[b] += dy;
+                if (c >= 0) adj[c] += dz;
+            }
+        };
+        if (!seg) {
+            for (int64_t i = tid; i < T.n; i += nthr) element(i, 0);
+        } else {
+            const int wave = G.tid >> 6;
+            const int lane = G.tid & 63;
+            const MC_CONST int* tiles = cptr(P.index) + T.tile_base;
+            const int* lanes = P.index + T.lane_base;
+            for (int t = wave; t < T.ntiles; t += WPC) {
+                const int off = tiles[3 * t];
+                const int v = t * 64 + lane;
+                const bool valid = v < T.nvirt;
+                const int kr = valid ? lanes[2 * v] : 0;
+                const int len = valid ? lanes[2 * v + 1] : 0;
+                for (int k = 0; k < nn; ++k)
+                    if (N[k].prim) part[k] = 0.0f;
+                for (int u = 0; u < len; ++u) element(seg_elem(off, u, lane), kr);
+                if (!VALUE_ONLY && valid) {
+                    for (int k = 0; k < nn; ++k)
+                        if (N[k].prim && N[k].pass == pass) g[N[k].leaf.poff + kr] += part[k];
+                }
+            }
+        }
+        if (!VALUE_ONLY && pass == 0) {
+            for (int k = 0; k < nn; ++k) {
+                if (N[k].op != MC_EX_LEAF || N[k].leaf.kind != MC_OP_PSCALAR) continue;
+                if (task) flush_slot_task(G, N[k].leaf.slot, part[k]);
+                else flush_slot(G, N[k].leaf.slot, part[k]);
+            }
+        }
+        if (!VALUE_ONLY && pass + 1 < npass) G.sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // VALUE_ONLY: the forward tape alone (Metropolis-Hastings, mh.h) — every
 // sweep keeps only its PASS_LP work and nothing is written to g.
 template <int WPC, bool VALUE_ONLY = false>
@@ -775,6 +970,10 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
     if (task && (G.tid >> 6) != T.wave_task) return;  // another wave owns it
     const int tid = task ? (G.tid & 63) : G.tid;
     const int nthr = task ? 64 : G.T;
+    if (T.dist == MC_DIST_EXPR) {
+        eval_expr<WPC, VALUE_ONLY>(T, P, q, g, G, task, tid, nthr, lp_acc);
+        return;
+    }
     const float uv = uniform_value(T.op[0], q);
     const float um = uniform_value(T.op[1], q);
     const float us = uniform_value(T.op[2], q);

@@ -65,10 +65,25 @@ struct DevTerm {
     int32_t affine;       // 0 / 1
     int32_t pad_aff;
     DevOperand ab, ax;    // slope (CONST / PSCALAR), x (DATA / PVEC / GATHER)
+    // ---- expression term (MC_DIST_EXPR): DevCtx::nodes[expr_base ..) --------
+    int32_t expr_base;
+    int32_t expr_n;       // nodes; the last is the root
+};
+
+// A node of an expression term (mc_expr_node).  `pass`: the sweep in which a
+// vector leaf deposits its cotangents (leaves with overlapping parameter
+// ranges deposit in different sweeps); `prim`: a leaf gathered through the
+// term's non-injective index (segmented terms: value q[poff + k] of the
+// lane's run, cotangent summed in a register and deposited once per run).
+struct DevExprNode {
+    int32_t op, a, b, c;
+    int32_t pass, prim;
+    DevOperand leaf;
 };
 
 struct DevCtx {
     const DevTerm* terms;
+    const DevExprNode* nodes;  // expression-term nodes (may be null)
     int32_t n_terms;
     int32_t D;
     float lp_const;

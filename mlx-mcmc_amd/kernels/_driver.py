@@ -74,10 +74,11 @@ def run_sampler(algorithm: str, log_prob_fn, initial_params, *, num_samples: int
     layout = program.layout
     note = program.kernel_note
     # no warning where the user cannot act on it: no lane-resident kernel
-    # exists for affine locs, so that note is structural
+    # exists for affine locs or expression terms, so that note is
+    # structural
     if (algorithm == "hmc" and note and num_slices == 0 and slice_kernel == "auto"
             and program.program_elements >= _LANES_WARN_ELEMENTS
-            and program.model.n_affines == 0):
+            and program.model.n_affines == 0 and program.model.n_exprs == 0):
         # a layout the lane-resident kernel declines runs
         # on a 2-4x slower kernel; say so instead of degrading silently
         warnings.warn(f"{note}; running on the {program.slice_kernel} kernel", RuntimeWarning,

@@ -11,7 +11,8 @@ by autograd exactly where the reference uses ``mx.grad``.
   Gamma       restates mlx_mcmc/distributions/gamma.py:40-88
   Beta        restates mlx_mcmc/distributions/beta.py:37-91
               (gammaln: host float64 value, no gradient, as the reference)
-  sum/array/log/exp/where/pi/inf  the mx.* calls those models use
+  sum/array/log/exp/sqrt/square/power/abs/log1p/tanh/sigmoid/where/pi/inf
+              the mx.* calls those models use
 
 Pinned by the reference's own known-answer tests (tests/test_oracle_pins.py
 re-asserts tests/test_distributions.py:18-32,67-79 of the reference).
@@ -53,8 +54,37 @@ def exp(x):
     return torch.exp(_t(x))
 
 
+def sqrt(x):
+    return torch.sqrt(_t(x))
+
+
+def square(x):
+    return torch.square(_t(x))
+
+
+def power(a, b):
+    return torch.pow(_t(a), _t(b))
+
+
+def abs(x):  # noqa: A001
+    return torch.abs(_t(x))
+
+
+def log1p(x):
+    return torch.log1p(_t(x))
+
+
+def tanh(x):
+    return torch.tanh(_t(x))
+
+
+def sigmoid(x):
+    return torch.sigmoid(_t(x))
+
+
 def where(c, a, b):
-    return torch.where(_t(c).bool() if not isinstance(c, torch.Tensor) else c, _t(a), _t(b))
+    c = _t(c)
+    return torch.where(c if c.dtype == torch.bool else c != 0, _t(a), _t(b))
 
 
 class Normal:

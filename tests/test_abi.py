@@ -41,6 +41,8 @@ int main(void) {
   printf("mc_operand %zu\\nmc_term %zu\\nmc_chain_scalars %zu\\nmc_run_config %zu\\nmc_trace %zu\\nmc_affine %zu\\n",
          sizeof(mc_operand), sizeof(mc_term), sizeof(mc_chain_scalars), sizeof(mc_run_config),
          sizeof(mc_trace), sizeof(mc_affine));
+  printf("mc_expr_node %zu\\nmc_expr %zu\\n", sizeof(mc_expr_node), sizeof(mc_expr));
+  O(mc_expr_node, leaf) O(mc_expr, count)
   O(mc_term, affine) O(mc_affine, x) O(mc_term, value) O(mc_term, loc) O(mc_term, scale) O(mc_chain_scalars, logp)
   O(mc_chain_scalars, depth_sum) O(mc_chain_scalars, n_divergent) O(mc_run_config, seed)
   O(mc_run_config, step_size) O(mc_run_config, slice_mode) O(mc_trace, n_leapfrog)
@@ -59,8 +61,11 @@ int main(void) {
     assert int(out["mc_run_config"]) == ctypes.sizeof(_lib.McRunConfig)
     assert int(out["mc_trace"]) == ctypes.sizeof(_lib.McTrace)
     assert int(out["mc_affine"]) == ctypes.sizeof(_lib.McAffine)
+    assert int(out["mc_expr_node"]) == ctypes.sizeof(_lib.McExprNode)
+    assert int(out["mc_expr"]) == ctypes.sizeof(_lib.McExpr)
     for key, (cls, field) in {
         "mc_term.affine": (_lib.McTerm, "affine"), "mc_affine.x": (_lib.McAffine, "x"),
+        "mc_expr_node.leaf": (_lib.McExprNode, "leaf"), "mc_expr.count": (_lib.McExpr, "count"),
         "mc_term.value": (_lib.McTerm, "value"), "mc_term.loc": (_lib.McTerm, "loc"),
         "mc_term.scale": (_lib.McTerm, "scale"),
         "mc_chain_scalars.logp": (_lib.McChainScalars, "logp"),

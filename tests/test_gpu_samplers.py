@@ -200,9 +200,9 @@ def test_vector_params_and_errors(gpu):
         m.hmc(std_normal, {"x": 0.0}, num_samples=10, num_warmup=0, progress=False)
     from mlx_mcmc_amd._trace import TraceError
 
-    with pytest.raises(TraceError):
-        m.nuts(lambda p: mx.log(p["x"]), {"x": 1.0}, num_samples=5, num_warmup=5,
-               progress=False)
+    with pytest.raises(TraceError):   # a Python branch on a parameter value
+        m.nuts(lambda p: m.Normal(0, 1).log_prob(p["x"]) if p["x"] > 0 else 0.0, {"x": 1.0},
+               num_samples=5, num_warmup=5, progress=False)
 
 
 def test_distribution_sampling(gpu):

@@ -133,24 +133,80 @@ X3 = np.arange(3, dtype=np.float32)
 
 
 @pytest.mark.parametrize("bad", [
-    lambda p: m.Normal(0, 1).log_prob(p["x"] * 2.0),          # an expression as a value
-    lambda p: mx.sum(m.Normal(p["x"] + p["x"] * X3 + p["x"] * X3, 1.0).log_prob(X3)),  # 2 products
-    lambda p: mx.sum(m.Normal(p["x"] * p["x"], 1.0).log_prob(X3)),  # product of parameters
-    lambda p: mx.sum(m.Normal(0.0, p["x"] * 2.0).log_prob(X3)),  # an expression as a scale
-    lambda p: m.Gamma(p["x"] * 2.0, 1.0).log_prob(p["x"]),      # not a Normal loc
-    lambda p: mx.sum(m.Normal((p["x"] + p["x"] * X3) * 2.0, 1.0).log_prob(X3)),  # scaled affine
+    lambda p: m.Gamma(p["x"] * 2.0, 1.0).log_prob(p["x"]),      # Gamma over an expression
     lambda p: m.Normal(0, 1).log_prob(p["x"]) if p["x"] > 0 else 0,  # Python branch
-    lambda p: mx.log(p["x"]),                                   # a parameter, not a density
     lambda p: m.Normal(0, 1).log_prob(p["v"]),                  # unsummed vector
-    lambda p: m.Normal(0, 1).log_prob(mx.exp(mx.exp(p["x"]))),  # a transform of a transform
-    lambda p: m.Normal(0, 1).log_prob(mx.exp(p["x"] * 2.0)),    # exp of an expression
-    lambda p: m.Normal(0, 1).log_prob(p["x"]) + p["x"] * p["x"],  # a product added to lp
     lambda p: m.Normal(0, 1).log_prob(p["x"]) + p["v"],         # unsummed vector identity
-    lambda p: mx.sum(m.Normal(2.0 * p["x"], 1.0).log_prob(X3)),  # const * scalar as a loc
+    lambda p: mx.sum(m.Normal(0, 1).log_prob((p["v"] * 2.0)[0])),  # indexing an expression
+    lambda p: mx.sum(mx.where(p["v"] > 0, p["v"], 0.0)),         # a traced where condition
+    lambda p: m.Normal(0, 1).log_prob(p["x"]) * p["x"],         # a density times a parameter
+    lambda p: mx.sum(m.Normal(p["v"] * X3, 1.0).log_prob(np.zeros(4, np.float32))),  # shapes
+    lambda p: mx.sum(_deep(p["v"], 40)),                        # more than 32 nodes
 ])
 def test_unsupported_models_raise(bad):
     with pytest.raises(_trace.TraceError):
         _trace.trace(bad, {"x": 1.0, "v": np.zeros(3, np.float32)})
+
+
+def _deep(x, k):
+    for i in range(k):
+        x = mx.tanh(x * (1.0 + i))
+    return x
+
+
+# Expressions the fused terms do not cover trace to expression terms
+# (MC_DIST_EXPR, eval.h eval_expr) — each of these raised TraceError before
+@pytest.mark.parametrize("good", [
+    lambda p: m.Normal(0, 1).log_prob(p["x"] * 2.0),          # an expression as a value
+    lambda p: mx.sum(m.Normal(p["x"] + p["x"] * X3 + p["x"] * X3, 1.0).log_prob(X3)),  # 2 products
+    lambda p: mx.sum(m.Normal(p["x"] * p["x"], 1.0).log_prob(X3)),  # product of parameters
+    lambda p: mx.sum(m.Normal(0.0, p["x"] * 2.0).log_prob(X3)),  # an expression as a scale
+    lambda p: mx.sum(m.Normal((p["x"] + p["x"] * X3) * 2.0, 1.0).log_prob(X3)),  # scaled affine
+    lambda p: mx.log(p["x"]),                                   # a scalar expression as lp
+    lambda p: m.Normal(0, 1).log_prob(mx.exp(mx.exp(p["x"]))),  # a transform of a transform
+    lambda p: m.Normal(0, 1).log_prob(mx.exp(p["x"] * 2.0)),    # exp of an expression
+    lambda p: m.Normal(0, 1).log_prob(p["x"]) + p["x"] * p["x"],  # a product added to lp
+    lambda p: mx.sum(m.Normal(2.0 * p["x"], 1.0).log_prob(X3)),  # const * scalar as a loc
+    lambda p: mx.sum(m.Normal(p["x"] + 1.0, 1.0).log_prob(X3)),  # scalar + constant as a loc
+    lambda p: mx.sum(m.Normal(p["x"] + p["y"], 1.0).log_prob(X3)),  # sum of scalars as a loc
+    lambda p: mx.sum(-0.5 * mx.square(p["v"] - X3) / p["x"]),   # a hand-written density
+    lambda p: mx.sum(mx.where(X3 > 1, mx.sqrt(mx.abs(p["v"])), mx.tanh(p["v"]))),
+    lambda p: mx.sum(mx.log1p(mx.sigmoid(p["v"]) ** 2.0)),
+    lambda p: m.HalfNormal(mx.exp(p["x"]) + 1.0).log_prob(p["y"] * p["y"]),
+    lambda p: m.Exponential(p["x"] * p["y"]).log_prob(mx.exp(p["y"])),
+])
+def test_general_expressions_trace(good):
+    tm = _trace.trace(good, {"x": 1.0, "y": 0.5, "v": np.zeros(3, np.float32)})
+    exprs = [t for t in tm.terms if t.dist == _lib.MC_DIST_EXPR]
+    assert exprs and tm.n_exprs == len(exprs) and tm.n_nodes >= 2
+    for k in range(tm.n_exprs):
+        first, count = tm.c_exprs[k].first, tm.c_exprs[k].count
+        for i in range(first, first + count):
+            nd = tm.c_nodes[i]
+            for a in (nd.a, nd.b, nd.c):   # arguments precede their users
+                assert a < i - first
+            if nd.op == _lib.MC_EX_LEAF:
+                assert nd.leaf.transform == 0 and (nd.a, nd.b, nd.c) == (-1, -1, -1)
+
+
+def test_expression_models_trace_to_expected_terms():
+    """The expression workloads keep their fused parts fused (priors, the
+    log-Jacobian identity term) and put only the rest in expression terms;
+    the varying-slopes likelihood gathers alpha and beta through one index."""
+    lp, init = W.two_predictor_regression(W.ns_product())
+    tm = _trace.trace(lp, init)
+    assert [t.dist for t in tm.terms].count(_lib.MC_DIST_EXPR) == 1
+    assert _lib.MC_DIST_IDENTITY in [t.dist for t in tm.terms]
+    ops = [tm.c_nodes[i].op for i in range(tm.n_nodes)]
+    assert ops[-1] == _lib.MC_EX_NORMAL_LP and _lib.MC_EX_EXP in ops
+    lp, init = W.varying_slopes(W.ns_product())
+    tm = _trace.trace(lp, init)
+    gathers = [tm.c_nodes[i].leaf for i in range(tm.n_nodes)
+               if tm.c_nodes[i].op == _lib.MC_EX_LEAF and tm.c_nodes[i].leaf.kind == _lib.MC_OP_GATHER]
+    assert len(gathers) == 2 and gathers[0].pool_offset == gathers[1].pool_offset
+    for f in (W.logistic_regression, W.cauchy_location):
+        tm = _trace.trace(*f(W.ns_product()))
+        assert any(t.dist == _lib.MC_DIST_EXPR for t in tm.terms)
 
 
 def test_layout_roundtrip():
@@ -182,23 +238,6 @@ def test_mcmc_method_errors():
             mc.run({"x": 0.0}, method="metropolis", verbose=False)
     with pytest.raises(ValueError):
         mc.summary()
-
-
-def test_scalar_param_plus_constant_loc_message():
-    """`mu + 1.0` as a loc names the real cause (a constant), not
-    'a sum of two scalar parameters'."""
-    y = W.simple_normal_data()
-
-    def shifted(p):
-        return mx.sum(m.Normal(p["mu"] + 1.0, 1.0).log_prob(mx.array(y)))
-
-    def two(p):
-        return mx.sum(m.Normal(p["mu"] + p["nu"], 1.0).log_prob(mx.array(y)))
-
-    with pytest.raises(_trace.TraceError, match="plus a constant"):
-        _trace.trace(shifted, {"mu": 0.0})
-    with pytest.raises(_trace.TraceError, match="two scalar parameters"):
-        _trace.trace(two, {"mu": 0.0, "nu": 0.0})
 
 
 def test_transformed_operands_and_identity_terms():

@@ -19,7 +19,9 @@ def ns_product():
 
     return SimpleNamespace(Normal=m.Normal, HalfNormal=m.HalfNormal, Exponential=m.Exponential,
                            Gamma=m.Gamma, Beta=m.Beta, sum=mx.sum, array=mx.array,
-                           exp=mx.exp, log=mx.log, name="product")
+                           exp=mx.exp, log=mx.log, sqrt=mx.sqrt, square=mx.square,
+                           power=mx.power, abs=mx.abs, log1p=mx.log1p, tanh=mx.tanh,
+                           sigmoid=mx.sigmoid, where=mx.where, pi=mx.pi, name="product")
 
 
 def ns_oracle():
@@ -27,7 +29,9 @@ def ns_oracle():
 
     return SimpleNamespace(Normal=ns.Normal, HalfNormal=ns.HalfNormal, Exponential=ns.Exponential,
                            Gamma=ns.Gamma, Beta=ns.Beta, sum=ns.sum, array=ns.array,
-                           exp=ns.exp, log=ns.log, name="oracle")
+                           exp=ns.exp, log=ns.log, sqrt=ns.sqrt, square=ns.square,
+                           power=ns.power, abs=ns.abs, log1p=ns.log1p, tanh=ns.tanh,
+                           sigmoid=ns.sigmoid, where=ns.where, pi=ns.pi, name="oracle")
 
 
 # ---- config 1: examples/01_simple_normal.py:26-50 (vectorised as in
@@ -302,3 +306,104 @@ def varying_intercept(ns, G=20, N=2000):
 
     return log_prob, {"mu": np.float32(1.0), "tau": np.float32(1.5), "beta": np.float32(0.7),
                       "sigma": np.float32(0.8), "alpha": np.ones(G, np.float32)}
+
+
+# ---- general elementwise expressions (expression terms, MC_DIST_EXPR) ------------
+def two_predictor_data(n=1000, seed=5):
+    rng = np.random.default_rng(seed)
+    x1 = rng.normal(0.0, 1.0, n).astype(np.float32)
+    x2 = rng.normal(0.0, 1.0, n).astype(np.float32)
+    y = (0.5 + 1.2 * x1 - 0.8 * x2 + rng.normal(0.0, 0.6, n)).astype(np.float32)
+    return x1, x2, y
+
+
+def two_predictor_regression(ns, n=1000):
+    """y ~ N(a + b1 x1 + b2 x2, exp(log_sigma)): two products in the loc and
+    a log-scale noise with its Jacobian (an expression term)."""
+    x1, x2, y = two_predictor_data(n)
+
+    def log_prob(params):
+        a, b1, b2, log_sigma = params["a"], params["b1"], params["b2"], params["log_sigma"]
+        sigma = ns.exp(log_sigma)
+        lp = ns.Normal(0, 10).log_prob(a) + ns.Normal(0, 10).log_prob(b1)
+        lp = lp + ns.Normal(0, 10).log_prob(b2) + ns.HalfNormal(5).log_prob(sigma) + log_sigma
+        mean = a + b1 * ns.array(x1) + b2 * ns.array(x2)
+        return lp + ns.sum(ns.Normal(mean, sigma).log_prob(ns.array(y)))
+
+    return log_prob, {"a": np.float32(0.0), "b1": np.float32(0.0), "b2": np.float32(0.0),
+                      "log_sigma": np.float32(0.0)}
+
+
+def logistic_data(n=500, seed=6):
+    rng = np.random.default_rng(seed)
+    x = rng.normal(0.0, 1.0, n).astype(np.float32)
+    p = 1.0 / (1.0 + np.exp(-(-0.3 + 1.1 * x)))
+    y = (rng.random(n) < p).astype(np.float32)
+    return x, y
+
+
+def logistic_regression(ns, n=500):
+    """Bernoulli likelihood written out with mx.sigmoid / mx.log / mx.log1p."""
+    x, y = logistic_data(n)
+
+    def log_prob(params):
+        a, b = params["a"], params["b"]
+        lp = ns.Normal(0, 5).log_prob(a) + ns.Normal(0, 5).log_prob(b)
+        p = ns.sigmoid(a + b * ns.array(x))
+        ll = ns.array(y) * ns.log(p) + (1.0 - ns.array(y)) * ns.log1p(-p)
+        return lp + ns.sum(ll)
+
+    return log_prob, {"a": np.float32(0.0), "b": np.float32(0.0)}
+
+
+def varying_slopes_data(G=16, N=1600, seed=7):
+    rng = np.random.default_rng(seed)
+    group = rng.integers(0, G, N).astype(np.int32)          # unsorted: the tape sorts it
+    alpha = rng.normal(1.0, 1.0, G)
+    beta = rng.normal(-0.5, 0.7, G)
+    x = rng.normal(0.0, 1.0, N).astype(np.float32)
+    y = (alpha[group] + beta[group] * x + rng.normal(0.0, 0.5, N)).astype(np.float32)
+    return x, y, group
+
+
+def varying_slopes(ns, G=16, N=1600):
+    """y_i ~ N(alpha[g_i] + beta[g_i] x_i, sigma): two gathers through one
+    non-injective index in a product and a sum (the segmented expression
+    path), alpha ~ N(mu_a, 2), beta ~ N(mu_b, 2)."""
+    x, y, group = varying_slopes_data(G, N)
+
+    def log_prob(params):
+        mu_a, mu_b, sigma = params["mu_a"], params["mu_b"], params["sigma"]
+        alpha, beta = params["alpha"], params["beta"]
+        lp = ns.Normal(0, 5).log_prob(mu_a) + ns.Normal(0, 5).log_prob(mu_b)
+        lp = lp + ns.HalfNormal(2).log_prob(sigma)
+        lp = lp + ns.sum(ns.Normal(mu_a, 2.0).log_prob(alpha))
+        lp = lp + ns.sum(ns.Normal(mu_b, 2.0).log_prob(beta))
+        mean = alpha[group] + beta[group] * ns.array(x)
+        return lp + ns.sum(ns.Normal(mean, sigma).log_prob(ns.array(y)))
+
+    return log_prob, {"mu_a": np.float32(1.0), "mu_b": np.float32(-0.5),
+                      "sigma": np.float32(0.5), "alpha": np.ones(G, np.float32),
+                      "beta": np.zeros(G, np.float32)}
+
+
+def cauchy_location(ns, n=200, seed=8):
+    """A Cauchy location-scale likelihood written by hand (the reference has no
+    Cauchy): -log(pi s) - log1p(((y - mu) / s)^2), s = sqrt(v); plus the other
+    elementwise ops (tanh, abs, power, where over a data mask) in a weak
+    extra term, so every expression op is differentiated somewhere."""
+    rng = np.random.default_rng(seed)
+    y = (2.0 + rng.standard_cauchy(n) * 0.7).astype(np.float32)
+    mask = (np.arange(n) % 3 == 0).astype(np.float32)
+
+    def log_prob(params):
+        mu, v, w = params["mu"], params["v"], params["w"]
+        s = ns.sqrt(v)
+        lp = ns.Normal(0, 10).log_prob(mu) + ns.Exponential(1.0).log_prob(v)
+        lp = lp + ns.Normal(0, 1).log_prob(w)
+        z = (ns.array(y) - mu) / s
+        lp = lp + ns.sum(-ns.log(ns.pi * s) - ns.log1p(ns.square(z)))
+        extra = ns.where(ns.array(mask), ns.tanh(w * z), -0.1 * ns.power(ns.abs(w) + 1.0, 1.5))
+        return lp + 0.01 * ns.sum(extra)
+
+    return log_prob, {"mu": np.float32(2.0), "v": np.float32(0.5), "w": np.float32(0.1)}
