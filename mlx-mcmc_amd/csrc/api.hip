@@ -112,6 +112,7 @@ struct mc_program {
     std::vector<DevTerm> terms;
     DevTerm* d_terms = nullptr;
     std::vector<DevExprNode> nodes;  // expression-term nodes (DevTerm::expr_base)
+    bool ex = false;                 // has expression terms: the EX kernel instantiations
     DevExprNode* d_nodes = nullptr;
     float* d_data = nullptr;
     int32_t* d_index = nullptr;
@@ -1983,6 +1984,7 @@ extern "C" int mc_program_create_expr(const mc_term* terms, int32_t n_terms,
     p->terms = dts;
     p->raw = raws;
     p->nodes = gnodes;
+    p->ex = !gnodes.empty();
     p->h_data = dpool;
     p->h_index = ipool;
     hipError_t e = hipSuccess;
@@ -2103,7 +2105,7 @@ static TraceDev trace_of(const mc_trace* t) {
 // ---------------------------------------------------------------------------
 // batched log density + gradient
 // ---------------------------------------------------------------------------
-template <int WPC>
+template <int WPC, bool EX>
 __global__ void __launch_bounds__(WPC >= 4 ? 64 * WPC : 256)
 k_logp(DevCtx P, int64_t n_points, const float* q, float* logp, float* grad, int lds_floats) {
     constexpr int CPB = (WPC >= 4) ? 1 : 4 / WPC;
@@ -2116,18 +2118,18 @@ k_logp(DevCtx P, int64_t n_points, const float* q, float* logp, float* grad, int
     SegScratch S;
     G.tid = threadIdx.x % T;
     carve_group<WPC>(smem + (int64_t)lc * lds_floats, G, S);
-    const float lp = eval_lp_grad<WPC>(P, q + c * P.D, grad + c * P.D, G, S);
+    const float lp = eval_lp_grad<WPC, false, EX>(P, q + c * P.D, grad + c * P.D, G, S);
     if (G.tid == 0) logp[c] = lp;
 }
 
-template <int WPC>
+template <int WPC, bool EX>
 static int launch_logp(const mc_program* p, int64_t n, const float* q, float* lp, float* g,
                        hipStream_t st) {
     const int lds_floats = scratch_of(p);
     const size_t lds = (size_t)cpb_of(WPC) * lds_floats * 4;
     const int64_t grid = (n + cpb_of(WPC) - 1) / cpb_of(WPC);
-    MC_HIP_TRY(allow_lds(k_logp<WPC>, lds));
-    hipLaunchKernelGGL(k_logp<WPC>, dim3((unsigned)grid), dim3(block_of(WPC)), lds, st, ctx_of(p),
+    MC_HIP_TRY(allow_lds(k_logp<WPC, EX>, lds));
+    hipLaunchKernelGGL((k_logp<WPC, EX>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st, ctx_of(p),
                        n, q, lp, g, lds_floats);
     MC_HIP_TRY(hipGetLastError());
     return MC_OK;
@@ -2141,9 +2143,12 @@ extern "C" int mc_logp_grad(const mc_program* p, int64_t n_points, const float* 
     if (!q || !logp || !grad) return fail(MC_ERR_INVALID, "NULL buffer");
     hipStream_t st = (hipStream_t)stream;
     switch (p->wpc) {
-        case 1: return launch_logp<1>(p, n_points, q, logp, grad, st);
-        case 4: return launch_logp<4>(p, n_points, q, logp, grad, st);
-        default: return launch_logp<8>(p, n_points, q, logp, grad, st);
+        case 1: return p->ex ? launch_logp<1, true>(p, n_points, q, logp, grad, st)
+                             : launch_logp<1, false>(p, n_points, q, logp, grad, st);
+        case 4: return p->ex ? launch_logp<4, true>(p, n_points, q, logp, grad, st)
+                             : launch_logp<4, false>(p, n_points, q, logp, grad, st);
+        default: return p->ex ? launch_logp<8, true>(p, n_points, q, logp, grad, st)
+                              : launch_logp<8, false>(p, n_points, q, logp, grad, st);
     }
 }
 
@@ -2200,7 +2205,7 @@ extern "C" int64_t mc_state_bytes(const mc_program* p, int64_t C) {
     return align256(C * (int64_t)sizeof(mc_chain_scalars)) + 2 * align256(C * p->D * 4);
 }
 
-template <int WPC>
+template <int WPC, bool EX>
 __global__ void __launch_bounds__(WPC >= 4 ? 64 * WPC : 256)
 k_init(DevCtx P, int64_t C, const float* q0, double eps0, float mu, mc_chain_scalars* scal,
        float* st_q, float* st_g, int lds_floats) {
@@ -2216,7 +2221,7 @@ k_init(DevCtx P, int64_t C, const float* q0, double eps0, float mu, mc_chain_sca
     carve_group<WPC>(smem + (int64_t)lc * lds_floats, G, S);
     const int D = P.D;
     for (int j = G.tid; j < D; j += T) st_q[c * D + j] = q0[c * D + j];
-    const float lp = eval_lp_grad<WPC>(P, q0 + c * D, st_g + c * D, G, S);
+    const float lp = eval_lp_grad<WPC, false, EX>(P, q0 + c * D, st_g + c * D, G, S);
     if (G.tid == 0) {
         mc_chain_scalars sc = {};
         sc.step_size = eps0;
@@ -2229,7 +2234,7 @@ k_init(DevCtx P, int64_t C, const float* q0, double eps0, float mu, mc_chain_sca
     }
 }
 
-template <int WPC>
+template <int WPC, bool EX>
 static int launch_init(const mc_program* p, int64_t C, const float* q0, double eps0,
                        void* state, hipStream_t st) {
     int64_t qo, go;
@@ -2239,8 +2244,8 @@ static int launch_init(const mc_program* p, int64_t C, const float* q0, double e
     const size_t lds = (size_t)cpb_of(WPC) * lds_floats * 4;
     const int64_t grid = (C + cpb_of(WPC) - 1) / cpb_of(WPC);
     const float mu = mc_logf_ref((float)(10.0 * eps0));  // nuts.py:63 mx.log(10 * step_size)
-    MC_HIP_TRY(allow_lds(k_init<WPC>, lds));
-    hipLaunchKernelGGL(k_init<WPC>, dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
+    MC_HIP_TRY(allow_lds(k_init<WPC, EX>, lds));
+    hipLaunchKernelGGL((k_init<WPC, EX>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
                        ctx_of(p), C, q0, eps0, mu, (mc_chain_scalars*)b, (float*)(b + qo),
                        (float*)(b + go), lds_floats);
     MC_HIP_TRY(hipGetLastError());
@@ -2253,9 +2258,12 @@ extern "C" int mc_state_init(const mc_program* p, int64_t C, const float* q0, do
     if (C == 0) return MC_OK;
     hipStream_t st = (hipStream_t)stream;
     switch (p->wpc) {
-        case 1: return launch_init<1>(p, C, q0, eps0, state, st);
-        case 4: return launch_init<4>(p, C, q0, eps0, state, st);
-        default: return launch_init<8>(p, C, q0, eps0, state, st);
+        case 1: return p->ex ? launch_init<1, true>(p, C, q0, eps0, state, st)
+                             : launch_init<1, false>(p, C, q0, eps0, state, st);
+        case 4: return p->ex ? launch_init<4, true>(p, C, q0, eps0, state, st)
+                             : launch_init<4, false>(p, C, q0, eps0, state, st);
+        default: return p->ex ? launch_init<8, true>(p, C, q0, eps0, state, st)
+                              : launch_init<8, false>(p, C, q0, eps0, state, st);
     }
 }
 
@@ -2583,7 +2591,7 @@ extern "C" int64_t mc_hmc_workspace_bytes(const mc_program* p, int64_t C) {
     return std::max(x, C * 5 * (int64_t)dpad_of(p->D) * 4);
 }
 
-template <int WPC, bool LDS>
+template <int WPC, bool LDS, bool EX>
 static int launch_hmc(const mc_program* p, const mc_run_config* cfg, void* state,
                       float* samples, const mc_trace* tr, float* ws, hipStream_t st) {
     int64_t qo, go;
@@ -2597,8 +2605,8 @@ static int launch_hmc(const mc_program* p, const mc_run_config* cfg, void* state
     A.scratch_floats = scratch_of(p);
     const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
     const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
-    MC_HIP_TRY(allow_lds(k_hmc<WPC, LDS>, lds));
-    hipLaunchKernelGGL((k_hmc<WPC, LDS>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
+    MC_HIP_TRY(allow_lds(k_hmc<WPC, LDS, EX>, lds));
+    hipLaunchKernelGGL((k_hmc<WPC, LDS, EX>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
                        ctx_of(p), A, (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go),
                        samples, trace_of(tr), ws);
     MC_HIP_TRY(hipGetLastError());
@@ -2643,12 +2651,12 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
     hipStream_t st = (hipStream_t)stream;
     float* w = (float*)ws;
     switch (p->wpc) {
-        case 1: return lds ? launch_hmc<1, true>(p, cfg, state, samples, tr, w, st)
-                           : launch_hmc<1, false>(p, cfg, state, samples, tr, w, st);
-        case 4: return lds ? launch_hmc<4, true>(p, cfg, state, samples, tr, w, st)
-                           : launch_hmc<4, false>(p, cfg, state, samples, tr, w, st);
-        default: return lds ? launch_hmc<8, true>(p, cfg, state, samples, tr, w, st)
-                            : launch_hmc<8, false>(p, cfg, state, samples, tr, w, st);
+        case 1: return lds ? (p->ex ? launch_hmc<1, true, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<1, true, false>(p, cfg, state, samples, tr, w, st))
+                           : (p->ex ? launch_hmc<1, false, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<1, false, false>(p, cfg, state, samples, tr, w, st));
+        case 4: return lds ? (p->ex ? launch_hmc<4, true, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<4, true, false>(p, cfg, state, samples, tr, w, st))
+                           : (p->ex ? launch_hmc<4, false, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<4, false, false>(p, cfg, state, samples, tr, w, st));
+        default: return lds ? (p->ex ? launch_hmc<8, true, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<8, true, false>(p, cfg, state, samples, tr, w, st))
+                            : (p->ex ? launch_hmc<8, false, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<8, false, false>(p, cfg, state, samples, tr, w, st));
     }
 }
 
@@ -2666,7 +2674,7 @@ extern "C" int64_t mc_mh_workspace_bytes(const mc_program* p, int64_t C) {
     return C * 2 * (int64_t)dpad_of(p->D) * 4;
 }
 
-template <int WPC, bool LDS>
+template <int WPC, bool LDS, bool EX>
 static int launch_mh(const mc_program* p, const mc_run_config* cfg, float scale, void* state,
                      float* samples, const mc_trace* tr, float* ws, hipStream_t st) {
     int64_t qo, go;
@@ -2680,8 +2688,8 @@ static int launch_mh(const mc_program* p, const mc_run_config* cfg, float scale,
     A.scratch_floats = scratch_of(p);
     const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
     const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
-    MC_HIP_TRY(allow_lds(k_mh<WPC, LDS>, lds));
-    hipLaunchKernelGGL((k_mh<WPC, LDS>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
+    MC_HIP_TRY(allow_lds(k_mh<WPC, LDS, EX>, lds));
+    hipLaunchKernelGGL((k_mh<WPC, LDS, EX>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
                        ctx_of(p), A, scale, (mc_chain_scalars*)b, (float*)(b + qo), samples,
                        trace_of(tr), ws);
     MC_HIP_TRY(hipGetLastError());
@@ -2704,12 +2712,12 @@ extern "C" int mc_mh_run(const mc_program* p, const mc_run_config* cfg, double p
     float* w = (float*)ws;
     const float sc = (float)proposal_scale;  // f32(proposal_scale): MLX's weak scalar
     switch (p->wpc) {
-        case 1: return lds ? launch_mh<1, true>(p, cfg, sc, state, samples, tr, w, st)
-                           : launch_mh<1, false>(p, cfg, sc, state, samples, tr, w, st);
-        case 4: return lds ? launch_mh<4, true>(p, cfg, sc, state, samples, tr, w, st)
-                           : launch_mh<4, false>(p, cfg, sc, state, samples, tr, w, st);
-        default: return lds ? launch_mh<8, true>(p, cfg, sc, state, samples, tr, w, st)
-                            : launch_mh<8, false>(p, cfg, sc, state, samples, tr, w, st);
+        case 1: return lds ? (p->ex ? launch_mh<1, true, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<1, true, false>(p, cfg, sc, state, samples, tr, w, st))
+                           : (p->ex ? launch_mh<1, false, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<1, false, false>(p, cfg, sc, state, samples, tr, w, st));
+        case 4: return lds ? (p->ex ? launch_mh<4, true, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<4, true, false>(p, cfg, sc, state, samples, tr, w, st))
+                           : (p->ex ? launch_mh<4, false, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<4, false, false>(p, cfg, sc, state, samples, tr, w, st));
+        default: return lds ? (p->ex ? launch_mh<8, true, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<8, true, false>(p, cfg, sc, state, samples, tr, w, st))
+                            : (p->ex ? launch_mh<8, false, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<8, false, false>(p, cfg, sc, state, samples, tr, w, st));
     }
 }
 
@@ -2733,7 +2741,7 @@ extern "C" int64_t mc_nuts_workspace_bytes(const mc_program* p, int64_t C, int32
     return C * nuts_arena_vectors(max_depth) * (int64_t)dpad_of(p->D) * 4;
 }
 
-template <int WPC, bool LDS>
+template <int WPC, bool LDS, bool EX>
 static int launch_nuts(const mc_program* p, const mc_run_config* cfg, void* state,
                        float* samples, const mc_trace* tr, float* ws, hipStream_t st) {
     int64_t qo, go;
@@ -2754,8 +2762,8 @@ static int launch_nuts(const mc_program* p, const mc_run_config* cfg, void* stat
         lds += dbytes;
     }
     const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
-    MC_HIP_TRY(allow_lds(k_nuts<WPC, LDS>, lds));
-    hipLaunchKernelGGL((k_nuts<WPC, LDS>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
+    MC_HIP_TRY(allow_lds(k_nuts<WPC, LDS, EX>, lds));
+    hipLaunchKernelGGL((k_nuts<WPC, LDS, EX>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
                        ctx_of(p), A, (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go),
                        samples, trace_of(tr), ws);
     MC_HIP_TRY(hipGetLastError());
@@ -2870,12 +2878,12 @@ extern "C" int mc_nuts_run(const mc_program* p, const mc_run_config* cfg, void* 
     float* w = (float*)ws;
     const bool lds = nuts_use_lds(p, cfg->max_tree_depth);
     switch (p->wpc) {
-        case 1: return lds ? launch_nuts<1, true>(p, cfg, state, samples, tr, w, st)
-                           : launch_nuts<1, false>(p, cfg, state, samples, tr, w, st);
-        case 4: return lds ? launch_nuts<4, true>(p, cfg, state, samples, tr, w, st)
-                           : launch_nuts<4, false>(p, cfg, state, samples, tr, w, st);
-        default: return lds ? launch_nuts<8, true>(p, cfg, state, samples, tr, w, st)
-                            : launch_nuts<8, false>(p, cfg, state, samples, tr, w, st);
+        case 1: return lds ? (p->ex ? launch_nuts<1, true, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<1, true, false>(p, cfg, state, samples, tr, w, st))
+                           : (p->ex ? launch_nuts<1, false, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<1, false, false>(p, cfg, state, samples, tr, w, st));
+        case 4: return lds ? (p->ex ? launch_nuts<4, true, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<4, true, false>(p, cfg, state, samples, tr, w, st))
+                           : (p->ex ? launch_nuts<4, false, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<4, false, false>(p, cfg, state, samples, tr, w, st));
+        default: return lds ? (p->ex ? launch_nuts<8, true, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<8, true, false>(p, cfg, state, samples, tr, w, st))
+                            : (p->ex ? launch_nuts<8, false, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<8, false, false>(p, cfg, state, samples, tr, w, st));
     }
 }
 

@@ -858,9 +858,13 @@ MC_DEV void ex_bwd(int op, float x, float y, float z, float v, float c, float c0
 // the run.  Vector leaves deposit in their pass only (sweeps separated by a
 // group barrier: deterministic, no atomics); broadcast (PSCALAR) leaves sum
 // per thread and flush to their cotangent slots after pass 0.
+// (not inlined: the node / adjoint arrays would otherwise raise the register
+// count of every tape kernel, expression program or not)
 template <int WPC, bool VALUE_ONLY>
-MC_DEV void eval_expr(const DevTerm& T, const DevCtx& P, const float* q, float* g,
-                      const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc) {
+__device__ __attribute__((noinline)) void eval_expr(const DevTerm& T, const DevCtx& P,
+                                                    const float* q, float* g,
+                                                    const Group<WPC>& G, bool task, int tid,
+                                                    int nthr, float& lp_acc) {
     const MC_CONST DevExprNode* N = cptr(P.nodes) + T.expr_base;
     const int nn = T.expr_n;
     const float w = T.weight;
@@ -962,7 +966,9 @@ MC_DEV void eval_expr(const DevTerm& T, const DevCtx& P, const float* q, float* 
 // ---------------------------------------------------------------------------
 // VALUE_ONLY: the forward tape alone (Metropolis-Hastings, mh.h) — every
 // sweep keeps only its PASS_LP work and nothing is written to g.
-template <int WPC, bool VALUE_ONLY = false>
+// EX: the program holds expression terms (separate kernel instantiations, so
+// programs without them keep the register budget they had).
+template <int WPC, bool VALUE_ONLY = false, bool EX = false>
 MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* g,
                       const Group<WPC>& G, float& lp_acc, const SegScratch& S) {
     MC_STAMP_DECL
@@ -970,9 +976,11 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
     if (task && (G.tid >> 6) != T.wave_task) return;  // another wave owns it
     const int tid = task ? (G.tid & 63) : G.tid;
     const int nthr = task ? 64 : G.T;
-    if (T.dist == MC_DIST_EXPR) {
-        eval_expr<WPC, VALUE_ONLY>(T, P, q, g, G, task, tid, nthr, lp_acc);
-        return;
+    if constexpr (EX) {
+        if (T.dist == MC_DIST_EXPR) {
+            eval_expr<WPC, VALUE_ONLY>(T, P, q, g, G, task, tid, nthr, lp_acc);
+            return;
+        }
     }
     const float uv = uniform_value(T.op[0], q);
     const float um = uniform_value(T.op[1], q);
@@ -1088,7 +1096,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
 // when the caller zeroed it in its own sweep), one before a term whose vector
 // writes overlap an earlier term's since the last barrier (host-computed
 // sync_before), one before and one after the fixed-order slot reduction.
-template <int WPC, bool VALUE_ONLY = false>
+template <int WPC, bool VALUE_ONLY = false, bool EX = false>
 MC_DEV float eval_lp_grad(const DevCtx& P, const float* q, float* g, const Group<WPC>& G,
                           const SegScratch& S, bool g_zeroed = false) {
     MC_STAMP_DECL
@@ -1102,7 +1110,7 @@ MC_DEV float eval_lp_grad(const DevCtx& P, const float* q, float* g, const Group
         const DevTerm T = load_term(terms + t);
         if (!VALUE_ONLY && T.sync_before) G.sync();
         MC_STAMP(2 + 2 * (t < 7 ? t : 7));
-        eval_term<WPC, VALUE_ONLY>(T, P, q, g, G, lp_acc, S);
+        eval_term<WPC, VALUE_ONLY, EX>(T, P, q, g, G, lp_acc, S);
         MC_STAMP(3 + 2 * (t < 7 ? t : 7));
     }
     const int lp_slot = P.nslots - 1;

@@ -21,7 +21,7 @@
 
 namespace mc {
 
-template <int WPC, bool LDS_ARENA>
+template <int WPC, bool LDS_ARENA, bool EX>
 __global__ void __launch_bounds__(WPC >= 4 ? 64 * WPC : 256)
 k_hmc(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, float* samples,
       TraceDev tr, float* ws) {
@@ -109,7 +109,7 @@ k_hmc(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, flo
             }
             G.sync();
             MC_STAMP(0);
-            lpn = eval_lp_grad<WPC>(P, qB, gB, G, S, true);
+            lpn = eval_lp_grad<WPC, false, EX>(P, qB, gB, G, S, true);
             MC_STAMP(1);
             cq = qB;
             cg = gB;

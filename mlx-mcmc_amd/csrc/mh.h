@@ -16,7 +16,7 @@
 
 namespace mc {
 
-template <int WPC, bool LDS_ARENA>
+template <int WPC, bool LDS_ARENA, bool EX>
 __global__ void __launch_bounds__(WPC >= 4 ? 64 * WPC : 256)
 k_mh(DevCtx P, RunArgs A, float scale, mc_chain_scalars* scal, float* st_q, float* samples,
      TraceDev tr, float* ws) {
@@ -61,7 +61,7 @@ k_mh(DevCtx P, RunArgs A, float scale, mc_chain_scalars* scal, float* st_q, floa
             }
         }
         G.sync();
-        const float lpn = eval_lp_grad<WPC, true>(P, qB, nullptr, G, S);
+        const float lpn = eval_lp_grad<WPC, true, EX>(P, qB, nullptr, G, S);
         const float ratio = lpn - lp;
         const mc_u32x4 ru = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_ACCEPT, 0, 0);
         const float logu = mc_logf_u01(mc_u01_f32(ru.x));

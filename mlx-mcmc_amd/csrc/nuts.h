@@ -69,7 +69,7 @@ MC_DEV int ctz_u32(uint32_t x) { return __builtin_ctz(x); }
 // LDS_ARENA: the arena lives in the workgroup's LDS after the group scratch
 // and the pending words (every trajectory vector one LDS round trip away
 // instead of an L2 one); else in the global workspace.
-template <int WPC, bool LDS_ARENA>
+template <int WPC, bool LDS_ARENA, bool EX>
 __global__ void __launch_bounds__(WPC >= 4 ? 64 * WPC : 256)
 k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, float* samples,
        TraceDev tr, float* ws) {
@@ -221,7 +221,7 @@ k_nuts(DevCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, fl
                 }
                 G.sync();
                 MC_STAMP(8);
-                const float lpl = eval_lp_grad<WPC>(Pd, Eq, Eg, G, S, true);
+                const float lpl = eval_lp_grad<WPC, false, EX>(Pd, Eq, Eg, G, S, true);
                 MC_STAMP(9);
                 float kl = 0.0f;
                 for (int jj = G.tid; jj < D; jj += T) {
