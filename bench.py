@@ -354,6 +354,23 @@ def converged_ess(prog, C, q0, dev, L, args):
     return out
 
 
+_STAGES = []
+
+
+def stage(name):
+    """MC_BENCH_STAGES=1: host timestamps of the bench's phases (stderr), to
+    see the idle gaps before the timed region (the clock drops after ~3 ms)."""
+    if os.environ.get("MC_BENCH_STAGES"):
+        _STAGES.append((name, time.perf_counter()))
+
+
+def print_stages():
+    if _STAGES:
+        t0 = _STAGES[0][1]
+        print("stages (ms): " + ", ".join(f"{n} {1e3 * (t - t0):.2f}" for n, t in _STAGES),
+              file=sys.stderr)
+
+
 def check(chains, where):
     """A sliced launch whose cross-workgroup exchange timed out skipped work:
     report it and exit non-zero rather than publish a number for it."""
@@ -596,7 +613,9 @@ def main():
 
         def scratch(n):
             tmp.run_hmc(samples=tmp_s, iter_begin=0, iter_count=n, **tmp_cfg)
+    stage("clock warm")
     clock_warm(args.clock_warm_ms, dev, scratch)
+    stage("clock warm done")
     if scratch is not None:
         check(tmp, "clock warm")
         del tmp, tmp_s
@@ -604,11 +623,14 @@ def main():
         chains.state.copy_(saved)   # the measured chains start from their initial state
         torch.cuda.synchronize()
         del saved
+    stage("restored")
     # ---- untimed warmup (step-size adaptation) -------------------------------
     for it0, n in launches(0, Wm):
         chains.run_hmc(samples=samples, iter_begin=it0, iter_count=n, **cfg)
     torch.cuda.synchronize()
+    stage("warmup done")
     check(chains, "warmup")
+    stage("checked")
 
     # ---- timed region: K steps in launches of B ---------------------------------
     stream = torch.cuda.current_stream()
@@ -618,6 +640,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    stage("t0")
     t0 = time.perf_counter()
     for (it0, n), (e0, e1) in zip(timed, ev):
         e0.record(stream)
@@ -627,6 +650,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    stage("t1")
+    print_stages()
     check(chains, "timed region")
     # kernel time per launch from the largest launches of the timed region
     # (HIP events on the launch stream): a run of K < B iterations is one

@@ -121,3 +121,68 @@ def test_product_fails_loudly_without_a_device():
               num_warmup=5, progress=False)
     with pytest.raises(_lib.EngineUnavailable):
         m.Normal(0, 1).log_prob(0.0)
+
+
+def _expr_program(nodes, n=3, n_params=4, index=None, via_affine=False):
+    """mc_program_create_expr on one expression term (host-side validation
+    only: every case below fails before any device allocation)."""
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    terms = (_lib.McTerm * 1)()
+    terms[0].dist = _lib.MC_DIST_EXPR
+    terms[0].n = n
+    terms[0].weight = 1.0
+    terms[0].affine = 1
+    exprs = (_lib.McExpr * 1)()
+    exprs[0].first, exprs[0].count = 0, len(nodes)
+    carr = (_lib.McExprNode * max(1, len(nodes)))()
+    for k, (op, a, b, c, leaf) in enumerate(nodes):
+        carr[k].op, carr[k].a, carr[k].b, carr[k].c = op, a, b, c
+        if leaf:
+            for f, v in leaf.items():
+                setattr(carr[k].leaf, f, v)
+    data = np.arange(3, dtype=np.float32)
+    idx = np.asarray(index if index is not None else [0, 0, 1], np.int32)
+    dp, ip = data.ctypes.data_as(ctypes.c_void_p), idx.ctypes.data_as(ctypes.c_void_p)
+    if via_affine:
+        return lib.mc_program_create_affine(terms, 1, None, 0, n_params, 0.0, dp, 3, ip,
+                                            idx.size, ctypes.byref(h)), lib.mc_last_error()
+    rc = lib.mc_program_create_expr(terms, 1, None, 0, exprs, 1, carr, len(nodes), n_params, 0.0,
+                                    dp, 3, ip, idx.size, ctypes.byref(h))
+    return rc, lib.mc_last_error()
+
+
+P0 = {"kind": _lib.MC_OP_PSCALAR, "param_offset": 0}
+DATA = {"kind": _lib.MC_OP_DATA, "pool_offset": 0}
+L, E = _lib.MC_EX_LEAF, _lib
+
+
+@pytest.mark.parametrize("nodes,code,msg", [
+    ([(L, -1, -1, -1, P0), (E.MC_EX_ADD, 0, -1, -1, None)], _lib.MC_ERR_INVALID,
+     b"bad arguments"),                                                   # missing operand
+    ([(L, -1, -1, -1, P0), (E.MC_EX_EXP, 1, -1, -1, None)], _lib.MC_ERR_INVALID,
+     b"bad arguments"),                                                   # forward reference
+    ([(L, -1, -1, -1, P0), (99, 0, -1, -1, None)], _lib.MC_ERR_INVALID, b"unknown op"),
+    ([(L, -1, -1, -1, dict(P0, transform=_lib.MC_XF_EXP))], _lib.MC_ERR_INVALID,
+     b"no transform"),
+    ([(L, -1, -1, -1, {"kind": _lib.MC_OP_PSCALAR, "param_offset": 9})], _lib.MC_ERR_INVALID,
+     b"out of range"),
+    ([(L, -1, -1, -1, P0), (L, -1, -1, -1, DATA), (E.MC_EX_WHERE, 0, 1, 1, None)],
+     _lib.MC_ERR_UNSUPPORTED, b"where mask"),                            # traced mask
+    ([(L, -1, -1, -1, P0)] * 33, _lib.MC_ERR_UNSUPPORTED, b"1 .. 32 nodes"),
+])
+def test_expression_validation(nodes, code, msg):
+    rc, err = _expr_program(nodes)
+    assert rc == code and msg in err, (rc, err)
+
+
+def test_expression_validation_gathers_and_entry_points():
+    g0 = {"kind": _lib.MC_OP_GATHER, "param_offset": 0, "pool_offset": 0}
+    g1 = {"kind": _lib.MC_OP_GATHER, "param_offset": 0, "pool_offset": 3}
+    # two non-injective gathers through different index values
+    rc, err = _expr_program([(L, -1, -1, -1, g0), (L, -1, -1, -1, g1),
+                             (E.MC_EX_MUL, 0, 1, -1, None)], index=[0, 0, 1, 1, 1, 0])
+    assert rc == _lib.MC_ERR_UNSUPPORTED and b"two different non-injective" in err
+    # expression terms only through mc_program_create_expr
+    rc, err = _expr_program([(L, -1, -1, -1, P0)], via_affine=True)
+    assert rc == _lib.MC_ERR_INVALID and b"mc_program_create_expr" in err
