@@ -858,18 +858,21 @@ MC_DEV void ex_bwd(int op, float x, float y, float z, float v, float c, float c0
 // the run.  Vector leaves deposit in their pass only (sweeps separated by a
 // group barrier: deterministic, no atomics); broadcast (PSCALAR) leaves sum
 // per thread and flush to their cotangent slots after pass 0.
-// (not inlined: the node / adjoint arrays would otherwise raise the register
-// count of every tape kernel, expression program or not)
-template <int WPC, bool VALUE_ONLY>
-__device__ __attribute__((noinline)) void eval_expr(const DevTerm& T, const DevCtx& P,
-                                                    const float* q, float* g,
-                                                    const Group<WPC>& G, bool task, int tid,
-                                                    int nthr, float& lp_acc) {
+// NMAX: the node arrays' size.  Terms of <= 16 nodes run the NMAX = 16
+// instantiation inlined into the (EX) kernel, whose value / adjoint /
+// partial arrays the compiler keeps in registers (uniform dynamic indices:
+// indirect register moves); larger terms run NMAX = 32 in a called function,
+// whose arrays live in scratch memory (an order of magnitude slower per node:
+// every argument read waits for a scratch load; the promotion to registers
+// is not done for called functions, nor affordable at 3 x 32 VGPRs).
+template <int WPC, bool VALUE_ONLY, int NMAX>
+MC_DEV void eval_expr_n(const DevTerm& T, const DevCtx& P, const float* q, float* g,
+                        const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc) {
     const MC_CONST DevExprNode* N = cptr(P.nodes) + T.expr_base;
     const int nn = T.expr_n;
     const float w = T.weight;
     const bool seg = T.primary >= 0;
-    float val[kExMaxNodes], adj[kExMaxNodes], part[kExMaxNodes];
+    float val[NMAX], adj[NMAX], part[NMAX];
     const int npass = VALUE_ONLY ? 1 : T.npass;
     for (int pass = 0; pass < npass; ++pass) {
         for (int k = 0; k < nn; ++k) part[k] = 0.0f;
@@ -961,6 +964,25 @@ __device__ __attribute__((noinline)) void eval_expr(const DevTerm& T, const DevC
         }
         if (!VALUE_ONLY && pass + 1 < npass) G.sync();
     }
+}
+
+template <int WPC, bool VALUE_ONLY>
+__device__ __attribute__((noinline)) void eval_expr_big(const DevTerm& T, const DevCtx& P,
+                                                        const float* q, float* g,
+                                                        const Group<WPC>& G, bool task,
+                                                        int tid, int nthr, float& lp_acc) {
+    eval_expr_n<WPC, VALUE_ONLY, kExMaxNodes>(T, P, q, g, G, task, tid, nthr, lp_acc);
+}
+
+// (only in the EX kernel instantiations: the node arrays would otherwise
+// raise the register count of every tape kernel)
+template <int WPC, bool VALUE_ONLY>
+MC_DEV void eval_expr(const DevTerm& T, const DevCtx& P, const float* q, float* g,
+                      const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc) {
+    if (T.expr_n <= 16)
+        eval_expr_n<WPC, VALUE_ONLY, 16>(T, P, q, g, G, task, tid, nthr, lp_acc);
+    else
+        eval_expr_big<WPC, VALUE_ONLY>(T, P, q, g, G, task, tid, nthr, lp_acc);
 }
 
 // ---------------------------------------------------------------------------
