@@ -861,10 +861,9 @@ MC_DEV void ex_bwd(int op, float x, float y, float z, float v, float c, float c0
 // NMAX: the node arrays' size.  Terms of <= 16 nodes run the NMAX = 16
 // instantiation inlined into the (EX) kernel, whose value / adjoint /
 // partial arrays the compiler keeps in registers (uniform dynamic indices:
-// indirect register moves); larger terms run NMAX = 32 in a called function,
-// whose arrays live in scratch memory (an order of magnitude slower per node:
-// every argument read waits for a scratch load; the promotion to registers
-// is not done for called functions, nor affordable at 3 x 32 VGPRs).
+// indirect register moves); larger terms run NMAX = 32, whose arrays live in
+// scratch memory (slower per node: every argument read waits for a scratch
+// load; 3 x 32 VGPRs are not affordable).
 template <int WPC, bool VALUE_ONLY, int NMAX>
 MC_DEV void eval_expr_n(const DevTerm& T, const DevCtx& P, const float* q, float* g,
                         const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc) {
@@ -966,23 +965,17 @@ MC_DEV void eval_expr_n(const DevTerm& T, const DevCtx& P, const float* q, float
     }
 }
 
-template <int WPC, bool VALUE_ONLY>
-__device__ __attribute__((noinline)) void eval_expr_big(const DevTerm& T, const DevCtx& P,
-                                                        const float* q, float* g,
-                                                        const Group<WPC>& G, bool task,
-                                                        int tid, int nthr, float& lp_acc) {
-    eval_expr_n<WPC, VALUE_ONLY, kExMaxNodes>(T, P, q, g, G, task, tid, nthr, lp_acc);
-}
-
 // (only in the EX kernel instantiations: the node arrays would otherwise
-// raise the register count of every tape kernel)
+// raise the register count of every tape kernel.  Both variants are inlined:
+// a call in a kernel turned every uniform branch of it into an exec-masked
+// one — all 19 op cases of every node executed for every element, 20x slower)
 template <int WPC, bool VALUE_ONLY>
 MC_DEV void eval_expr(const DevTerm& T, const DevCtx& P, const float* q, float* g,
                       const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc) {
     if (T.expr_n <= 16)
         eval_expr_n<WPC, VALUE_ONLY, 16>(T, P, q, g, G, task, tid, nthr, lp_acc);
     else
-        eval_expr_big<WPC, VALUE_ONLY>(T, P, q, g, G, task, tid, nthr, lp_acc);
+        eval_expr_n<WPC, VALUE_ONLY, kExMaxNodes>(T, P, q, g, G, task, tid, nthr, lp_acc);
 }
 
 // ---------------------------------------------------------------------------
