@@ -2102,6 +2102,21 @@ static TraceDev trace_of(const mc_trace* t) {
     return d;
 }
 
+// The instantiation of a chain-per-workgroup launcher for a program: waves
+// per chain (1, 4 or 8), LDS arena or not, expression terms or not (EX).
+template <typename F>
+static int dispatch_tape(const mc_program* p, bool lds, F&& f) {
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    auto ex = [&](auto w, auto l) { return p->ex ? f(w, l, T_{}) : f(w, l, F_{}); };
+    auto arena = [&](auto w) { return lds ? ex(w, T_{}) : ex(w, F_{}); };
+    switch (p->wpc) {
+        case 1: return arena(std::integral_constant<int, 1>{});
+        case 4: return arena(std::integral_constant<int, 4>{});
+        default: return arena(std::integral_constant<int, 8>{});
+    }
+}
+
 // ---------------------------------------------------------------------------
 // batched log density + gradient
 // ---------------------------------------------------------------------------
@@ -2650,14 +2665,10 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
         return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
     hipStream_t st = (hipStream_t)stream;
     float* w = (float*)ws;
-    switch (p->wpc) {
-        case 1: return lds ? (p->ex ? launch_hmc<1, true, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<1, true, false>(p, cfg, state, samples, tr, w, st))
-                           : (p->ex ? launch_hmc<1, false, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<1, false, false>(p, cfg, state, samples, tr, w, st));
-        case 4: return lds ? (p->ex ? launch_hmc<4, true, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<4, true, false>(p, cfg, state, samples, tr, w, st))
-                           : (p->ex ? launch_hmc<4, false, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<4, false, false>(p, cfg, state, samples, tr, w, st));
-        default: return lds ? (p->ex ? launch_hmc<8, true, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<8, true, false>(p, cfg, state, samples, tr, w, st))
-                            : (p->ex ? launch_hmc<8, false, true>(p, cfg, state, samples, tr, w, st) : launch_hmc<8, false, false>(p, cfg, state, samples, tr, w, st));
-    }
+    return dispatch_tape(p, lds, [&](auto W, auto L, auto E) {
+        return launch_hmc<decltype(W)::value, decltype(L)::value, decltype(E)::value>(
+            p, cfg, state, samples, tr, w, st);
+    });
 }
 
 // ---- Metropolis-Hastings (metropolis.py:6-101) --------------------------------
@@ -2711,14 +2722,10 @@ extern "C" int mc_mh_run(const mc_program* p, const mc_run_config* cfg, double p
     hipStream_t st = (hipStream_t)stream;
     float* w = (float*)ws;
     const float sc = (float)proposal_scale;  // f32(proposal_scale): MLX's weak scalar
-    switch (p->wpc) {
-        case 1: return lds ? (p->ex ? launch_mh<1, true, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<1, true, false>(p, cfg, sc, state, samples, tr, w, st))
-                           : (p->ex ? launch_mh<1, false, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<1, false, false>(p, cfg, sc, state, samples, tr, w, st));
-        case 4: return lds ? (p->ex ? launch_mh<4, true, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<4, true, false>(p, cfg, sc, state, samples, tr, w, st))
-                           : (p->ex ? launch_mh<4, false, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<4, false, false>(p, cfg, sc, state, samples, tr, w, st));
-        default: return lds ? (p->ex ? launch_mh<8, true, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<8, true, false>(p, cfg, sc, state, samples, tr, w, st))
-                            : (p->ex ? launch_mh<8, false, true>(p, cfg, sc, state, samples, tr, w, st) : launch_mh<8, false, false>(p, cfg, sc, state, samples, tr, w, st));
-    }
+    return dispatch_tape(p, lds, [&](auto W, auto L, auto E) {
+        return launch_mh<decltype(W)::value, decltype(L)::value, decltype(E)::value>(
+            p, cfg, sc, state, samples, tr, w, st);
+    });
 }
 
 // LDS floats per chain group of k_nuts: group scratch, pending words and,
@@ -2877,14 +2884,10 @@ extern "C" int mc_nuts_run(const mc_program* p, const mc_run_config* cfg, void* 
     }
     float* w = (float*)ws;
     const bool lds = nuts_use_lds(p, cfg->max_tree_depth);
-    switch (p->wpc) {
-        case 1: return lds ? (p->ex ? launch_nuts<1, true, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<1, true, false>(p, cfg, state, samples, tr, w, st))
-                           : (p->ex ? launch_nuts<1, false, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<1, false, false>(p, cfg, state, samples, tr, w, st));
-        case 4: return lds ? (p->ex ? launch_nuts<4, true, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<4, true, false>(p, cfg, state, samples, tr, w, st))
-                           : (p->ex ? launch_nuts<4, false, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<4, false, false>(p, cfg, state, samples, tr, w, st));
-        default: return lds ? (p->ex ? launch_nuts<8, true, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<8, true, false>(p, cfg, state, samples, tr, w, st))
-                            : (p->ex ? launch_nuts<8, false, true>(p, cfg, state, samples, tr, w, st) : launch_nuts<8, false, false>(p, cfg, state, samples, tr, w, st));
-    }
+    return dispatch_tape(p, lds, [&](auto W, auto L, auto E) {
+        return launch_nuts<decltype(W)::value, decltype(L)::value, decltype(E)::value>(
+            p, cfg, state, samples, tr, w, st);
+    });
 }
 
 // ---------------------------------------------------------------------------
