@@ -1,8 +1,9 @@
 """One HMC launch of the N = 100 K affine regression (and of the same
 likelihood as an expression term) for rocprofv3 counter passes: what bounds
 the chain-per-workgroup tape at large N."""
+import os
 import sys
-sys.path[:0] = ["."]
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__)))]
 import numpy as np
 import torch
 import mlx_mcmc_amd as m
