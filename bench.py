@@ -3,7 +3,8 @@
 Workload (BASELINE.json configs[2], SURVEY §8d "Large"): hierarchical Normal,
 D = 1000 parameters (theta[997], mu, tau, sigma), N = 100,000 observations,
 HMC with L = 20 leapfrog steps, 256 chains per GPU (configs[3] at N = 8: 2048
-chains, 256/GPU; ESS and R-hat reduced over RCCL as [2, D] moment blocks).
+chains, 256/GPU; ESS sums and split R-hat over every rank's chains from
+[2, D] f64 moment blocks all-reduced over RCCL, diagnostics.chain_diagnostics).
 One *step* = one HMC iteration of every chain (L leapfrog steps, fused
 gradient tape, accept, sample store) inside the persistent sampler kernel,
 which is launched in chunks of --iters-per-launch iterations (default 50).
@@ -75,8 +76,8 @@ def parse():
                          "worker counts as, this one included; 0: skip)")
     ap.add_argument("--no-ess", action="store_true")
     ap.add_argument("--ess-draws", type=int, default=5000,
-                    help="draws of the converged-ESS run (N=1, untimed by the headline: fixed "
-                         "eps, R-hat checked); 0: skip")
+                    help="draws of the converged-ESS run (every rank runs its shard of the global "
+                         "chains; untimed by the headline: fixed eps, R-hat checked); 0: skip")
     ap.add_argument("--ess-warmup", type=int, default=1000)
     ap.add_argument("--ess-step-size", type=float, default=None,
                     help="fixed step size of the converged-ESS run (default: the posterior "
@@ -259,24 +260,31 @@ def pmc_traffic(shape, iters_per_launch):
 def ess_block(samples, accept_n, K, elapsed):
     """ESS/s over the timed draws (reference rule, examples/06_nuts_comparison.py:22-41,
     summed over chains) — published only from chains that moved, with at least
-    100 draws and split R-hat max <= 1.1; otherwise null with the reason."""
+    100 draws and split R-hat max <= 1.1; otherwise null with the reason.
+    Under torch.distributed every rank passes its own shard: the per-element
+    moment blocks are all-reduced (diagnostics.chain_diagnostics), so the
+    result covers every rank's moving chains and every rank takes the same
+    branch; `elapsed` is the max-over-ranks wall time."""
     import numpy as np
     import torch
 
     from mlx_mcmc_amd.diagnostics import chain_diagnostics
+    from mlx_mcmc_amd.distributed import sum_over_ranks
 
     moving = np.nonzero(accept_n > 0)[0]
-    out = {"draws": K, "chains_used": int(moving.size), "frozen_chains": int(accept_n.size - moving.size)}
+    n_moving = int(sum_over_ranks(float(moving.size), device=samples.device))
+    n_all = int(sum_over_ranks(float(accept_n.size), device=samples.device))
+    out = {"draws": K, "chains_used": n_moving, "frozen_chains": n_all - n_moving}
     if K < 100:
         out["ess_per_sec"] = None
         out["ess_null_reason"] = f"{K} timed draws < 100"
         return out
-    if moving.size < 2:
+    if n_moving < 2:
         out["ess_per_sec"] = None
         out["ess_null_reason"] = "fewer than two chains accepted a proposal"
         return out
     idx = torch.from_numpy(moving).to(samples.device)
-    d = chain_diagnostics(samples[:, :K, :].index_select(0, idx), group=False)
+    d = chain_diagnostics(samples[:, :K, :].index_select(0, idx))
     rh = d["rhat"]
     out["rhat"] = {"max": float(np.nanmax(rh)), "median": float(np.nanmedian(rh)), "split": True}
     if d["n_constant"] or not np.isfinite(rh).all() or np.nanmax(rh) > 1.1:
@@ -292,47 +300,67 @@ def ess_block(samples, accept_n, K, elapsed):
         return out
     out["ess_per_sec"] = {"min": float(d["ess_sum"].min()) / elapsed,
                           "median": float(np.median(d["ess_sum"])) / elapsed,
-                          "unit": "effective samples/s (sum over moving chains)"}
+                          "unit": "effective samples/s (sum over moving chains of every rank)"}
     return out
 
 
-def converged_ess(prog, C, q0, dev, L, args):
+def converged_ess(prog, C, q0, dev, L, args, chain_offset=0, world=1):
     """ESS/s where the draws are from the posterior: the same kernel, model and
     chain count at the fixed step size of the posterior tests (eps = 2e-3,
     tests/test_gpu_posterior_exact.py: accept ~0.98), W = --ess-warmup,
     S = --ess-draws sampling iterations timed; reported only with split R-hat
     max <= 1.1.  ESS/s over the sampling seconds and over warmup + sampling
-    (SURVEY 8d)."""
+    (SURVEY 8d).  Multi-rank: rank r runs its shard of the global chains
+    (chain_offset), the phases are bracketed by barriers and timed as the max
+    over ranks, and ESS sums / R-hat come from the all-reduced moment blocks —
+    so the line equals a one-rank run over the same global chains up to the
+    f64 summation order."""
     import numpy as np
     import torch
+    import torch.distributed as dist
 
     from mlx_mcmc_amd import _engine
     from mlx_mcmc_amd.diagnostics import chain_diagnostics
+    from mlx_mcmc_amd.distributed import max_over_ranks
 
     S, Wm, eps = args.ess_draws, args.ess_warmup, args.ess_step_size
     chains = _engine.ChainSet(prog, C, q0, eps, device=dev)
     samples = torch.empty((C, S, prog.D), dtype=torch.float32, device=dev)
-    cfg = dict(chain_offset=0, num_warmup=Wm, num_samples=S, sample_begin=0, sample_capacity=S,
-               seed=args.seed + 1, step_size=eps, target_accept=0.8, num_leapfrog_steps=L,
-               adapt_step_size=False)
-    torch.cuda.synchronize()
+    cfg = dict(chain_offset=chain_offset, num_warmup=Wm, num_samples=S, sample_begin=0,
+               sample_capacity=S, seed=args.seed + 1, step_size=eps, target_accept=0.8,
+               num_leapfrog_steps=L, adapt_step_size=False)
+
+    def sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    sync()
     t0 = time.perf_counter()
     for it0 in range(0, Wm, 500):
         chains.run_hmc(samples=samples, iter_begin=it0, iter_count=min(500, Wm - it0), **cfg)
-    torch.cuda.synchronize()
+    sync()
     t1 = time.perf_counter()
     for it0 in range(Wm, Wm + S, 500):
         chains.run_hmc(samples=samples, iter_begin=it0, iter_count=min(500, Wm + S - it0), **cfg)
-    torch.cuda.synchronize()
+    sync()
     t2 = time.perf_counter()
     check(chains, "converged-ESS run")
+    warm_s = max_over_ranks(t1 - t0, device=dev)
+    samp_s = max_over_ranks(t2 - t1, device=dev)
     sc = chains.scalars()
-    d = chain_diagnostics(samples, group=False)
+    acc = np.array([np.sum(sc["n_accept"]), np.sum(sc["n_total"])], np.float64)
+    if world > 1:
+        from mlx_mcmc_amd.distributed import sum_over_ranks
+
+        acc = np.array([sum_over_ranks(float(v), device=dev) for v in acc])
+    d = chain_diagnostics(samples)
     rh = d["rhat"]
-    out = {"step_size": eps, "warmup": Wm, "draws": S, "chains": C,
-           "accept_rate": float(np.mean(sc["n_accept"] / np.maximum(sc["n_total"], 1))),
-           "sampling_s": t2 - t1, "warmup_s": t1 - t0,
+    out = {"step_size": eps, "warmup": Wm, "draws": S, "chains": C * world,
+           "accept_rate": float(acc[0] / max(acc[1], 1.0)),
+           "sampling_s": samp_s, "warmup_s": warm_s,
            "rhat": {"max": float(np.nanmax(rh)), "median": float(np.nanmedian(rh)), "split": True}}
+    t0, t1, t2 = 0.0, warm_s, warm_s + samp_s
     if d["n_constant"] or not np.isfinite(rh).all() or np.nanmax(rh) > 1.1:
         out["ess_per_sec"] = None
         out["ess_null_reason"] = f"split R-hat max {np.nanmax(rh):.3g} > 1.1"
@@ -349,7 +377,9 @@ def converged_ess(prog, C, q0, dev, L, args):
                               "median": float(np.median(e)) / (t2 - t1),
                               "min_over_warmup_and_sampling": float(e.min()) / (t2 - t0),
                               "unit": "effective samples/s (sum over chains, reference rule)"}
-        out["ess_sum"] = {"min": float(e.min()), "median": float(np.median(e))}
+        out["ess_sum"] = {"min": float(e.min()), "median": float(np.median(e)),
+                          "total": float(np.sum(e))}
+        out["rhat"]["mean"] = float(np.nanmean(rh))
     del chains, samples
     return out
 
@@ -675,13 +705,15 @@ def main():
     # timed draws of the chains that moved (ess_block says when it is null)
     ess = None
     diag_ms = None
-    if not args.no_ess and K >= 1 and world == 1:
+    # (every rank takes part: the moment blocks are all-reduced over RCCL)
+    if not args.no_ess and K >= 1:
         td = time.perf_counter()
         ess = ess_block(samples, sc["n_accept"], K, elapsed)
         diag_ms = (time.perf_counter() - td) * 1e3
     ess_conv = None
-    if not args.no_ess and world == 1 and args.ess_draws > 0:
-        ess_conv = converged_ess(prog, C, prog.layout.flatten(init), dev, L, args)
+    if not args.no_ess and args.ess_draws > 0:
+        ess_conv = converged_ess(prog, C, prog.layout.flatten(init), dev, L, args,
+                                 chain_offset=chain_offset, world=world)
     gather_ms = None
     if world > 1 and args.gather:
         tg = time.perf_counter()

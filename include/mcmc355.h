@@ -52,7 +52,10 @@
 extern "C" {
 #endif
 
-#define MC_ABI_VERSION 1
+/* ABI 2: mc_operand.transform (formerly `reserved`) and mc_term.affine are
+ * read and validated (an unknown transform, or a transform on a non-parameter
+ * operand, is MC_ERR_INVALID): callers written against ABI 1 must zero them. */
+#define MC_ABI_VERSION 2
 
 /* ---- error codes -------------------------------------------------------- */
 #define MC_OK              0

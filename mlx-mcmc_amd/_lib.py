@@ -265,7 +265,7 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.mc_abi_version() != 1:
+    if lib.mc_abi_version() != 2:
         raise EngineUnavailable("libmcmc355.so ABI version mismatch")
     _lib = lib
     return lib

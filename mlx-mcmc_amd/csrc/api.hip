@@ -1389,8 +1389,11 @@ extern "C" int mc_program_create_affine(const mc_term* terms, int32_t n_terms,
 // vector leaves with overlapping parameter ranges deposit in different passes.
 static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, int32_t n_exprs,
                            const mc_expr_node* nodes, int32_t n_nodes, int32_t n_params,
-                           std::vector<float>& dpool, std::vector<int32_t>& ipool,
-                           std::vector<DevExprNode>& gnodes, DevTerm& dt, int wpc) {
+                           int64_t n_data, int64_t n_index, std::vector<float>& dpool,
+                           std::vector<int32_t>& ipool, std::vector<DevExprNode>& gnodes,
+                           DevTerm& dt, int wpc) {
+    // (leaf ranges are checked against the caller's pools, n_data / n_index:
+    // dpool / ipool already hold the library's own tiled copies of earlier terms)
     if (src.affine < 1 || src.affine > n_exprs)
         return fail(MC_ERR_INVALID, "term %d: expression index %d out of range", t, src.affine);
     if (src.value.kind != MC_OP_NONE || src.loc.kind != MC_OP_NONE || src.scale.kind != MC_OP_NONE)
@@ -1437,7 +1440,7 @@ static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, 
                                     o.param_offset);
                     break;
                 case MC_OP_DATA:
-                    if (o.pool_offset < 0 || o.pool_offset + n > (int64_t)dpool.size())
+                    if (o.pool_offset < 0 || o.pool_offset + n > n_data)
                         return fail(MC_ERR_INVALID, "term %d node %d: data range out of pool", t, k);
                     break;
                 case MC_OP_PVEC:
@@ -1446,7 +1449,7 @@ static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, 
                                     k);
                     break;
                 case MC_OP_GATHER: {
-                    if (o.pool_offset < 0 || o.pool_offset + n > (int64_t)ipool.size())
+                    if (o.pool_offset < 0 || o.pool_offset + n > n_index)
                         return fail(MC_ERR_INVALID, "term %d node %d: index range out of pool", t,
                                     k);
                     std::vector<int32_t> v(ipool.begin() + o.pool_offset,
@@ -1545,6 +1548,8 @@ static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, 
             pr[placed].push_back({lo, hi});
             d.pass = placed;
         }
+        if (pr.size() > 16)
+            return fail(MC_ERR_UNSUPPORTED, "term %d: more than 16 overlapping vector leaves", t);
         dt.npass = std::max<int>(1, (int)pr.size());
     }
     if (prim_pool >= 0) {
@@ -1636,8 +1641,8 @@ extern "C" int mc_program_create_expr(const mc_term* terms, int32_t n_terms,
         DevTerm dt;
         std::memset(&dt, 0, sizeof(dt));
         if (src.dist == MC_DIST_EXPR) {
-            const int rc = build_expr_term(t, src, exprs, n_exprs, nodes, n_nodes, n_params, dpool,
-                                           ipool, gnodes, dt, wpc);
+            const int rc = build_expr_term(t, src, exprs, n_exprs, nodes, n_nodes, n_params,
+                                           n_data, n_index, dpool, ipool, gnodes, dt, wpc);
             if (rc) return rc;
             raws.push_back(dt);
             dts.push_back(dt);
@@ -2599,9 +2604,11 @@ extern "C" int mc_workspace_status(const mc_program* p, const void* ws, int64_t 
 
 extern "C" int64_t mc_hmc_workspace_bytes(const mc_program* p, int64_t C) {
     if (!p || C < 0) return -1;
-    if (sliced(p)) return sl_workspace_bytes(p, C);
-    // (a lanes1 program runs L = 0 configurations on the unsliced kernel)
-    const int64_t x = lanes1(p) ? sl_workspace_bytes(p, C) : 0;
+    // (a lanes1 program runs L = 0 configurations on the unsliced kernel, and
+    // so does a sliced program with transformed operands, which the term
+    // interpreter does not take: mc_hmc_run)
+    const int64_t x = (lanes1(p) || sliced(p)) ? sl_workspace_bytes(p, C) : 0;
+    if (sliced(p) && !has_transform(p)) return x;
     if (hmc_use_lds(p)) return x;
     return std::max(x, C * 5 * (int64_t)dpad_of(p->D) * 4);
 }
@@ -2635,7 +2642,10 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
     if (rc) return rc;
     if (cfg->num_leapfrog_steps < 0) return fail(MC_ERR_INVALID, "num_leapfrog_steps < 0");
     if (cfg->num_chains == 0 || cfg->iter_count == 0) return MC_OK;
-    if (sliced(p) || (lanes1(p) && use_lanes(p, cfg))) {
+    // L = 0 with transformed operands: the interpreter (k_hmc_sl) declines
+    // them, so such a run takes the chain-per-workgroup tape (as lanes1 does)
+    const bool sl_tape = sliced(p) && !use_lanes(p, cfg) && has_transform(p);
+    if ((sliced(p) && !sl_tape) || (lanes1(p) && use_lanes(p, cfg))) {
         const int64_t need = sl_workspace_bytes(p, cfg->num_chains);
         if (ws == nullptr || ws_bytes < need)
             return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);

@@ -872,34 +872,61 @@ MC_DEV void eval_expr_n(const DevTerm& T, const DevCtx& P, const float* q, float
     const float w = T.weight;
     const bool seg = T.primary >= 0;
     float val[NMAX], adj[NMAX], part[NMAX];
+    // the node descriptors, read once per term: lane k of these registers
+    // holds node k (packed op / arguments / flags, leaf offsets, constant);
+    // a node visit reads them with readlane into SGPRs (re-reading them from
+    // constant memory per node and element cost ~20 scalar loads per element)
+    int dcode = 0, dpoff = 0, dpool = 0;
+    float dcval = 0.0f;
+    {
+        const int ln = G.tid & 63;
+        if (ln < nn) {
+            const MC_CONST DevExprNode* d = N + ln;
+            dcode = (d->op & 31) | ((d->a + 1) << 5) | ((d->b + 1) << 11) | ((d->c + 1) << 17) |
+                    ((d->prim & 1) << 23) | ((d->pass & 15) << 24) | ((d->leaf.kind & 7) << 28);
+            dpoff = d->leaf.poff;
+            dpool = (int)d->leaf.pool;
+            dcval = d->leaf.cval;
+        }
+    }
+    auto code = [&](int k) { return __builtin_amdgcn_readlane(dcode, k); };
+    auto cop = [](int d) { return d & 31; };
+    auto carg = [](int d, int sh) { return ((d >> sh) & 63) - 1; };
+    auto cprim = [](int d) { return ((d >> 23) & 1) != 0; };
+    auto cpass = [](int d) { return (d >> 24) & 15; };
+    auto ckind = [](int d) { return (d >> 28) & 7; };
+    auto cval_of = [&](int k) {
+        return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dcval), k));
+    };
     const int npass = VALUE_ONLY ? 1 : T.npass;
     for (int pass = 0; pass < npass; ++pass) {
         for (int k = 0; k < nn; ++k) part[k] = 0.0f;
         // element e (strided index, or tiled position), run parameter kr
         auto element = [&](int64_t e, int kr) {
             for (int k = 0; k < nn; ++k) {
-                const int op = N[k].op;
+                const int d = code(k);
+                const int op = cop(d);
                 float v;
                 if (op == MC_EX_LEAF) {
-                    const int kind = N[k].leaf.kind;
-                    const int poff = N[k].leaf.poff;
-                    if (N[k].prim) {
+                    const int kind = ckind(d);
+                    const int poff = __builtin_amdgcn_readlane(dpoff, k);
+                    if (cprim(d)) {
                         v = q[poff + kr];
                     } else if (kind == MC_OP_CONST) {
-                        v = N[k].leaf.cval;
+                        v = cval_of(k);
                     } else if (kind == MC_OP_PSCALAR) {
                         v = q[poff];
                     } else if (kind == MC_OP_DATA) {
-                        v = P.data[N[k].leaf.pool + e];
+                        v = P.data[__builtin_amdgcn_readlane(dpool, k) + e];
                     } else if (kind == MC_OP_PVEC) {
                         v = q[poff + e];
                     } else {
-                        v = q[poff + P.index[N[k].leaf.pool + e]];
+                        v = q[poff + P.index[__builtin_amdgcn_readlane(dpool, k) + e]];
                     }
                 } else {
-                    const int a = N[k].a, b = N[k].b, c = N[k].c;
+                    const int a = carg(d, 5), b = carg(d, 11), c = carg(d, 17);
                     v = ex_fwd(op, val[a], b >= 0 ? val[b] : 0.0f, c >= 0 ? val[c] : 0.0f,
-                               N[k].leaf.cval);
+                               cval_of(k));
                 }
                 val[k] = v;
             }
@@ -909,24 +936,26 @@ MC_DEV void eval_expr_n(const DevTerm& T, const DevCtx& P, const float* q, float
             adj[nn - 1] = w;
             for (int k = nn - 1; k >= 0; --k) {
                 const float ck = adj[k];
-                const int op = N[k].op;
+                const int d = code(k);
+                const int op = cop(d);
                 if (op == MC_EX_LEAF) {
-                    const int kind = N[k].leaf.kind;
-                    if (kind == MC_OP_PSCALAR || N[k].prim) {
+                    const int kind = ckind(d);
+                    if (kind == MC_OP_PSCALAR || cprim(d)) {
                         part[k] += ck;
-                    } else if ((kind == MC_OP_PVEC || kind == MC_OP_GATHER) && N[k].pass == pass) {
-                        const int poff = N[k].leaf.poff;
-                        const int64_t j = kind == MC_OP_PVEC
-                                              ? (int64_t)poff + e
-                                              : (int64_t)poff + P.index[N[k].leaf.pool + e];
+                    } else if ((kind == MC_OP_PVEC || kind == MC_OP_GATHER) && cpass(d) == pass) {
+                        const int poff = __builtin_amdgcn_readlane(dpoff, k);
+                        const int64_t j =
+                            kind == MC_OP_PVEC
+                                ? (int64_t)poff + e
+                                : (int64_t)poff + P.index[__builtin_amdgcn_readlane(dpool, k) + e];
                         g[j] += ck;
                     }
                     continue;
                 }
-                const int a = N[k].a, b = N[k].b, c = N[k].c;
+                const int a = carg(d, 5), b = carg(d, 11), c = carg(d, 17);
                 float dx, dy, dz;
                 ex_bwd(op, val[a], b >= 0 ? val[b] : 0.0f, c >= 0 ? val[c] : 0.0f, val[k], ck,
-                       N[k].leaf.cval, dx, dy, dz);
+                       cval_of(k), dx, dy, dz);
                 adj[a] += dx;
                 if (b >= 0) adj[b] += dy;
                 if (c >= 0) adj[c] += dz;

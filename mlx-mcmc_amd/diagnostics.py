@@ -109,9 +109,13 @@ def chain_diagnostics(samples, max_lag: int = MAX_LAG, group=None) -> Dict[str, 
     C, S, D = x.shape
     lib = _lib.load()
     stream = _lib.stream_handle()
-    st = series_stats(x, max_lag)
-    red = torch.empty((2, D), dtype=torch.float64, device=x.device)
-    _lib.check(lib.mc_stats_reduce(C, S, D, _lib.ptr(st), None, 0, _lib.ptr(red), stream))
+    # a rank whose shard holds no chain (e.g. every one of its chains was
+    # left out as frozen) still joins the all-reduces with zero blocks
+    st = series_stats(x, max_lag) if C > 0 else torch.zeros(
+        (_lib.MC_ST_COUNT, 0), dtype=torch.float64, device=x.device)
+    red = torch.zeros((2, D), dtype=torch.float64, device=x.device)
+    if C > 0:
+        _lib.check(lib.mc_stats_reduce(C, S, D, _lib.ptr(st), None, 0, _lib.ptr(red), stream))
     # [split chains, constant series]: a constant series scores ESS = n by
     # the reference rule, so callers need to know how many there are
     counts = torch.stack([torch.tensor(2.0 * C, dtype=torch.float64, device=x.device),
@@ -124,9 +128,10 @@ def chain_diagnostics(samples, max_lag: int = MAX_LAG, group=None) -> Dict[str, 
     m = m_total
     if S >= 4 and m >= 2:
         center = red[0].contiguous()
-        spread = torch.empty((2, D), dtype=torch.float64, device=x.device)
-        _lib.check(lib.mc_stats_reduce(C, S, D, _lib.ptr(st), _lib.ptr(center), m,
-                                       _lib.ptr(spread), stream))
+        spread = torch.zeros((2, D), dtype=torch.float64, device=x.device)
+        if C > 0:
+            _lib.check(lib.mc_stats_reduce(C, S, D, _lib.ptr(st), _lib.ptr(center), m,
+                                           _lib.ptr(spread), stream))
         _all_reduce(spread, group)
         _lib.check(lib.mc_rhat(D, m, S, _lib.ptr(spread), _lib.ptr(rhat), stream))
     return {"ess": st[_lib.MC_ST_ESS].view(C, D).cpu().numpy(),

@@ -3,7 +3,12 @@
 Same signature, defaults, return value and progress output as the
 reference's ``hmc()``; the whole iteration loop (momentum draw, L leapfrog
 steps with the fused gradient tape, Metropolis accept, step-size adaptation,
-sample store) runs in the persistent HIP kernel ``k_hmc`` (csrc/hmc.h).
+sample store) runs in one persistent HIP kernel chosen by the program's plan:
+``k_hmc_lf`` (csrc/lanes_fast.h: lane-resident, fast-form programs such as the
+hierarchical and isotropic Gaussians), ``k_hmc_lr`` (csrc/lanes.h: other
+lane-resident programs), ``k_hmc_sl`` (csrc/sliced.h: the term interpreter
+over data slices) or ``k_hmc`` (csrc/hmc.h: the chain-per-workgroup tape,
+every other program).
 
 Additions (keyword-only): ``num_chains`` runs independent chains in one
 launch (samples gain a leading chain axis), ``chain_offset`` selects the RNG

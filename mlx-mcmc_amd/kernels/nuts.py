@@ -2,8 +2,10 @@
 
 Same signature, defaults, return value and progress output as the
 reference's ``nuts()`` (slice NUTS, Hoffman & Gelman 2014 Alg. 3, dual
-averaging).  Tree building runs iteratively inside the persistent HIP kernel
-``k_nuts`` (csrc/nuts.h), one chain per chain group.
+averaging).  Tree building runs iteratively inside a persistent HIP kernel:
+``k_nuts_lr`` (csrc/nuts_lanes.h, one chain per wave, lane-resident state)
+when the model plans as one lane-resident slice, else ``k_nuts`` (csrc/nuts.h,
+one chain per chain group on the gradient tape).
 
 ``nuts_kernel``: "auto" runs the lane-resident kernel ``k_nuts_lr``
 (csrc/nuts_lanes.h: chain state in registers, tree arena in LDS) when the

@@ -103,7 +103,7 @@ def test_validation_errors_before_device_work():
     rc = lib.mc_program_create(terms, 1, 2, 0.0, None, 0, idx.ctypes.data_as(ctypes.c_void_p),
                                3, ctypes.byref(h))
     assert rc == _lib.MC_ERR_INVALID and b"out of range" in lib.mc_last_error()
-    assert lib.mc_abi_version() == 1
+    assert lib.mc_abi_version() == 2
     # host-side switch of the exchange kernels' timeout test hook
     assert lib.mc_debug_exchange_fault(0) == 0
     assert lib.mc_rng_fill(0, 0, 0, 0, 0, 0, 1, 9, None, None) == _lib.MC_ERR_INVALID
@@ -170,6 +170,12 @@ L, E = _lib.MC_EX_LEAF, _lib
     ([(L, -1, -1, -1, P0), (L, -1, -1, -1, DATA), (E.MC_EX_WHERE, 0, 1, 1, None)],
      _lib.MC_ERR_UNSUPPORTED, b"where mask"),                            # traced mask
     ([(L, -1, -1, -1, P0)] * 33, _lib.MC_ERR_UNSUPPORTED, b"1 .. 32 nodes"),
+    # leaf ranges past the caller's pools (checked against n_data / n_index,
+    # not the library's grown copies of them)
+    ([(L, -1, -1, -1, {"kind": _lib.MC_OP_DATA, "pool_offset": 1})], _lib.MC_ERR_INVALID,
+     b"data range out of pool"),
+    ([(L, -1, -1, -1, {"kind": _lib.MC_OP_GATHER, "param_offset": 0, "pool_offset": 2})],
+     _lib.MC_ERR_INVALID, b"index range out of pool"),
 ])
 def test_expression_validation(nodes, code, msg):
     rc, err = _expr_program(nodes)

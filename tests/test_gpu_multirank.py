@@ -103,7 +103,8 @@ def test_bench_ranks_gloo(gpu, world, workload):
            "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "20", "--warmup", "5",
            "--chains", "64", "--no-cpu-baseline", "--clock-warm-ms", "0"]
-    cmd += ["--workload", "nuts"] if workload == "nuts" else ["--shape", "small", "--gather"]
+    cmd += ["--workload", "nuts"] if workload == "nuts" else [
+        "--shape", "small", "--gather", "--ess-draws", "400", "--ess-warmup", "100"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=170, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -121,6 +122,53 @@ def test_bench_ranks_gloo(gpu, world, workload):
         assert "gather_ms" in out
         assert out["value"] == pytest.approx(C * 20 * 20 / (out["ms_per_step"] * 20 / 1e3),
                                              rel=1e-6)
+
+
+def _bench_line(world, chains, extra):
+    env = dict(os.environ, MC_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--chains", str(chains),
+           "--no-cpu-baseline", "--clock-warm-ms", "0"] + extra
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=170, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_ess_two_ranks_equal_one_rank(gpu):
+    """The ESS/s half of the metric on the multi-rank line (VERDICT r3
+    "Next round" 3): two ranks of 32 chains each report the converged-ESS
+    block (ESS summed over every rank's chains, split R-hat over all of them,
+    all-reduced moment blocks) and the timed-draw block equal to one rank
+    running the same 64 global chains, up to the f64 summation order."""
+    extra = ["--shape", "small", "--steps", "150", "--warmup", "20",
+             "--ess-draws", "400", "--ess-warmup", "100"]
+    two = _bench_line(2, 32, extra)
+    one = _bench_line(1, 64, extra)
+    for out in (one, two):
+        assert out["config"]["total_chains"] == 64
+        assert "ess_converged" in out and "ess_timed" in out
+    a, b = one["ess_converged"], two["ess_converged"]
+    assert a["chains"] == b["chains"] == 64
+    assert a["accept_rate"] == pytest.approx(b["accept_rate"], rel=1e-12)
+    for k in ("max", "median", "mean"):
+        if k in a["rhat"]:
+            assert a["rhat"][k] == pytest.approx(b["rhat"][k], rel=1e-9), k
+    assert (a["ess_per_sec"] is None) == (b["ess_per_sec"] is None)
+    if a["ess_per_sec"] is not None:
+        for k in ("min", "median", "total"):
+            assert a["ess_sum"][k] == pytest.approx(b["ess_sum"][k], rel=1e-9), k
+        assert b["ess_per_sec"]["min"] > 0
+    ta, tb = one["ess_timed"], two["ess_timed"]
+    assert ta["chains_used"] == tb["chains_used"]
+    assert ta["frozen_chains"] == tb["frozen_chains"]
+    if "rhat" in ta:
+        assert ta["rhat"]["max"] == pytest.approx(tb["rhat"]["max"], rel=1e-9)
+    assert (one["ess_per_sec"] is None) == (two["ess_per_sec"] is None)
+    print("ESS converged (1 rank / 2 ranks):", a.get("ess_sum"), b.get("ess_sum"))
 
 
 def _run_large(C, offset):
@@ -149,24 +197,14 @@ def test_large_shape_rank_shard_bit_identical(gpu, rank):
 
 
 def test_bench_large_two_ranks_gloo(gpu):
-    """Two ranks of the large, sliced program share the one GPU (each launch
-    needs its 4 chain blocks x 16 slices co-resident): the run completes with
-    one aggregate line (samples gathered), or fails fast with the exchange
-    timeout status — it never hangs (the subprocess limit would fail this)."""
-    env = dict(os.environ, MC_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
-           "--chains", "64", "--shape", "large", "--gather", "--no-cpu-baseline",
-           "--clock-warm-ms", "0"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=170, env=env, cwd=ROOT)
-    if r.returncode != 0:
-        assert "timed out" in r.stderr, r.stderr[-3000:]
-        print("two ranks on one GPU: exchange timeout reported (fail fast)")
-        return
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
-    out = json.loads(lines[0])
+    """Two ranks of the large, sliced program share the one GPU: each launch
+    needs its 4 chain blocks x 16 slices co-resident, 64 of the 256 CUs, so
+    both grids fit side by side and the run must complete with one aggregate
+    line (samples gathered, ESS over both ranks' chains).  An exchange
+    timeout here is a failure."""
+    out = _bench_line(2, 64, ["--steps", "20", "--warmup", "5", "--shape", "large",
+                              "--gather", "--ess-draws", "200", "--ess-warmup", "50"])
     assert out["n_gpus"] == 2 and out["config"]["total_chains"] == 128
     assert "gather_ms" in out and out["value"] > 0
+    assert out["ess_converged"]["chains"] == 128
     print("two ranks on one GPU:", out["value"] / 1e6, "M steps/s")

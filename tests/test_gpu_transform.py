@@ -177,6 +177,30 @@ def test_transform_lanes_match_tape(gpu, shape, kernel):
     assert full >= 10, "most chains agree over the whole run (the rest to a proven near-tie)"
 
 
+def test_transform_sliced_zero_leapfrog_steps(gpu):
+    """num_leapfrog_steps = 0 (accepted by the reference's hmc(): the proposal
+    is the current point, H is unchanged, every log U < 0 accepts) on a
+    sliced program with transformed shared parameters: the lane kernels need
+    L > 0 and the term interpreter declines transforms, so the run takes the
+    chain-per-workgroup tape — it must succeed, not fail with UNSUPPORTED
+    (ADVICE r3)."""
+    import mlx_mcmc_amd as m
+    from mlx_mcmc_amd import _trace
+
+    lp, init = W.hierarchical_reparam(W.ns_product(), *W.SHAPES["large"])
+    prog = _trace.compile_model(lp, init)
+    assert prog.num_slices == 16 and prog.slice_kernel == "lanes"
+    s, rate, info = m.hmc(lp, init, num_samples=4, num_warmup=2, step_size=1e-3,
+                          num_leapfrog_steps=0, key=m.random.key(0), num_chains=4,
+                          progress=False, return_info=True)
+    assert np.all(np.asarray(rate) == 1.0)
+    for k, v in init.items():
+        want = np.broadcast_to(np.asarray(v, np.float32), np.asarray(s[k]).shape[2:])
+        for c in range(4):
+            for i in range(4):
+                np.testing.assert_array_equal(np.asarray(s[k])[c, i], want)
+
+
 def test_transform_nuts_trace_matches_oracle(gpu):
     import mlx_mcmc_amd as m
 
