@@ -1,148 +1,9 @@
-// api.hip — libmcmc355.so: program builder, launchers and the C-ABI of
-// include/mcmc355.h.  One translation unit so every kernel is launched from
-// the unit that defines it.
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cmath>
-#include <cstdarg>
-#include <cstdio>
-#include <cstring>
-#include <cstdlib>
-#include <map>
-#include <mutex>
-#include <tuple>
-#include <type_traits>
-#include <numeric>
-#include <unordered_map>
-#include <string>
-#include <vector>
-
-#include "diag.h"
-#include "eval.h"
-#include "hmc.h"
-#include "internal.h"
-#include "lanes.h"
-#include "lanes_fast.h"
-#include "nuts_lanes.h"
-#include "mh.h"
-#include "nuts.h"
-#include "philox.h"
-#include "sliced.h"
-
-using namespace mc;
-
-// ---------------------------------------------------------------------------
-// errors
-// ---------------------------------------------------------------------------
-static thread_local std::string g_last_error;
-
-static int fail(int code, const char* fmt, ...) {
-    char buf[1024];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof(buf), fmt, ap);
-    va_end(ap);
-    g_last_error = buf;
-    return code;
-}
-
-#define MC_HIP_TRY(expr)                                                                \
-    do {                                                                                \
-        hipError_t e_ = (expr);                                                         \
-        if (e_ != hipSuccess)                                                           \
-            return fail(MC_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));      \
-    } while (0)
-
-// ---------------------------------------------------------------------------
-// program
-// ---------------------------------------------------------------------------
-// Host copy of a sliced layout (sliced.h) and its device tables.
-struct SlicePlan {
-    int S = 1, Lp = 0, Pmax = 0, Dsh = 0, nitems = 0, sdata_floats = 0, nb_max = 0, combine = 0;
-    std::vector<SlTerm> terms;
-    std::vector<SlTerm> sterms;  // scalar terms (after the exchange)
-    std::vector<float> data;
-    std::vector<int32_t> index;
-    std::vector<int64_t> blocks;
-    std::vector<int32_t> gidx;
-    SlTerm* d_terms = nullptr;
-    SlTerm* d_sterms = nullptr;
-    float* d_data = nullptr;
-    int32_t* d_index = nullptr;
-    int64_t* d_blocks = nullptr;
-    int32_t* d_gidx = nullptr;
-};
-
-// Host copy of the lane-resident layout (lanes.h) and its device tables.
-struct LanePlan {
-    int ok = 0;          // the sliced program qualifies
-    int rs = 1;          // register slots per lane (1, 2 or 4)
-    int sdata_floats = 0;
-    int S = 0, Dsh = 0, nitems = 0;  // slice geometry (S = 1: an unsliced program, no exchange)
-    int32_t shl[kLrMaxShared] = {0, 0, 0, 0};  // shared parameters by ordinal
-    int32_t n_generic = 0;  // scalar terms that are not "own" priors
-    int fast = 0;        // fast form: only swept / direct terms and own priors (k_hmc_lf)
-    int form = -1;       // the fast form's LF_* bits when every slice has the same terms
-                         // and distinct shared roles (compile-time k_hmc_lf), else -1
-    int32_t shxf[kLrMaxShared] = {0, 0, 0, 0};  // transforms of the shared parameters
-    float shid[kLrMaxShared] = {0.f, 0.f, 0.f, 0.f};  // raw identity weights (k_hmc_lf)
-    int has_xf = 0;      // a shared parameter is transformed, or an identity term
-                         // (no NUTS lanes, no term interpreter)
-    std::string why;     // why it does not qualify
-    std::vector<LrTerm> terms;
-    std::vector<float> data;
-    std::vector<int64_t> blocks;
-    std::vector<int32_t> gidx;
-    std::vector<LrSterm> sterms;
-    LrTerm* d_terms = nullptr;
-    LrSterm* d_sterms = nullptr;
-    float* d_data = nullptr;
-    int64_t* d_blocks = nullptr;
-    int32_t* d_gidx = nullptr;
-};
-
-struct mc_program {
-    int32_t D = 0;
-    float lp_const = 0.0f;
-    int32_t wpc = 1;
-    int32_t nslots = 1;
-    int64_t sfin_base = 0;
-    int64_t max_n = 0;
-    std::vector<DevTerm> terms;
-    DevTerm* d_terms = nullptr;
-    std::vector<DevExprNode> nodes;  // expression-term nodes (DevTerm::expr_base)
-    bool ex = false;                 // has expression terms: the EX kernel instantiations
-    DevExprNode* d_nodes = nullptr;
-    float* d_data = nullptr;
-    int32_t* d_index = nullptr;
-    // terms as validated (before the chain-per-workgroup tiling) and the host
-    // pools they point into: the input of the slice planner
-    std::vector<DevTerm> raw;
-    std::vector<float> h_data;
-    std::vector<int32_t> h_index;
-    SlicePlan sl;
-    LanePlan lr;
-    int32_t slice_kernel = 0;  // 0 automatic, 1 term interpreter, 2 lane-resident
-    // why the automatic plan did not reach the lane-resident kernel ("" when it
-    // did or was not asked to): mc_program_kernel_note
-    std::string note;
-};
-
-static DevCtx ctx_of(const mc_program* p) {
-    DevCtx c;
-    c.terms = p->d_terms;
-    c.nodes = p->d_nodes;
-    c.n_terms = (int32_t)p->terms.size();
-    c.D = p->D;
-    c.lp_const = p->lp_const;
-    c.nslots = p->nslots;
-    c.data = p->d_data;
-    c.index = p->d_index;
-    c.sfin_base = p->sfin_base;
-    return c;
-}
-
+// api.hip — libmcmc355.so: program builder, slice / lane planners, tape,
+// state and diagnostics launches and the rest of the C-ABI of
+// include/mcmc355.h (the sampler launches are in run_hmc.hip, run_mh.hip,
+// run_nuts.hip).
+#include "host.h"
+#include "diag.h"  // (non-template kernels: this unit only)
 static bool is_vec_kind(int k) { return k == MC_OP_DATA || k == MC_OP_PVEC || k == MC_OP_GATHER; }
 static bool is_acc_vec(int k) { return k == MC_OP_PVEC || k == MC_OP_GATHER; }
 
@@ -318,36 +179,12 @@ static void free_slices(SlicePlan& P) {
     P = SlicePlan();
 }
 
-static SlCtx slctx_of(const mc_program* p) {
-    SlCtx c;
-    std::memset(&c, 0, sizeof(c));
-    const SlicePlan& P = p->sl;
-    c.terms = P.d_terms;
-    c.data = P.d_data;
-    c.index = P.d_index;
-    c.blocks = P.d_blocks;
-    c.gidx = P.d_gidx;
-    c.n_terms = (int32_t)p->raw.size();
-    c.S = P.S;
-    c.Lp = P.Lp;
-    c.Pmax = P.Pmax;
-    c.Dsh = P.Dsh;
-    c.D = p->D;
-    c.nitems = P.nitems;
-    c.sdata_floats = P.sdata_floats;
-    c.lp_const = p->lp_const;
-    c.combine = P.combine;
-    c.sterms = P.d_sterms;
-    c.n_sterms = (int32_t)P.sterms.size();
-    return c;
-}
 
 static int sl_lds_bytes(const mc_program* p, int nb) {
     const SlCtx c = slctx_of(p);
     return 4 * (nb == 16 ? SlLayout<16>(c).total : SlLayout<8>(c).total);
 }
 
-static constexpr int kSlLdsBudget = 150 * 1024;
 
 static int64_t pp_index(const DevTerm& t, int a, int64_t i, const std::vector<int32_t>& ip) {
     const DevOperand& o = t.op[a];
@@ -367,41 +204,6 @@ struct SlPartition {
     std::vector<std::vector<std::vector<int64_t>>> elems;  // [slice][term] element ids
 };
 
-static bool has_affine(const mc_program* p) {
-    for (const DevTerm& t : p->raw)
-        if (t.affine) return true;
-    return false;
-}
-static bool has_expr(const mc_program* p) {
-    for (const DevTerm& t : p->raw)
-        if (t.dist == MC_DIST_EXPR) return true;
-    return false;
-}
-// Transformed parameter operands and identity terms (the reparameterised
-// models of mc_transform_kind).
-static bool has_transform(const mc_program* p) {
-    for (const DevTerm& t : p->raw) {
-        if (t.dist == MC_DIST_IDENTITY) return true;
-        for (int a = 0; a < 3; ++a)
-            if (t.op[a].xf != MC_XF_NONE) return true;
-        if (t.affine && (t.ab.xf != MC_XF_NONE || t.ax.xf != MC_XF_NONE)) return true;
-    }
-    return false;
-}
-// ... whose transforms all act on broadcast (PSCALAR) parameters and whose
-// identity terms are scalar: the lane-resident kernel k_hmc_lr runs them
-// (lanes.h LrCtx::shxf); anything else runs on the chain-per-workgroup kernels.
-static bool transform_on_shared_only(const mc_program* p) {
-    for (const DevTerm& t : p->raw) {
-        if (t.affine) return false;
-        for (int a = 0; a < 3; ++a)
-            if (t.op[a].xf != MC_XF_NONE && t.op[a].kind != MC_OP_PSCALAR) return false;
-        if (t.dist == MC_DIST_IDENTITY && t.op[0].kind != MC_OP_PSCALAR &&
-            t.op[0].kind != MC_OP_CONST)
-            return false;
-    }
-    return true;
-}
 
 static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = nullptr) {
     const std::vector<DevTerm>& raw = p->raw;
@@ -844,32 +646,6 @@ static void free_lanes(LanePlan& L) {
     L = LanePlan();
 }
 
-static LrCtx lrctx_of(const mc_program* p) {
-    LrCtx c;
-    std::memset(&c, 0, sizeof(c));
-    const LanePlan& L = p->lr;
-    c.terms = L.d_terms;
-    c.data = L.d_data;
-    c.blocks = L.d_blocks;
-    c.gidx = L.d_gidx;
-    c.sterms = L.d_sterms;
-    c.n_terms = (int32_t)p->raw.size();
-    c.n_sterms = (int32_t)L.sterms.size();
-    c.n_sterms_generic = L.n_generic;
-    c.S = L.S;
-    c.Dsh = L.Dsh;
-    c.D = p->D;
-    c.nitems = L.nitems;
-    c.sdata_floats = L.sdata_floats;
-    c.lp_const = p->lp_const;
-    for (int k = 0; k < kLrMaxShared; ++k) {
-        c.shl[k] = L.shl[k];
-        c.shxf[k] = L.shxf[k];
-        c.shid[k] = L.shid[k];
-    }
-    c.has_xf = L.has_xf;
-    return c;
-}
 
 // Deal every slice's private parameters to (lane, slot), longest first onto
 // the least loaded lane with a free slot, and tile each term's elements per
@@ -1344,7 +1120,6 @@ extern "C" int32_t mc_program_slice_kernel(const mc_program* p) {
     return 2;
 }
 
-static bool lanes_fast_enabled();
 extern "C" int32_t mc_program_lanes_fast(const mc_program* p) {
     if (!p) return -1;
     const int32_t k = mc_program_slice_kernel(p);
@@ -2048,79 +1823,6 @@ extern "C" int mc_program_destroy(mc_program* p) {
 extern "C" int32_t mc_program_num_params(const mc_program* p) { return p ? p->D : -1; }
 extern "C" int32_t mc_program_waves_per_chain(const mc_program* p) { return p ? p->wpc : -1; }
 
-// ---------------------------------------------------------------------------
-// geometry helpers
-// ---------------------------------------------------------------------------
-static int cpb_of(int wpc) { return wpc >= 4 ? 1 : 4 / wpc; }
-static int block_of(int wpc) { return 64 * wpc * cpb_of(wpc); }
-static int32_t dpad_of(int32_t D) { return (D + 15) / 16 * 16; }
-static constexpr int64_t kLdsArenaBudget = 64 * 1024;  // keep >= 2 workgroups per CU
-
-static int scratch_of(const mc_program* p) {
-    // keep every chain group's region 16-byte aligned
-    return (group_scratch_floats(p->wpc, p->nslots) + 3) / 4 * 4;
-}
-static int64_t hmc_lds_floats(const mc_program* p, bool lds_arena) {
-    return scratch_of(p) + (lds_arena ? 5 * (int64_t)dpad_of(p->D) : 0);
-}
-static bool hmc_use_lds(const mc_program* p) {
-    return cpb_of(p->wpc) * hmc_lds_floats(p, true) * 4 <= kLdsArenaBudget;
-}
-
-template <typename K>
-static hipError_t allow_lds(K kernel, size_t bytes) {
-    if (bytes <= 64 * 1024) return hipSuccess;
-    // the attribute is a per-(kernel, device) maximum: the largest value set so
-    // far is cached and a launch needing no more skips the call (it costs host
-    // time on every launch otherwise; launch functions run once per chunk of
-    // iterations).  A launch needing more raises it — never lowers it, so a
-    // later large launch of the same instantiation is never refused.
-    static std::mutex mu;
-    static std::map<std::pair<const void*, int>, size_t> max_set;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const auto key = std::make_pair(reinterpret_cast<const void*>(kernel), dev);
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = max_set.find(key);
-    if (it != max_set.end() && bytes <= it->second) return hipSuccess;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    if (e == hipSuccess) max_set[key] = bytes;
-    return e;
-}
-
-static TraceDev trace_of(const mc_trace* t) {
-    TraceDev d;
-    std::memset(&d, 0, sizeof(d));
-    if (t) {
-        d.iter_begin = t->iter_begin;
-        d.capacity = t->capacity;
-        d.accepted = t->accepted;
-        d.accept_stat = t->accept_stat;
-        d.step_size = t->step_size;
-        d.energy = t->energy;
-        d.tree_depth = t->tree_depth;
-        d.n_leapfrog = t->n_leapfrog;
-    } else {
-        d.capacity = 0;
-    }
-    return d;
-}
-
-// The instantiation of a chain-per-workgroup launcher for a program: waves
-// per chain (1, 4 or 8), LDS arena or not, expression terms or not (EX).
-template <typename F>
-static int dispatch_tape(const mc_program* p, bool lds, F&& f) {
-    using T_ = std::true_type;
-    using F_ = std::false_type;
-    auto ex = [&](auto w, auto l) { return p->ex ? f(w, l, T_{}) : f(w, l, F_{}); };
-    auto arena = [&](auto w) { return lds ? ex(w, T_{}) : ex(w, F_{}); };
-    switch (p->wpc) {
-        case 1: return arena(std::integral_constant<int, 1>{});
-        case 4: return arena(std::integral_constant<int, 4>{});
-        default: return arena(std::integral_constant<int, 8>{});
-    }
-}
 
 // ---------------------------------------------------------------------------
 // batched log density + gradient
@@ -2287,618 +1989,8 @@ extern "C" int mc_state_init(const mc_program* p, int64_t C, const float* q0, do
     }
 }
 
-// ---------------------------------------------------------------------------
-// HMC / NUTS launches
-// ---------------------------------------------------------------------------
-static int check_cfg(const mc_program* p, const mc_run_config* cfg, void* state) {
-    if (!p || !cfg || !state) return fail(MC_ERR_INVALID, "NULL program/config/state");
-    if (cfg->num_chains < 0 || cfg->iter_count < 0 || cfg->iter_begin < 0 ||
-        cfg->num_warmup < 0 || cfg->num_samples < 0)
-        return fail(MC_ERR_INVALID, "negative count in config");
-    if (cfg->chain_offset < 0 || cfg->chain_offset + cfg->num_chains > (int64_t)UINT32_MAX)
-        return fail(MC_ERR_INVALID, "chain ids must fit in 32 bits");
-    if (cfg->iter_begin + cfg->iter_count > (int64_t)UINT32_MAX)
-        return fail(MC_ERR_INVALID, "iteration ids must fit in 32 bits");
-    return MC_OK;
-}
 
-// ---- sliced launches ---------------------------------------------------------
-static int device_cus() {
-    static int cached[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    if (cached[dev] == 0) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 0;
-        cached[dev] = n;
-    }
-    return cached[dev];
-}
-// Exchange kernels (k_hmc_sl, k_hmc_lr with S >= 2) spin on records of the
-// other workgroups of their chain block, so every workgroup of a launch must
-// be resident at once.  An occupancy query of the same kernel, block size and
-// LDS caps the grid at what the device holds: a launch that cannot be
-// co-resident fails fast with MC_ERR_UNSUPPORTED.  They are then launched
-// plainly: on a device shared with other work that keeps some of the grid
-// out, the spin times out and the launch reports MC_ERR_TIMEOUT with the
-// stranded block's state unchanged (mc_workspace_status).  (Round 2 also
-// offered cooperative launches behind an environment switch: ~50 us more per
-// launch on MI355X, profiles/r2/v17_coop_ab.json, and a crash in torch's HIP
-// exit handlers under rocprofv3 whose cause was not found — removed.)
-template <typename... KA, typename... A>
-static hipError_t launch_exchange(void (*k)(KA...), int64_t grid, int block, size_t lds,
-                                  hipStream_t st, A&&... a) {
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(block), lds, st,
-                       std::decay_t<KA>(std::forward<A>(a))...);
-    return hipGetLastError();
-}
-// workgroups of kernel k (block threads, lds bytes) the device holds at once
-template <typename K>
-static int64_t resident_capacity(K k, int block, size_t lds) {
-    // cached per (kernel, device, block, LDS): the occupancy query is a host
-    // call on every exchange launch otherwise
-    static std::mutex mu;
-    static std::map<std::tuple<const void*, int, int, size_t>, int64_t> cache;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const auto key = std::make_tuple(reinterpret_cast<const void*>(k), dev, block, lds);
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        auto it = cache.find(key);
-        if (it != cache.end()) return it->second;
-    }
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(k), block,
-                                                     lds) != hipSuccess)
-        return -1;
-    const int64_t cap = (int64_t)n * device_cus();
-    std::lock_guard<std::mutex> lk(mu);
-    cache[key] = cap;
-    return cap;
-}
-static int g_exchange_fault = 0;  // mc_debug_exchange_fault
-static bool sliced(const mc_program* p) { return p->sl.S >= 2 && p->sl.d_terms != nullptr; }
-// an unsliced program planned onto the lane-resident kernel (one slice)
-static bool lanes1(const mc_program* p) { return p->sl.S < 2 && p->lr.ok && p->lr.S == 1; }
-static int sl_nb_for(const mc_program* p, int64_t C) {
-    return (p->sl.nb_max >= 16 && C > 8) ? 16 : 8;
-}
-// chain blocks per launch: every workgroup of a launch must be resident at
-// once (the slices of a block wait for each other), one workgroup per CU
-static int64_t sl_groups_per_launch(const mc_program* p, int64_t C) {
-    const int nb = sl_nb_for(p, C);
-    const int64_t groups = (C + nb - 1) / nb;
-    const int64_t cap = std::max<int64_t>(1, device_cus() / p->sl.S);
-    return std::min(groups, cap);
-}
-static constexpr int64_t kSlStatusBytes = 256;
-// waves per workgroup of the lane-resident kernel: 8 (16 chains, two waves per
-// SIMD) for up to 16 slices... 4 (8 chains, one wave per SIMD) for <= 8 slices
-// one slice: one wave per workgroup (no exchange, so no block structure to
-// keep; a lone wave per CU does not share the scalar unit or LDS with others)
-static int lr_nw(const mc_program* p) { return p->lr.S == 1 ? 1 : (p->lr.S <= 8 ? 4 : 8); }
-static int64_t lr_groups_per_launch(const mc_program* p, int64_t C) {
-    const int nb = 2 * lr_nw(p);
-    const int64_t groups = (C + nb - 1) / nb;
-    if (p->lr.S == 1) return groups;  // no exchange: no co-residency needed
-    const int64_t cap = std::max<int64_t>(1, device_cus() / p->lr.S);
-    return std::min(groups, cap);
-}
-static int64_t sl_workspace_bytes(const mc_program* p, int64_t C) {
-    if (lanes1(p)) return kSlStatusBytes;
-    const int nb = sl_nb_for(p, C);
-    int64_t x = 2 * sl_groups_per_launch(p, C) * p->sl.S * (int64_t)p->sl.nitems * nb * 8;
-    if (p->lr.ok)  // either kernel may run on the same workspace (lanes.h: one
-                   // 128-byte line per (wave, slice) record)
-        x = std::max(x, 2 * lr_groups_per_launch(p, C) * lr_nw(p) * p->sl.S * 128);
-    return kSlStatusBytes + x;
-}
-static bool use_lanes(const mc_program* p, const mc_run_config* cfg) {
-    return p->lr.ok && p->slice_kernel != 1 && cfg->num_leapfrog_steps > 0;
-}
 
-// Exchange tags of the lane-resident kernel continue across launches on one
-// workspace: a process-wide counter per workspace address hands every launch
-// a fresh tag range, so the granule lines need clearing only the first time
-// the library sees a workspace (or after it is released, reused by another
-// kernel, or the 32-bit counter would wrap) — not ahead of every launch.
-static std::mutex g_ws_mu;
-struct WsTags {
-    uint32_t epoch;    // last tag handed out
-    uint64_t cleared;  // bytes of the workspace cleared when its tags started
-};
-static std::unordered_map<const void*, WsTags> g_ws_epoch;
-// workspaces whose last launch was an exchange kernel (k_hmc_sl / k_hmc_lr):
-// only those hold a status word for mc_workspace_status
-static std::unordered_map<const void*, char> g_ws_status;
-static void ws_forget(const void* ws) {
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    g_ws_epoch.erase(ws);
-    g_ws_status.erase(ws);
-}
-static void ws_mark_status(const void* ws) {
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    g_ws_status[ws] = 1;
-}
-static bool ws_has_status(const void* ws) {
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    return g_ws_status.count(ws) != 0;
-}
-// Reserve `need` tags on ws, whose launch uses `bytes` of it: *base = first
-// tag - 1; returns true if the workspace must be cleared first — the first
-// time, when the tags would wrap, or when the launch uses more of it than was
-// cleared (a larger layout after mc_program_set_slices / set_slice_kernel
-// would otherwise read stale words beyond the cleared range).
-static bool ws_reserve(const void* ws, uint64_t need, uint64_t bytes, uint32_t* base) {
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    auto it = g_ws_epoch.find(ws);
-    const bool clear = it == g_ws_epoch.end() || (uint64_t)it->second.epoch + need >= 0xFFFFFFF0ull ||
-                       bytes > it->second.cleared;
-    *base = clear ? 0u : it->second.epoch;
-    const uint64_t cleared = clear ? bytes : it->second.cleared;
-    g_ws_epoch[ws] = WsTags{(uint32_t)(*base + need), cleared};
-    return clear;
-}
-
-extern "C" int mc_workspace_release(const void* ws) {
-    if (ws) ws_forget(ws);
-    return MC_OK;
-}
-
-extern "C" int mc_debug_exchange_fault(int on) {
-    g_exchange_fault = on ? 1 : 0;
-    return MC_OK;
-}
-
-// the fast-form kernel (lanes_fast.h) for programs that qualify, unless
-// MC_LANES_FAST=0 in the environment (A/B timing against k_hmc_lr)
-static int g_lanes_fast = -1;  // mc_debug_lanes_fast; -1: MC_LANES_FAST from the environment
-static bool lanes_fast_enabled() {
-    if (g_lanes_fast < 0) {
-        const char* e = std::getenv("MC_LANES_FAST");
-        g_lanes_fast = (e && e[0] == '0') ? 0 : 1;
-    }
-    return g_lanes_fast == 1;
-}
-extern "C" int mc_debug_lanes_fast(int on) {
-    g_lanes_fast = on ? 1 : 0;
-    return MC_OK;
-}
-
-// compile-time forms of k_hmc_lf: MC_LANES_FORM=0 in the environment or
-// mc_debug_lanes_forms(0) selects the run-time form kernel (A/B timing, tests)
-static int g_lanes_forms = -1;
-static bool lanes_forms_enabled() {
-    if (g_lanes_forms < 0) {
-        const char* e = std::getenv("MC_LANES_FORM");
-        g_lanes_forms = (e && e[0] == '0') ? 0 : 1;
-    }
-    return g_lanes_forms == 1;
-}
-extern "C" int mc_debug_lanes_forms(int on) {
-    g_lanes_forms = on ? 1 : 0;
-    return MC_OK;
-}
-
-template <int RS, int NSH, int NW, bool X1>
-static int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* state,
-                         float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
-    const bool fast = p->lr.fast && lanes_fast_enabled();
-    auto kern = fast ? k_hmc_lf<RS, NSH, NW, X1, -1> : k_hmc_lr<RS, NSH, NW, X1>;
-    const bool forms = lanes_forms_enabled();
-    if constexpr (NSH == 3) {  // the compile-time forms (one instantiation each)
-        constexpr int HIER = LF_SW | LF_SWS | LF_DIR | LF_DM | LF_DS;
-        if (fast && forms && p->lr.form == HIER) kern = k_hmc_lf<RS, lf_nroles(HIER), NW, X1, HIER>;
-        if (fast && forms && p->lr.form == LF_DIR) kern = k_hmc_lf<RS, lf_nroles(LF_DIR), NW, X1, LF_DIR>;
-    }
-    int64_t qo, go;
-    mc_state_offsets(p, cfg->num_chains, &qo, &go);
-    char* b = (char*)state;
-    RunArgs A;
-    std::memset(&A, 0, sizeof(A));
-    A.cfg = *cfg;
-    const LrCtx ctx = lrctx_of(p);
-    const size_t lds = (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm);
-    MC_HIP_TRY(allow_lds(kern, lds));
-    const int64_t C = cfg->num_chains;
-    constexpr int NB = 2 * NW;
-    const int64_t groups = (C + NB - 1) / NB;
-    const int64_t gpl = lr_groups_per_launch(p, C);
-    const int64_t used = sl_workspace_bytes(p, C);
-    int* status = (int*)ws;
-    unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
-    const uint64_t per_launch = (uint64_t)cfg->iter_count * cfg->num_leapfrog_steps + 1;
-    const int64_t nlaunch = (groups + gpl - 1) / gpl;
-    if (!X1) {
-        const int64_t cap = resident_capacity(kern, 64 * NW, lds);
-        if (cap < std::min(gpl, groups) * p->lr.S)
-            return fail(MC_ERR_UNSUPPORTED,
-                        "lane-resident HMC: %lld workgroups must be co-resident, the device holds "
-                        "%lld of this kernel", (long long)(std::min(gpl, groups) * p->lr.S),
-                        (long long)cap);
-        A.fault = g_exchange_fault;
-    }
-    uint32_t base = 0;
-    if (ws_reserve(ws, per_launch * (uint64_t)nlaunch, (uint64_t)used, &base))
-        MC_HIP_TRY(hipMemsetAsync(ws, 0, used, st));  // status word and granule lines
-    ws_mark_status(ws);
-    for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
-        const int64_t ng = std::min(gpl, groups - g0);
-        const int64_t grid = ng * p->lr.S;
-        if (X1) {
-            hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), lds, st, ctx, A,
-                               g0 * NB, ng, (mc_chain_scalars*)b, (float*)(b + qo),
-                               (float*)(b + go), samples, trace_of(tr), xch, status, base);
-            MC_HIP_TRY(hipGetLastError());
-        } else {
-            const hipError_t e = launch_exchange(
-                kern, grid, 64 * NW, lds, st, ctx, A, g0 * NB, ng,
-                (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples, trace_of(tr),
-                xch, status, base);
-            MC_HIP_TRY(e);
-        }
-        base += (uint32_t)per_launch;
-    }
-    return MC_OK;
-}
-
-template <int NB>
-static int launch_hmc_sl(const mc_program* p, const mc_run_config* cfg, void* state,
-                         float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
-    if (has_transform(p))
-        return fail(MC_ERR_UNSUPPORTED, "the term interpreter does not run transformed operands");
-    int64_t qo, go;
-    mc_state_offsets(p, cfg->num_chains, &qo, &go);
-    char* b = (char*)state;
-    RunArgs A;
-    std::memset(&A, 0, sizeof(A));
-    A.cfg = *cfg;
-    const SlCtx ctx = slctx_of(p);
-    const size_t lds = (size_t)SlLayout<NB>(ctx).total * 4;
-    MC_HIP_TRY(allow_lds(k_hmc_sl<NB>, lds));
-    const int64_t C = cfg->num_chains;
-    const int64_t groups = (C + NB - 1) / NB;
-    const int64_t gpl = sl_groups_per_launch(p, C);
-    const int64_t used = sl_workspace_bytes(p, C);
-    int* status = (int*)ws;
-    unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
-    const int64_t cap = resident_capacity(k_hmc_sl<NB>, kSlLanes * NB / 2, lds);
-    if (cap < std::min(gpl, groups) * p->sl.S)
-        return fail(MC_ERR_UNSUPPORTED,
-                    "sliced HMC: %lld workgroups must be co-resident, the device holds %lld of "
-                    "this kernel", (long long)(std::min(gpl, groups) * p->sl.S), (long long)cap);
-    A.fault = g_exchange_fault;
-    ws_forget(ws);  // its tags restart at 1: the lane-resident kernel must clear again
-    ws_mark_status(ws);
-    for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
-        const int64_t ng = std::min(gpl, groups - g0);
-        // the exchange tags restart at 1 in every launch: clear the granules
-        // (and, first, the status word) ahead of it
-        MC_HIP_TRY(hipMemsetAsync(g0 == 0 ? ws : (void*)xch, 0,
-                                  g0 == 0 ? used : used - kSlStatusBytes, st));
-        const int64_t grid = ng * p->sl.S;
-        const hipError_t e = launch_exchange(k_hmc_sl<NB>, grid, kSlLanes * NB / 2, lds, st, ctx,
-                                             A, g0 * NB, ng, (mc_chain_scalars*)b,
-                                             (float*)(b + qo), (float*)(b + go), samples,
-                                             trace_of(tr), xch, status);
-        MC_HIP_TRY(e);
-    }
-    return MC_OK;
-}
-
-extern "C" int mc_workspace_status(const mc_program* p, const void* ws, int64_t bytes,
-                                   void* stream) {
-    if (!p) return fail(MC_ERR_INVALID, "program is NULL");
-    if (!ws || !ws_has_status(ws)) return MC_OK;  // the last launch on ws had no exchange
-    if (bytes < kSlStatusBytes) return fail(MC_ERR_INVALID, "bad workspace");
-    int v = 0;
-    MC_HIP_TRY(hipMemcpyAsync(&v, ws, sizeof(int), hipMemcpyDeviceToHost, (hipStream_t)stream));
-    MC_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    if (v != 0) {
-        ws_forget(ws);  // the next launch clears the status word and the granules
-        return fail(MC_ERR_TIMEOUT, "sliced HMC: a cross-workgroup exchange timed out");
-    }
-    return MC_OK;
-}
-
-extern "C" int64_t mc_hmc_workspace_bytes(const mc_program* p, int64_t C) {
-    if (!p || C < 0) return -1;
-    // (a lanes1 program runs L = 0 configurations on the unsliced kernel, and
-    // so does a sliced program with transformed operands, which the term
-    // interpreter does not take: mc_hmc_run)
-    const int64_t x = (lanes1(p) || sliced(p)) ? sl_workspace_bytes(p, C) : 0;
-    if (sliced(p) && !has_transform(p)) return x;
-    if (hmc_use_lds(p)) return x;
-    return std::max(x, C * 5 * (int64_t)dpad_of(p->D) * 4);
-}
-
-template <int WPC, bool LDS, bool EX>
-static int launch_hmc(const mc_program* p, const mc_run_config* cfg, void* state,
-                      float* samples, const mc_trace* tr, float* ws, hipStream_t st) {
-    int64_t qo, go;
-    mc_state_offsets(p, cfg->num_chains, &qo, &go);
-    char* b = (char*)state;
-    RunArgs A;
-    std::memset(&A, 0, sizeof(A));
-    A.cfg = *cfg;
-    A.dpad = dpad_of(p->D);
-    A.lds_floats = (int32_t)hmc_lds_floats(p, LDS);
-    A.scratch_floats = scratch_of(p);
-    const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
-    const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
-    MC_HIP_TRY(allow_lds(k_hmc<WPC, LDS, EX>, lds));
-    hipLaunchKernelGGL((k_hmc<WPC, LDS, EX>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
-                       ctx_of(p), A, (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go),
-                       samples, trace_of(tr), ws);
-    MC_HIP_TRY(hipGetLastError());
-    return MC_OK;
-}
-
-extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* state,
-                          float* samples, const mc_trace* tr, void* ws, int64_t ws_bytes,
-                          void* stream) {
-    int rc = check_cfg(p, cfg, state);
-    if (rc) return rc;
-    if (cfg->num_leapfrog_steps < 0) return fail(MC_ERR_INVALID, "num_leapfrog_steps < 0");
-    if (cfg->num_chains == 0 || cfg->iter_count == 0) return MC_OK;
-    // L = 0 with transformed operands: the interpreter (k_hmc_sl) declines
-    // them, so such a run takes the chain-per-workgroup tape (as lanes1 does)
-    const bool sl_tape = sliced(p) && !use_lanes(p, cfg) && has_transform(p);
-    if ((sliced(p) && !sl_tape) || (lanes1(p) && use_lanes(p, cfg))) {
-        const int64_t need = sl_workspace_bytes(p, cfg->num_chains);
-        if (ws == nullptr || ws_bytes < need)
-            return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
-        if (device_cus() <= 0) return fail(MC_ERR_HIP, "no HIP device");
-        if (use_lanes(p, cfg)) {
-            hipStream_t st = (hipStream_t)stream;
-            const bool n4 = p->lr.Dsh > 3, w4 = lr_nw(p) == 4, x1 = p->lr.S == 1;
-#define MC_LR(RS_, NSH_)                                                                   \
-    return x1 ? launch_hmc_lr<RS_, NSH_, 1, true>(p, cfg, state, samples, tr, ws, st)      \
-         : w4 ? launch_hmc_lr<RS_, NSH_, 4, false>(p, cfg, state, samples, tr, ws, st)     \
-              : launch_hmc_lr<RS_, NSH_, 8, false>(p, cfg, state, samples, tr, ws, st)
-            switch (p->lr.rs) {
-                case 1: if (n4) MC_LR(1, 4); else MC_LR(1, 3);
-                case 2: if (n4) MC_LR(2, 4); else MC_LR(2, 3);
-                default: if (n4) MC_LR(4, 4); else MC_LR(4, 3);
-            }
-#undef MC_LR
-        }
-        return sl_nb_for(p, cfg->num_chains) == 16
-                   ? launch_hmc_sl<16>(p, cfg, state, samples, tr, ws, (hipStream_t)stream)
-                   : launch_hmc_sl<8>(p, cfg, state, samples, tr, ws, (hipStream_t)stream);
-    }
-    ws_forget(ws);
-    const bool lds = hmc_use_lds(p);
-    const int64_t need = mc_hmc_workspace_bytes(p, cfg->num_chains);
-    if (!lds && (ws == nullptr || ws_bytes < need))
-        return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
-    hipStream_t st = (hipStream_t)stream;
-    float* w = (float*)ws;
-    return dispatch_tape(p, lds, [&](auto W, auto L, auto E) {
-        return launch_hmc<decltype(W)::value, decltype(L)::value, decltype(E)::value>(
-            p, cfg, state, samples, tr, w, st);
-    });
-}
-
-// ---- Metropolis-Hastings (metropolis.py:6-101) --------------------------------
-static int64_t mh_lds_floats(const mc_program* p, bool lds_arena) {
-    return scratch_of(p) + (lds_arena ? 2 * (int64_t)dpad_of(p->D) : 0);
-}
-static bool mh_use_lds(const mc_program* p) {
-    return cpb_of(p->wpc) * mh_lds_floats(p, true) * 4 <= kLdsArenaBudget;
-}
-
-extern "C" int64_t mc_mh_workspace_bytes(const mc_program* p, int64_t C) {
-    if (!p || C < 0) return -1;
-    if (mh_use_lds(p)) return 0;
-    return C * 2 * (int64_t)dpad_of(p->D) * 4;
-}
-
-template <int WPC, bool LDS, bool EX>
-static int launch_mh(const mc_program* p, const mc_run_config* cfg, float scale, void* state,
-                     float* samples, const mc_trace* tr, float* ws, hipStream_t st) {
-    int64_t qo, go;
-    mc_state_offsets(p, cfg->num_chains, &qo, &go);
-    char* b = (char*)state;
-    RunArgs A;
-    std::memset(&A, 0, sizeof(A));
-    A.cfg = *cfg;
-    A.dpad = dpad_of(p->D);
-    A.lds_floats = (int32_t)mh_lds_floats(p, LDS);
-    A.scratch_floats = scratch_of(p);
-    const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
-    const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
-    MC_HIP_TRY(allow_lds(k_mh<WPC, LDS, EX>, lds));
-    hipLaunchKernelGGL((k_mh<WPC, LDS, EX>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
-                       ctx_of(p), A, scale, (mc_chain_scalars*)b, (float*)(b + qo), samples,
-                       trace_of(tr), ws);
-    MC_HIP_TRY(hipGetLastError());
-    return MC_OK;
-}
-
-extern "C" int mc_mh_run(const mc_program* p, const mc_run_config* cfg, double proposal_scale,
-                         void* state, float* samples, const mc_trace* tr, void* ws,
-                         int64_t ws_bytes, void* stream) {
-    int rc = check_cfg(p, cfg, state);
-    if (rc) return rc;
-    if (!std::isfinite(proposal_scale)) return fail(MC_ERR_INVALID, "proposal_scale not finite");
-    if (cfg->num_chains == 0 || cfg->iter_count == 0) return MC_OK;
-    const bool lds = mh_use_lds(p);
-    const int64_t need = mc_mh_workspace_bytes(p, cfg->num_chains);
-    if (!lds && (ws == nullptr || ws_bytes < need))
-        return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
-    ws_forget(ws);  // another kernel's data: a later sliced launch clears it
-    hipStream_t st = (hipStream_t)stream;
-    float* w = (float*)ws;
-    const float sc = (float)proposal_scale;  // f32(proposal_scale): MLX's weak scalar
-    return dispatch_tape(p, lds, [&](auto W, auto L, auto E) {
-        return launch_mh<decltype(W)::value, decltype(L)::value, decltype(E)::value>(
-            p, cfg, sc, state, samples, tr, w, st);
-    });
-}
-
-// LDS floats per chain group of k_nuts: group scratch, pending words and,
-// with the LDS arena, the trajectory arena
-static int64_t nuts_lds_floats(const mc_program* p, int32_t max_depth, bool lds_arena) {
-    return scratch_of(p) + kNutsLdsWords +
-           (lds_arena ? nuts_arena_vectors(max_depth) * (int64_t)dpad_of(p->D) : 0);
-}
-// The arena goes to LDS when a workgroup's share fits 150 KB (one workgroup
-// per CU: NUTS runs few chains — 64 per GPU in config 5 — so occupancy is not
-// what bounds it; the L2 round trips of a global arena are)
-static constexpr int64_t kNutsLdsBudget = 150 * 1024;
-static bool nuts_use_lds(const mc_program* p, int32_t max_depth) {
-    return cpb_of(p->wpc) * nuts_lds_floats(p, max_depth, true) * 4 <= kNutsLdsBudget;
-}
-
-extern "C" int64_t mc_nuts_workspace_bytes(const mc_program* p, int64_t C, int32_t max_depth) {
-    if (!p || C < 0 || max_depth < 0 || max_depth > kMaxTreeDepth) return -1;
-    if (nuts_use_lds(p, max_depth)) return 0;
-    return C * nuts_arena_vectors(max_depth) * (int64_t)dpad_of(p->D) * 4;
-}
-
-template <int WPC, bool LDS, bool EX>
-static int launch_nuts(const mc_program* p, const mc_run_config* cfg, void* state,
-                       float* samples, const mc_trace* tr, float* ws, hipStream_t st) {
-    int64_t qo, go;
-    mc_state_offsets(p, cfg->num_chains, &qo, &go);
-    char* b = (char*)state;
-    RunArgs A;
-    std::memset(&A, 0, sizeof(A));
-    A.cfg = *cfg;
-    A.dpad = dpad_of(p->D);
-    A.scratch_floats = scratch_of(p);
-    A.lds_floats = (int32_t)nuts_lds_floats(p, cfg->max_tree_depth, LDS);
-    size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
-    // the data pool after the chain groups when it fits as well
-    const size_t dbytes = (p->h_data.size() + 3) / 4 * 16;
-    A.data_lds = 0;
-    if (LDS && lds + dbytes <= (size_t)kNutsLdsBudget) {
-        A.data_lds = (int32_t)p->h_data.size();
-        lds += dbytes;
-    }
-    const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
-    MC_HIP_TRY(allow_lds(k_nuts<WPC, LDS, EX>, lds));
-    hipLaunchKernelGGL((k_nuts<WPC, LDS, EX>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
-                       ctx_of(p), A, (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go),
-                       samples, trace_of(tr), ws);
-    MC_HIP_TRY(hipGetLastError());
-    return MC_OK;
-}
-
-// The lane-resident NUTS kernel (nuts_lanes.h) for programs planned as one
-// lane-resident slice (the layout k_hmc_lr runs with X1), unless
-// MC_NUTS_LANES=0 in the environment (A/B timing against k_nuts) or the
-// arena does not fit the LDS budget.
-static bool nuts_lanes_enabled() {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = std::getenv("MC_NUTS_LANES");
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
-    return on == 1;
-}
-static size_t nuts_lr_lds_bytes(const mc_program* p, int max_depth) {
-    return (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm) +
-           (size_t)nuts_lr_arena_floats(p->lr.rs, max_depth) * 4;
-}
-static bool use_nuts_lanes(const mc_program* p, int max_depth) {
-    return nuts_lanes_enabled() && p->sl.S < 2 && p->lr.ok && p->lr.S == 1 && !p->lr.has_xf &&
-           p->slice_kernel != 1 && nuts_lr_lds_bytes(p, max_depth) <= (size_t)kSlLdsBudget;
-}
-// no broadcast parameter, no scalar term and one slice term with at most one
-// element per (lane, slot): a data-scale term or a direct term with constant
-// loc and scale (k_nuts_lr<..., 2>: the gradient from per-slot registers)
-static bool lanes_register_only(const mc_program* p) {
-    const LanePlan& L = p->lr;
-    if (!L.ok || L.S != 1 || L.Dsh != 0 || !L.sterms.empty() || L.blocks[2] != 1) return false;
-    const LrTerm& T = L.terms[0];
-    const bool ds = T.sig == LS_DSCALE && T.kind[1 - T.pp] != SK_SHARED;
-    const bool dir = T.sig == LS_PP_C_C && T.pp == 0;
-    if (!ds && !dir) return false;
-    const int32_t* lens = (const int32_t*)&L.data[(size_t)L.blocks[0] + T.len_off];
-    for (int i = 0; i < T.nslot * 64; ++i)
-        if (lens[i] > 1) return false;
-    return true;
-}
-
-extern "C" int32_t mc_program_nuts_lanes(const mc_program* p, int32_t max_tree_depth) {
-    if (!p) return -1;
-    if (!use_nuts_lanes(p, max_tree_depth)) return 0;
-    return lanes_register_only(p) ? 2 : 1;
-}
-
-// every slice term of the one-slice lane plan has a specialised form and
-// every scalar term is an own prior (k_nuts_lr<..., SPEC>)
-static bool lanes_specialised(const mc_program* p) {
-    const LanePlan& L = p->lr;
-    if (L.n_generic != 0 || L.S != 1) return false;
-    const int nact = (int)L.blocks[2];
-    for (int t = 0; t < nact; ++t)
-        if (L.terms[t].sig == LS_GENERIC) return false;
-    return true;
-}
-
-static int g_nuts_variant = -1;  // mc_debug_nuts_variant
-extern "C" int mc_debug_nuts_variant(int variant) {
-    g_nuts_variant = (variant < -1 || variant > 1) ? -1 : variant;
-    return MC_OK;
-}
-
-template <int RS, int NSH>
-static int launch_nuts_lr(const mc_program* p, const mc_run_config* cfg, void* state,
-                          float* samples, const mc_trace* tr, hipStream_t st) {
-    int64_t qo, go;
-    mc_state_offsets(p, cfg->num_chains, &qo, &go);
-    char* b = (char*)state;
-    RunArgs A;
-    std::memset(&A, 0, sizeof(A));
-    A.cfg = *cfg;
-    const size_t lds = nuts_lr_lds_bytes(p, cfg->max_tree_depth);
-    auto kern = lanes_specialised(p) ? k_nuts_lr<RS, NSH, 1> : k_nuts_lr<RS, NSH, 0>;
-    if constexpr (NSH == 3)
-        if (lanes_register_only(p) && g_nuts_variant < 0) kern = k_nuts_lr<RS, NSH, 2>;
-    if (g_nuts_variant == 0) kern = k_nuts_lr<RS, NSH, 0>;
-    MC_HIP_TRY(allow_lds(kern, lds));
-    hipLaunchKernelGGL(kern, dim3((unsigned)cfg->num_chains), dim3(64), lds, st, lrctx_of(p), A,
-                       (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples,
-                       trace_of(tr));
-    MC_HIP_TRY(hipGetLastError());
-    return MC_OK;
-}
-
-extern "C" int mc_nuts_run(const mc_program* p, const mc_run_config* cfg, void* state,
-                           float* samples, const mc_trace* tr, void* ws, int64_t ws_bytes,
-                           void* stream) {
-    int rc = check_cfg(p, cfg, state);
-    if (rc) return rc;
-    if (cfg->max_tree_depth < 0 || cfg->max_tree_depth > kMaxTreeDepth)
-        return fail(MC_ERR_UNSUPPORTED, "max_tree_depth must be in [0, %d]", kMaxTreeDepth);
-    if (cfg->num_chains == 0 || cfg->iter_count == 0) return MC_OK;
-    const int64_t need = mc_nuts_workspace_bytes(p, cfg->num_chains, cfg->max_tree_depth);
-    if (need > 0 && (ws == nullptr || ws_bytes < need))
-        return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
-    if (ws) ws_forget(ws);  // another kernel's data: a later sliced launch clears it
-    hipStream_t st = (hipStream_t)stream;
-    if (use_nuts_lanes(p, cfg->max_tree_depth)) {
-        const bool n4 = p->lr.Dsh > 3;
-        switch (p->lr.rs) {
-            case 1: return n4 ? launch_nuts_lr<1, 4>(p, cfg, state, samples, tr, st)
-                              : launch_nuts_lr<1, 3>(p, cfg, state, samples, tr, st);
-            case 2: return n4 ? launch_nuts_lr<2, 4>(p, cfg, state, samples, tr, st)
-                              : launch_nuts_lr<2, 3>(p, cfg, state, samples, tr, st);
-            default: return n4 ? launch_nuts_lr<4, 4>(p, cfg, state, samples, tr, st)
-                               : launch_nuts_lr<4, 3>(p, cfg, state, samples, tr, st);
-        }
-    }
-    float* w = (float*)ws;
-    const bool lds = nuts_use_lds(p, cfg->max_tree_depth);
-    return dispatch_tape(p, lds, [&](auto W, auto L, auto E) {
-        return launch_nuts<decltype(W)::value, decltype(L)::value, decltype(E)::value>(
-            p, cfg, state, samples, tr, w, st);
-    });
-}
 
 // ---------------------------------------------------------------------------
 // RNG fill (test hook and Distribution.sample)
@@ -2941,25 +2033,6 @@ extern "C" int mc_rng_fill(uint64_t seed, uint32_t chain, uint32_t iter, uint32_
     return MC_OK;
 }
 
-#ifdef MC_STAMPS
-// diagnostic build only: copy out / reset the section stamp accumulators
-extern "C" int mc_debug_stamps(unsigned long long* acc, unsigned long long* cnt, int reset) {
-    if (acc) MC_HIP_TRY(hipMemcpyFromSymbol(acc, HIP_SYMBOL(mc_stamp_acc), sizeof(mc_stamp_acc)));
-    if (cnt) MC_HIP_TRY(hipMemcpyFromSymbol(cnt, HIP_SYMBOL(mc_stamp_cnt), sizeof(mc_stamp_cnt)));
-    if (reset) {
-        unsigned long long z[16 * 32] = {0};
-        MC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mc_stamp_acc), z, sizeof(z)));
-        MC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mc_stamp_cnt), z, sizeof(z)));
-        std::vector<unsigned long long> zw(1024 * 4, 0);
-        MC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mc_stamp_wg), zw.data(), zw.size() * 8));
-    }
-    return MC_OK;
-}
-extern "C" int mc_debug_stamps_wg(unsigned long long* wg) {
-    MC_HIP_TRY(hipMemcpyFromSymbol(wg, HIP_SYMBOL(mc_stamp_wg), 1024 * 4 * 8));
-    return MC_OK;
-}
-#endif
 
 // ---------------------------------------------------------------------------
 // diagnostics (diag.h)

@@ -754,6 +754,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 drift_private(true);
                 sweep(M1, M2);
             }
+            MC_STAMP(8);
             // poll: pass ps reads pair 4 ps + perm[row] of slice col
             const bool kstep = (l == 0) || (l == L - 1);
             const uint32_t need =

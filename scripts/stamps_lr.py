@@ -15,7 +15,7 @@ from mlx_mcmc_amd import _lib  # noqa: E402
 
 _lib.LIB_PATH = os.path.join(ROOT, "scripts", os.environ.get("STAMPS_LIB", "libmcmc355_stamps.so"))
 lib = _lib.load()
-lib.mc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+lib.mc_debug_stamps_lanes.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -54,7 +54,7 @@ cfg = dict(chain_offset=0, num_warmup=0, num_samples=10, sample_begin=0, sample_
 cs.run_hmc(iter_begin=0, iter_count=1, **cfg)
 torch.cuda.synchronize()
 cs.check_status()
-lib.mc_debug_stamps(None, None, 1)
+lib.mc_debug_stamps_lanes(None, None, 1)
 t = time.perf_counter()
 cs.run_hmc(iter_begin=1, iter_count=2, **cfg)
 torch.cuda.synchronize()
@@ -62,7 +62,7 @@ dt = time.perf_counter() - t
 cs.check_status()
 acc = (ctypes.c_ulonglong * (16 * 32))()
 cnt = (ctypes.c_ulonglong * (16 * 32))()
-lib.mc_debug_stamps(acc, cnt, 0)
+lib.mc_debug_stamps_lanes(acc, cnt, 0)
 a = np.array(acc[:], dtype=np.float64).reshape(16, 32)
 c = np.array(cnt[:], dtype=np.float64).reshape(16, 32)
 steps = max(c[0, 1], 1)
@@ -75,8 +75,8 @@ for sec, name in SECS:
     vals = " ".join(f"{a[w, sec] / steps:7.0f}" for w in range(8))
     print(f"  {name:28s} {vals}")
 wg = (ctypes.c_ulonglong * (1024 * 4))()
-lib.mc_debug_stamps_wg.argtypes = [ctypes.c_void_p]
-lib.mc_debug_stamps_wg(wg)
+lib.mc_debug_stamps_lanes_wg.argtypes = [ctypes.c_void_p]
+lib.mc_debug_stamps_lanes_wg(wg)
 wga = np.array(wg[:], dtype=np.float64).reshape(1024, 4) / steps
 # chain block 0's slices (XCD-aware placement: workgroup 8 r holds slice r)
 print("  block 0, wave 0, per slice:  eval / publish / poll")

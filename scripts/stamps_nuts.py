@@ -15,7 +15,7 @@ from mlx_mcmc_amd import _lib  # noqa: E402
 
 _lib.LIB_PATH = os.path.join(ROOT, "scripts", os.environ.get("STAMPS_LIB", "libmcmc355_stamps.so"))
 lib = _lib.load()
-lib.mc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+lib.mc_debug_stamps_nuts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -31,14 +31,14 @@ cfg = dict(chain_offset=0, num_warmup=200, num_samples=100, sample_begin=0, samp
            slice_mode=0)
 cs.run_nuts(iter_begin=0, iter_count=200, **cfg)   # warm up the step size
 torch.cuda.synchronize()
-lib.mc_debug_stamps(None, None, 1)
+lib.mc_debug_stamps_nuts(None, None, 1)
 n0 = cs.scalars()["n_grad"].copy()
 cs.run_nuts(iter_begin=200, iter_count=20, **cfg)
 torch.cuda.synchronize()
 leaves = (cs.scalars()["n_grad"] - n0)[:4]
 acc = (ctypes.c_ulonglong * (16 * 32))()
 cnt = (ctypes.c_ulonglong * (16 * 32))()
-lib.mc_debug_stamps(acc, cnt, 0)
+lib.mc_debug_stamps_nuts(acc, cnt, 0)
 a = np.array(acc[:], dtype=np.float64).reshape(16, 32)
 c = np.array(cnt[:], dtype=np.float64).reshape(16, 32)
 print("leaves (chains 0-3):", leaves)
