@@ -102,6 +102,12 @@ def parse():
                          "set of the same program (its own state, seed and sample buffer); "
                          "same: the sampler kernel on the measured chain set's buffers and "
                          "workspace, its state restored bit-exactly afterwards")
+    ap.add_argument("--nuts-model", default="illcond", choices=["illcond", "hier"],
+                    help="--workload nuts: illcond = BASELINE configs[4]'s 100-dim kappa = 1000 "
+                         "Gaussian; hier = the hierarchical model of --shape (the README rows)")
+    ap.add_argument("--nuts-step-size", type=float, default=None,
+                    help="NUTS initial step size (dual averaging adapts it over the warmup; "
+                         "default 0.1 illcond, 2e-3 hier)")
     ap.add_argument("--workload", default="hmc", choices=["hmc", "nuts"],
                     help="hmc: the headline (BASELINE configs[2]/[3]); nuts: BASELINE "
                          "configs[4] (NUTS depth 10 + dual averaging, 100-dim kappa = 1000 "
@@ -111,6 +117,8 @@ def parse():
         args.ess_step_size = {"large": 2e-3, "medium": 5e-3, "small": 0.01}[args.shape]
     if args.workload == "nuts" and not any(a.startswith("--chains") for a in sys.argv[1:]):
         args.chains = 64
+    if args.nuts_step_size is None:
+        args.nuts_step_size = 0.1 if args.nuts_model == "illcond" else 2e-3
     return args
 
 
@@ -468,7 +476,21 @@ NUTS_D = 100
 NUTS_FLOPS_PER_LEAF = 19 * NUTS_D
 
 
-def nuts_cpu_baseline(budget_s):
+def nuts_model(args, ns):
+    """(log_prob, init, D, flops per leaf, label) of the NUTS line's model."""
+    import workloads as W
+
+    if args.nuts_model == "illcond":
+        lp, init = W.illcond_normal(ns, NUTS_D)
+        return lp, init, NUTS_D, NUTS_FLOPS_PER_LEAF, f"D={NUTS_D} kappa=1000 Gaussian"
+    G, N = W.SHAPES[args.shape]
+    lp, init = W.hierarchical(ns, G, N)
+    # a leaf = one leapfrog step: the gradient's 5N + 13D flops (SURVEY 8d)
+    return (lp, init, G + 3, W.hierarchical_flops_per_step(G, N),
+            f"hierarchical '{args.shape}' D={G + 3}, N={N}")
+
+
+def nuts_cpu_baseline(budget_s, args):
     """The oracle's NUTS (reference cost structure: two gradients per leaf,
     recursive build_tree) on the same model, one chain, one thread: leaves/s."""
     import torch
@@ -477,11 +499,11 @@ def nuts_cpu_baseline(budget_s):
     from oracle import samplers as S
 
     torch.set_num_threads(1)
-    lp, init = W.illcond_normal(W.ns_oracle(), NUTS_D)
+    lp, init, D, _, label = nuts_model(args, W.ns_oracle())
     leaves, t0, runs = 0, time.perf_counter(), 0
     while time.perf_counter() - t0 < budget_s:
-        r = S.nuts(lp, init, num_samples=20, num_warmup=20, step_size=0.1, max_tree_depth=10,
-                   seed=runs)
+        r = S.nuts(lp, init, num_samples=20, num_warmup=20, step_size=args.nuts_step_size,
+                   max_tree_depth=10, seed=runs)
         leaves += int(sum(r.trace["leaves"]))
         runs += 1
     dt = time.perf_counter() - t0
@@ -489,8 +511,8 @@ def nuts_cpu_baseline(budget_s):
             "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
             "sample": (f"oracle/samplers.py NUTS restatement (torch-CPU autograd, 2 gradients per "
                        f"leaf), 1 chain, 1 thread: {runs} runs of 20 warmup + 20 sampling "
-                       f"iterations (depth <= 10) on the same D={NUTS_D} model, {leaves} leaves "
-                       f"in {dt:.1f} s")}
+                       f"iterations (depth <= 10) on the same {label} model, {leaves} leaves "
+                       f"in {dt:.1f} s (a run in progress at the budget's end finishes)")}
 
 
 def main_nuts(args):
@@ -508,13 +530,14 @@ def main_nuts(args):
 
     world, rank, local, dev = init_ranks()
     C, K, Wm, B = args.chains, args.steps, args.warmup, max(1, args.iters_per_launch)
-    lp_fn, init = W.illcond_normal(W.ns_product(), NUTS_D)
+    lp_fn, init, D, flops_per_leaf, label = nuts_model(args, W.ns_product())
     prog = _trace.compile_model(lp_fn, init)
-    chains = _engine.ChainSet(prog, C, prog.layout.flatten(init), 0.1, device=dev)
-    samples = torch.empty((C, max(K, 1), NUTS_D), dtype=torch.float32, device=dev)
+    eps0 = args.nuts_step_size
+    chains = _engine.ChainSet(prog, C, prog.layout.flatten(init), eps0, device=dev)
+    samples = torch.empty((C, max(K, 1), D), dtype=torch.float32, device=dev)
     chain_offset, _ = shard(C * world, world, rank)
     cfg = dict(chain_offset=chain_offset, num_warmup=Wm, num_samples=K, sample_begin=0,
-               sample_capacity=K, seed=args.seed, step_size=0.1, target_accept=0.8,
+               sample_capacity=K, seed=args.seed, step_size=eps0, target_accept=0.8,
                max_tree_depth=10, adapt_step_size=True, slice_mode=0)
 
     def launches(first, count):
@@ -553,16 +576,21 @@ def main_nuts(args):
         value = leaves_all / elapsed
         # per launch: the timed leaves spread over the launches by their time
         leaves_per_launch = leaves * (launch_ms / launch_ms_total) if launch_ms_total else 0.0
-        achieved = leaves_per_launch * NUTS_FLOPS_PER_LEAF / (launch_ms * 1e-3) / 1e12
+        achieved = leaves_per_launch * flops_per_leaf / (launch_ms * 1e-3) / 1e12
+        hier = args.nuts_model == "hier"
         out = {
-            "metric": "leapfrog-steps/sec (all chains), NUTS 100-dim kappa=1000 Gaussian",
+            "metric": ("leapfrog-steps/sec (all chains), NUTS " +
+                       (label if hier else "100-dim kappa=1000 Gaussian")),
             "value": value, "unit": "leaf-steps/s", "n_gpus": world, "steps": K,
             "warmup": Wm, "ms_per_step": elapsed * 1e3 / max(K, 1), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (fixed kappa = 1000 diagonal scales, SURVEY §8d config 5)",
-            "config": {"workload": (f"NUTS depth 10 + dual averaging (BASELINE configs[4]): "
+            "data": ("synthetic (fixed-seed hierarchical Normal data, SURVEY §8d)" if hier else
+                     "synthetic (fixed kappa = 1000 diagonal scales, SURVEY §8d config 5)"),
+            "config": {"workload": (f"NUTS depth 10 + dual averaging on the {label} model, "
+                                    f"{C} chains per GPU" if hier else
+                                    f"NUTS depth 10 + dual averaging (BASELINE configs[4]): "
                                     f"D={NUTS_D}, kappa=1000, {C} chains per GPU"),
-                       "num_params": NUTS_D, "max_tree_depth": 10, "chains_per_gpu": C,
+                       "num_params": D, "max_tree_depth": 10, "chains_per_gpu": C,
                        "total_chains": C * world, "parallelism": f"chains sharded {C}/GPU"},
             "roofline": {
                 "bound": "valu_fp32", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
@@ -572,9 +600,11 @@ def main_nuts(args):
                             "k_nuts_lr (lane-resident, one chain per wave)")
                            if prog.nuts_kernel(10) == "lanes" else f"k_nuts<{prog.waves_per_chain}>"),
                 "launch_ms": launch_ms,
-                "iters_per_launch": B, "flops_per_leaf": NUTS_FLOPS_PER_LEAF,
-                "note": (f"latency bound: {C} chains = {C * prog.waves_per_chain} waves on "
-                         "1024 SIMDs; F = 19 D flops per leaf (SURVEY 8d unit: one leaf)")},
+                "iters_per_launch": B, "flops_per_leaf": flops_per_leaf,
+                "note": (f"{C} chains = {C * prog.waves_per_chain} waves on 1024 SIMDs; "
+                         + ("F = 5N + 13D flops per leaf (one gradient of the hierarchical "
+                            "model)" if hier else "F = 19 D flops per leaf")
+                         + " (SURVEY 8d unit: one leaf)")},
             "leaves": leaves_all, "leaves_rank0": leaves, "mean_tree_depth": float(np.mean(sc["depth_sum"] / np.maximum(
                 sc["n_total"], 1))),
             "accept_stat_mean": float(np.mean(sc["alpha_sum"]) / max(Wm + K, 1)),
@@ -582,7 +612,7 @@ def main_nuts(args):
             "clock_warm_ms": args.clock_warm_ms,
         }
         if world == 1 and not args.no_cpu_baseline:
-            cb = nuts_cpu_baseline(min(args.cpu_seconds, 15.0))
+            cb = nuts_cpu_baseline(min(args.cpu_seconds, 15.0), args)
             cb["gpu_over_cpu"] = value / cb["value"]
             out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)

@@ -49,6 +49,14 @@
 #pragma once
 #include "lanes.h"
 
+// MC_LF_EARLY_POLL (default 0): 1 issues the exchange poll inside the
+// moment sweep (see k_hmc_lf): A/B on one box 83.2 vs 94.7 M steps/s for
+// polling after it (profiles/r4/ab1): a poll issued before the records have
+// landed costs a second round trip
+#ifndef MC_LF_EARLY_POLL
+#define MC_LF_EARLY_POLL 0
+#endif
+
 namespace mc {
 
 // compile-time term forms (FORM bits)
@@ -133,7 +141,17 @@ MC_DEV f2 lf_hi_minus(f2 xy, f2 th) {
 // parameter th) for both chains, packed FP32: d = x - th, s1 += d,
 // s2 = fma(d, d, s2), with the even and odd elements in separate packed
 // accumulators (two independent dependency chains each).
-MC_DEV void lf_moments(const float* xv, int len, int lmin4, int lmax, f2 th, f2& s1, f2& s2) {
+//
+// hook(): called once, at the start of the 16-element round that begins at
+// group `cut` (uniform; a multiple of 4 below lmin4 - 4, else never) — the
+// kernel issues its exchange poll there, so the loads' round trip overlaps
+// the rest of the sweep.
+struct LfNoHook {
+    MC_DEV void operator()() const {}
+};
+template <typename Hook = LfNoHook>
+MC_DEV void lf_moments(const float* xv, int len, int lmin4, int lmax, f2 th, f2& s1, f2& s2,
+                       int cut = -1, Hook&& hook = Hook()) {
     f2 a1[2] = {{0.f, 0.f}, {0.f, 0.f}}, a2[2] = {{0.f, 0.f}, {0.f, 0.f}};
     // a register pair's elements broadcast by swizzle (op_sel on the pair,
     // no copy of the odd register)
@@ -173,11 +191,13 @@ MC_DEV void lf_moments(const float* xv, int len, int lmin4, int lmax, f2 th, f2&
             round(A);
             u4 += 4;
             if (!more_b) break;
+            if (u4 == cut) hook();
             const bool more_a = u4 + 8 <= lmin4;
             load(A, min(u4 + 4, last));
             round(B);
             u4 += 4;
             if (!more_a) break;
+            if (u4 == cut) hook();
         }
     }
     // the groups every lane holds in full (uniform), then the ragged end:
@@ -437,13 +457,28 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
              d_clogs = vpin(bc2(F.d_clogs));
     const f2 half = bc2(0.5f), one = bc2(1.0f);
     const float lp_const = vpin(P.lp_const);
-    // the swept terms' moment sums at the current point, both chains
-    auto sweep = [&](f2 (&s1)[RS], f2 (&s2)[RS]) {
+    // early poll (MC_LF_EARLY_POLL): the sweep issues the exchange poll at
+    // about 3/4 of the last slot with at least 8 full groups in every lane
+    // (uniform), so the loads' L2 round trip overlaps the rest of the sweep
+    // instead of following it; a step without such a slot polls after it
+    int cut_r = -1, cut_u4 = -1;
+#pragma unroll
+    for (int r = 0; r < RS; ++r)
+        if (!X1 && MC_LF_EARLY_POLL && lmin4[r] >= 8) {
+            cut_r = r;
+            // (the hook runs at a round start u4 with u4 + 4 <= lmin4)
+            cut_u4 = min(max(4, ((3 * lmin4[r]) / 4) & ~3), (lmin4[r] - 4) & ~3);
+        }
+    // the swept terms' moment sums at the current point, both chains; hook()
+    // at group cut_u4 of slot cut_r (every lane active there: lmin4 >= 8)
+    auto sweep = [&](f2 (&s1)[RS], f2 (&s2)[RS], auto&& hook) {
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             s1[r] = (f2){0.f, 0.f};
             s2[r] = (f2){0.f, 0.f};
-            if (len[r] > 0) lf_moments(xv[r], len[r], lmin4[r], lmax[r], q[r], s1[r], s2[r]);
+            if (len[r] > 0)
+                lf_moments(xv[r], len[r], lmin4[r], lmax[r], q[r], s1[r], s2[r],
+                           r == cut_r ? cut_u4 : -1, hook);
         }
     };
 
@@ -562,7 +597,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         f2 M1[RS], M2[RS];
         drift_private(false);
         drift_shared(false);
-        sweep(M1, M2);
+        sweep(M1, M2, LfNoHook());
         for (int l = 0; l < L; ++l) {
             MC_STAMP(0);
             const bool lst = l == L - 1;  // log p: the last step only
@@ -748,13 +783,6 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             // A/B on one box 92.0 -> 100.0 M steps/s, the same with priority 1, 2
             // or 3, and with the poll at either level, profiles/r3/ab/ab34)
             __builtin_amdgcn_s_setprio(1);
-            // while the records travel: the private parameters' next position
-            // and the swept terms' sums there
-            if (l + 1 < L) {
-                drift_private(true);
-                sweep(M1, M2);
-            }
-            MC_STAMP(8);
             // poll: pass ps reads pair 4 ps + perm[row] of slice col
             const bool kstep = (l == 0) || (l == L - 1);
             const uint32_t need =
@@ -768,11 +796,22 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             // rewritten before this wave publishes the next one (the line
             // parity alternates per step), so the values of the last load
             // are the record's.
-            auto poll = [&]() {
-                unsigned long long y[NPASS];
+            unsigned long long y[NPASS];
+            auto poll_issue = [&]() {
 #pragma unroll
                 for (int ps = 0; ps < NPASS; ++ps)
                     y[ps] = (ps < NPASS_V || kstep) ? granule_load(gp[par] + 4 * ps) : 0ull;
+            };
+            // while the records travel: the private parameters' next position
+            // and the swept terms' sums there (the first poll issued inside)
+            const bool early = cut_r >= 0 && l + 1 < L;
+            if (l + 1 < L) {
+                drift_private(true);
+                sweep(M1, M2, poll_issue);
+            }
+            MC_STAMP(8);
+            if (!X1 && !early) poll_issue();
+            auto poll_eval = [&]() {
                 bool ready = true;  // (bitwise: lane masks, no branches)
 #pragma unroll
                 for (int ps = 0; ps < NPASS; ++ps) {
@@ -784,7 +823,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 }
                 return ready;
             };
-            bool ready = X1 ? true : poll();
+            bool ready = X1 ? true : poll_eval();
             MC_STAMP(7);
             uint32_t spins = 0;
             while (__ballot(!ready)) {
@@ -793,7 +832,8 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
-                ready = poll();
+                poll_issue();
+                ready = poll_eval();
             }
             if (!ok) {
                 __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

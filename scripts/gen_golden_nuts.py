@@ -6,6 +6,10 @@ test infrastructure, run here on the CPU and committed.
       global chains 0, 1, 33, 63 of the 64-chain launch, seed 0, eps0 = 0.1,
       W = 40 warmup iterations with dual averaging acting, S = 20 sampling
       iterations at eps-bar, max_tree_depth 10.
+  tests/golden/nuts_large_trace.npz
+      The README "Large" hierarchical model (D = 1000, N = 100 K), chains 0,
+      1, 2, seed 0, a fixed step size 2e-3 (adapt_step_size=False), W = 2,
+      S = 10, max_tree_depth 10 (depths 7-8).
   tests/golden/nuts_hier_trace.npz
       The small hierarchical model (workloads.hierarchical, G = 7, N = 1 K:
       broadcast mu, tau, sigma and private theta), chains 0, 2 and 5 (5: the
@@ -18,7 +22,7 @@ alpha, step size, H0, the f32 log U of the slice draw, and the decision
 margins (smallest slice gap |log u + H'|, divergence gap, relative U-turn
 dot; oracle/samplers.py nuts); the S stored draws [S, D].
 
-    python scripts/gen_golden_nuts.py
+    python scripts/gen_golden_nuts.py [illcond hier large]
 """
 import json
 import os
@@ -34,6 +38,12 @@ RUNS = {
                                                     max_tree_depth=10, target_accept=0.65)),
     "hier": dict(chains=(0, 2, 5), cfg=dict(num_warmup=40, num_samples=20, step_size=0.01,
                                          max_tree_depth=10, target_accept=0.65)),
+    # the README "Large" row (D = 1000, N = 100 K) at a fixed step size (no
+    # dual averaging: the trees are then compared without an adaptation that
+    # amplifies alpha rounding into eps): depths 7-8, 127-255 leaves
+    "large": dict(chains=(0, 1, 2), cfg=dict(num_warmup=2, num_samples=10, step_size=2e-3,
+                                          max_tree_depth=10, target_accept=0.65,
+                                          adapt_step_size=False)),
 }
 SEED = 0
 KEYS = ("depth", "leaves", "alpha", "step_size", "energy", "slice_gap", "div_gap",
@@ -45,6 +55,8 @@ def model(name, ns):
 
     if name == "illcond":
         return W.illcond_normal(ns)
+    if name == "large":
+        return W.hierarchical(ns, *W.SHAPES["large"])
     return W.hierarchical(ns, *W.SHAPES["small"])
 
 
@@ -73,10 +85,13 @@ def _run(job):
 def main():
     import numpy as np
 
-    jobs = [(n, c) for n, r in RUNS.items() for c in r["chains"]]
+    only = sys.argv[1:] or list(RUNS)
+    jobs = [(n, c) for n, r in RUNS.items() if n in only for c in r["chains"]]
     with Pool(min(8, len(jobs))) as pool:
         res = pool.map(_run, jobs)
     for name, spec in RUNS.items():
+        if name not in only:
+            continue
         outs = [o for n, c, o in sorted((t for t in res if t[0] == name),
                                         key=lambda t: spec["chains"].index(t[1]))]
         arrays = {k: np.stack([o[k] for o in outs]) for k in KEYS + ("log_u",)}

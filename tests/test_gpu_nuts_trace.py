@@ -191,3 +191,59 @@ def test_nuts_trace_against_oracle(gpu, name, variant):
               f"gap {fx['slice_gap'][j][i]:.3g}, U-turn margin {fx['uturn_margin'][j][i]:.3g})")
         assert same_fx >= MIN_SAME, f"chain {chain}: trees diverge from the fixture at {same_fx}"
     assert max(depths_seen) >= 3, "real trees"
+
+
+def test_nuts_large_shape_against_oracle(gpu):
+    """NUTS on the README "Large" model (D = 1000, N = 100 K; VERDICT r3
+    "Next round" 6): the kernel the automatic plan picks (k_nuts: the model
+    is sliced, not one lane-resident slice) against the oracle's trace at a
+    fixed step size (tests/golden/nuts_large_trace.npz, chains 0-2, depths
+    7-8): trees identical until a near-tie proven by the oracle's own margins
+    (slice / divergence gap or relative U-turn dot within the tie bound of
+    the iteration), H0 within the tie bound before it, alpha within its
+    relative error, stored draws within rtol 1e-4."""
+    import mlx_mcmc_amd as m
+
+    fx = _fixture("large")
+    cfg = fx["config"]
+    lp, init = W.hierarchical(W.ns_product(), *W.SHAPES["large"])
+    s, rate, info = m.nuts(lp, init, num_samples=cfg["num_samples"], num_warmup=cfg["num_warmup"],
+                           step_size=cfg["step_size"], max_tree_depth=cfg["max_tree_depth"],
+                           adapt_step_size=False, target_accept=cfg["target_accept"],
+                           key=m.random.key(cfg["seed"]), num_chains=4, progress=False,
+                           return_info=True, return_trace=True, keep_on_device=True)
+    print("large NUTS kernel:", info.extra["kernel"])
+    n = cfg["num_warmup"] + cfg["num_samples"]
+    tr = info.trace
+    D = info.device_samples.shape[-1]
+    total = 0
+    for j, chain in enumerate(fx["chains"]):
+        chain = int(chain)
+        gd, gl = tr["tree_depth"][chain], tr["n_leapfrog"][chain]
+        np.testing.assert_array_equal(tr["step_size"][chain][:n].astype(np.float32),
+                                      np.float32(cfg["step_size"]))
+        same = _first_flip(gd, gl, fx["depth"][j], fx["leaves"][j], n)
+        h_drift = np.abs(tr["energy"][chain][:n].astype(np.float64) - fx["energy"][j][:n])
+        ties = np.array([8 * _ulp(_hscale(fx["energy"][j][i], D)) + 4 * h_drift[i]
+                         for i in range(n)])
+        print(f"large chain {chain}: trees identical for {same} of {n} iterations, depths "
+              f"{fx['depth'][j][:same].tolist()}, H0 drift max {h_drift[:same].max():.3g}")
+        if same < n:
+            i = same
+            tie_dot = 1e-5 + 4 * h_drift[i] / max(abs(fx["energy"][j][i]), 1.0)
+            assert (fx["slice_gap"][j][i] <= ties[i] or fx["div_gap"][j][i] <= ties[i]
+                    or fx["uturn_margin"][j][i] <= tie_dot), (
+                f"chain {chain}: trees differ at {i} without a near-tie (gpu {gd[i]}/{gl[i]}, "
+                f"oracle {fx['depth'][j][i]}/{fx['leaves'][j][i]})")
+        # H0 of the compared iterations: the positions' fp32 summation order only
+        assert np.all(h_drift[:same] <= 1e-5 * (np.abs(fx["energy"][j][:same]) + D)), h_drift
+        ga = tr["accept_stat"][chain][:same].astype(np.float64)
+        ra = fx["alpha"][j][:same]
+        assert np.all(np.abs(ga - ra) <= ra * np.expm1(ties[:same]) + 1e-5), (ga, ra)
+        ns = max(0, same - cfg["num_warmup"])
+        np.testing.assert_allclose(info.device_samples[chain, :ns].cpu().numpy(),
+                                   fx["samples"][j][:ns], rtol=1e-4, atol=1e-5)
+        total += same
+        assert same >= 6, f"chain {chain}: compared only {same}"
+        assert fx["depth"][j][:same].max() >= 7
+    print("large NUTS: identical trees over", total, "chain-iterations")
