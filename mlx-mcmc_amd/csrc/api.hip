@@ -210,9 +210,10 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = n
     if (has_expr(p))
         return fail(MC_ERR_UNSUPPORTED, "expression terms run on the chain-per-workgroup "
                     "kernels (not sliceable)");
-    if (has_affine(p))
-        return fail(MC_ERR_UNSUPPORTED, "affine loc operands run on the chain-per-workgroup "
-                    "kernels (not sliceable)");
+    if (has_affine(p) && !affine_lanes_ok(p))
+        return fail(MC_ERR_UNSUPPORTED, "affine loc operands other than `loc + b * x` over "
+                    "data x (x a parameter vector, a non-Normal term, a per-element scale) run "
+                    "on the chain-per-workgroup kernels (not sliceable)");
     const bool xf = has_transform(p);
     if (xf && !transform_on_shared_only(p))
         return fail(MC_ERR_UNSUPPORTED, "transformed parameter operands (mx.exp / mx.log) of "
@@ -234,9 +235,11 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = n
             }
     // shared (broadcast) parameters and the private parameters' costs
     std::vector<char> shared(D, 0);
-    for (const DevTerm& t : raw)
+    for (const DevTerm& t : raw) {
         for (int a = 0; a < 3; ++a)
             if (t.op[a].kind == MC_OP_PSCALAR) shared[t.op[a].poff] = 1;
+        if (t.affine && t.ab.kind == MC_OP_PSCALAR) shared[t.ab.poff] = 1;  // the slope
+    }
     std::vector<int64_t> cost(D, 1);
     for (int t = 0; t < nT; ++t)
         if (ppr[t] >= 0)
@@ -705,6 +708,25 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         rs = std::max(rs, need);
     }
     if (rs == 3) rs = 4;
+    // replication (lanes.h LrCtx::rep): with at most 32 private parameters per
+    // slice, each is dealt to a group of `rep` lanes (the largest power of two
+    // <= 16 that still fits every parameter) and its elements are split over
+    // the group: a lone wave's sweep runs n / rep elements instead of n (the
+    // README "Small" shape: 7 groups of ~143 observations, 7 busy lanes of 64).
+    // MC_LANES_REP=<k> caps it (1: off; A/B and tests).
+    int rep = 1;
+    if (rs == 1) {
+        size_t maxp = 1;
+        for (int s = 0; s < S; ++s) maxp = std::max(maxp, part.priv[s].size());
+        int np2 = 1;
+        while ((size_t)np2 < maxp) np2 <<= 1;
+        rep = std::max(1, std::min(16, 64 / np2));
+        if (const char* e = std::getenv("MC_LANES_REP")) {
+            const int cap = std::atoi(e);
+            while (rep > 1 && rep > cap) rep >>= 1;
+        }
+    }
+    const int ngroups = 64 / rep;
     for (int t = 0; t < nT; ++t) {
         if (part.scalar[t] || part.ppr[t] < 0) continue;
         for (int64_t i = 0; i < raw[t].n; ++i)
@@ -712,6 +734,7 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
                 return no("a per-element operand reads a broadcast parameter");
     }
     L.rs = rs;
+    L.rep = rep;
     L.S = S;
     L.Dsh = SP.Dsh;
     L.nitems = SP.nitems;
@@ -737,16 +760,18 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         std::vector<int> ord(pv.size());
         std::iota(ord.begin(), ord.end(), 0);
         std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cost[a] > cost[b]; });
-        std::vector<int64_t> load(64, 0);
-        std::vector<int> used(64, 0);
+        // (lane groups of `rep` lanes; lane_of = the group's leader lane)
+        std::vector<int64_t> load(ngroups, 0);
+        std::vector<int> used(ngroups, 0);
         for (int k : ord) {
             int best = -1;
-            for (int l = 0; l < 64; ++l)
+            for (int l = 0; l < ngroups; ++l)
                 if (used[l] < rs && (best < 0 || load[l] < load[best])) best = l;
-            lane_of[pv[k]] = best;
+            lane_of[pv[k]] = best * rep;
             slot_of_p[pv[k]] = used[best]++;
             load[best] += cost[k];
-            L.gidx[((size_t)s * kLrMaxSlots + slot_of_p[pv[k]]) * 64 + best] = pv[k];
+            for (int x = 0; x < rep; ++x)
+                L.gidx[((size_t)s * kLrMaxSlots + slot_of_p[pv[k]]) * 64 + best * rep + x] = pv[k];
         }
         // ---- terms: the swept ones (lanes.h kLrSweep) first ----
         while (L.data.size() % 4) L.data.push_back(0.0f);
@@ -794,11 +819,21 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
                 else if (a == SK_PP && b == SK_DATA && c == SK_SHARED) lt.sig = LS_PP_DATA_SH;
                 else if (a == SK_DATA && b == SK_SHARED && c == SK_SHARED) lt.sig = LS_DATA_SH_SH;
             }
+            // an affine loc (loc + b * x over data x): lanes.h lr_affine_term
+            if (rt.affine) {
+                if (rt.dist != MC_DIST_NORMAL || lt.mode != 0 || lt.kind[0] != SK_DATA ||
+                    rt.ax.kind != MC_OP_DATA)
+                    return no("an affine loc the lane kernels do not take");
+                lt.sig = LS_AFF;
+                lt.kb = rt.ab.kind == MC_OP_PSCALAR ? SK_SHARED : SK_CONST;
+                lt.jb = rt.ab.kind == MC_OP_PSCALAR ? part.jsh[rt.ab.poff] : 0;
+                lt.cb = rt.ab.kind == MC_OP_CONST ? rt.ab.cval : 0.0f;
+            }
             // Normal with a per-element data scale, one of value / loc private
             // (theta ~ N(m, s_i), y_i ~ N(theta_g, s_i)): lanes.h lr_dscale_term
             if (rt.dist == MC_DIST_NORMAL && lt.kind[2] == SK_DATA && lt.pp >= 0 && lt.pp <= 1 &&
                 lt.kind[lt.pp] == SK_PP && lt.kind[1 - lt.pp] != SK_PP &&
-                lt.kind[1 - lt.pp] != SK_NONE)
+                lt.kind[1 - lt.pp] != SK_NONE && !rt.affine)
                 lt.sig = LS_DSCALE;
             // element lists per (slot, lane), in element order
             std::vector<std::vector<int64_t>> lists((size_t)kLrMaxSlots * 64);
@@ -810,6 +845,22 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
                     lists[(size_t)r * 64 + lane_of[g]].push_back(i);
                     nslot = std::max(nslot, r + 1);
                 }
+                // a replicated parameter's elements: near-equal contiguous
+                // chunks over its group (a lone element stays with the leader)
+                if (rep > 1)
+                    for (int r = 0; r < nslot; ++r)
+                        for (int l0 = 0; l0 < 64; l0 += rep) {
+                            std::vector<int64_t> all;
+                            all.swap(lists[(size_t)r * 64 + l0]);
+                            const int64_t n = (int64_t)all.size();
+                            int64_t f = 0;
+                            for (int x = 0; x < rep; ++x) {
+                                const int64_t len = n / rep + (x < n % rep ? 1 : 0);
+                                lists[(size_t)r * 64 + l0 + x].assign(all.begin() + f,
+                                                                       all.begin() + f + len);
+                                f += len;
+                            }
+                        }
             } else {  // chunk term: contiguous near-equal chunks over the lanes (slot 0)
                 const int64_t nE = (int64_t)E.size(), nch = std::min<int64_t>(64, nE);
                 int64_t f = 0;
@@ -836,12 +887,12 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
                 lt.lmin4[r] = lmax > 0 ? (int32_t)(lmin / 4) : 0;
                 tot += 64 * ((lmax + 3) / 4 * 4);
             }
-            for (int a = 0; a < 3; ++a) {
-                if (lt.kind[a] != SK_DATA) continue;
+            for (int a = 0; a < 4; ++a) {  // (a = 3: an affine term's x)
+                if (a < 3 ? lt.kind[a] != SK_DATA : lt.sig != LS_AFF) continue;
                 while (L.data.size() % 4) L.data.push_back(0.0f);
                 const int64_t base = (int64_t)L.data.size();
                 L.data.resize(base + tot, 0.0f);
-                const int64_t src = rt.op[a].pool;
+                const int64_t src = a < 3 ? rt.op[a].pool : rt.ax.pool;
                 for (int r = 0; r < nslot; ++r)
                     for (int l = 0; l < 64; ++l) {
                         const std::vector<int64_t>& li = lists[(size_t)r * 64 + l];
@@ -849,7 +900,8 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
                             L.data[base + lt.toff[r] + (u >> 2) * 256 + 4 * l + (u & 3)] =
                                 dp[src + li[u]];
                     }
-                lt.doff[a] = (int32_t)(base - blk0);
+                if (a < 3) lt.doff[a] = (int32_t)(base - blk0);
+                else lt.xoff = (int32_t)(base - blk0);
             }
             if (lt.sig == LS_DSCALE) {
                 // the scale tile becomes 1/s^2 and the private operand's (free)
@@ -975,7 +1027,8 @@ static int64_t program_elements(const mc_program* p) {
 // stay unsliced (a per-step exchange costs more than the whole evaluation).
 static constexpr int64_t kLrAutoMinElements = 2048;
 static int auto_slices(const mc_program* p) {
-    if (has_expr(p) || has_affine(p) || (has_transform(p) && !transform_on_shared_only(p)))
+    if (has_expr(p) || (has_affine(p) && !affine_lanes_ok(p)) ||
+        (has_transform(p) && !transform_on_shared_only(p)))
         return 1;
     const int64_t n = program_elements(p);
     if (n >= 65536) return 16;
@@ -1073,11 +1126,12 @@ extern "C" int mc_program_set_slices(mc_program* p, int32_t S) {
         free_lanes(LP);
         LP.why = why;
         p->note = "lane-resident kernel: " + why;
-        if (has_transform(p)) {  // the term interpreter has no transforms
+        if (!interp_ok(p)) {  // the term interpreter has no transforms / affine locs
             free_slices(p->sl);
             if (!automatic)
                 return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: %s (a program with "
-                            "transformed operands is sliced onto it only)", why.c_str());
+                            "transformed operands or affine locs is sliced onto it only)",
+                            why.c_str());
             return MC_OK;
         }
         if (automatic && program_elements(p) < 16384) {  // only worth it on the lanes kernel
@@ -1106,9 +1160,9 @@ extern "C" int mc_program_set_slice_kernel(mc_program* p, int32_t kernel) {
     }
     if (kernel == 2 && !p->lr.ok)
         return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: %s", p->lr.why.c_str());
-    if (kernel == 1 && has_transform(p))
+    if (kernel == 1 && !interp_ok(p))
         return fail(MC_ERR_UNSUPPORTED, "the term interpreter does not run transformed operands "
-                    "(mx.exp / mx.log) or identity terms");
+                    "(mx.exp / mx.log), identity terms or affine locs");
     p->slice_kernel = kernel;
     return MC_OK;
 }

@@ -43,7 +43,7 @@ namespace mc {
 #ifdef MC_STAMPS
 __device__ unsigned long long mc_stamp_acc[16 * 32];  // [wave][section]
 __device__ unsigned long long mc_stamp_cnt[16 * 32];
-__device__ unsigned long long mc_stamp_wg[1024 * 4];  // [workgroup][section 0..3], wave 0
+__device__ unsigned long long mc_stamp_wg[1024 * 16];  // [workgroup][section 0..15], wave 0
 struct StampClock {
     unsigned long long last;
 };
@@ -75,7 +75,7 @@ MC_DEV void stamp(StampClock& c, int sec) {
 MC_DEV void stamp_flush() {
     if (threadIdx.x == 0 && blockIdx.x < 1024) {
         const unsigned long long* a = mc_stamp_lds();
-        for (int s = 0; s < 4; ++s) mc_stamp_wg[blockIdx.x * 4 + s] += a[s];
+        for (int s = 0; s < 16; ++s) mc_stamp_wg[blockIdx.x * 16 + s] += a[s];
     }
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && threadIdx.x < 16 * 64) {
         const unsigned long long* a = mc_stamp_lds();

@@ -90,6 +90,7 @@ struct LanePlan {
                          // and distinct shared roles (compile-time k_hmc_lf), else -1
     int32_t shxf[kLrMaxShared] = {0, 0, 0, 0};  // transforms of the shared parameters
     float shid[kLrMaxShared] = {0.f, 0.f, 0.f, 0.f};  // raw identity weights (k_hmc_lf)
+    int rep = 1;         // lanes per private parameter (lanes.h LrCtx::rep)
     int has_xf = 0;      // a shared parameter is transformed, or an identity term
                          // (no NUTS lanes, no term interpreter)
     std::string why;     // why it does not qualify
@@ -196,7 +197,7 @@ inline bool has_transform(const mc_program* p) {
 // (lanes.h LrCtx::shxf); anything else runs on the chain-per-workgroup kernels.
 inline bool transform_on_shared_only(const mc_program* p) {
     for (const DevTerm& t : p->raw) {
-        if (t.affine) return false;
+        if (t.affine && (t.ab.xf != MC_XF_NONE || t.ax.xf != MC_XF_NONE)) return false;
         for (int a = 0; a < 3; ++a)
             if (t.op[a].xf != MC_XF_NONE && t.op[a].kind != MC_OP_PSCALAR) return false;
         if (t.dist == MC_DIST_IDENTITY && t.op[0].kind != MC_OP_PSCALAR &&
@@ -205,6 +206,29 @@ inline bool transform_on_shared_only(const mc_program* p) {
     }
     return true;
 }
+// Affine terms the lane-resident kernels take (lanes.h LS_AFF): Normal, value
+// data, loc private (a parameter vector or gather), shared or constant, slope
+// shared or constant, x data, no transform on the slope or x.  Any other
+// affine term (x a parameter vector: the non-centred mu + tau * z) keeps the
+// program on the chain-per-workgroup kernels.
+inline bool affine_lanes_ok(const mc_program* p) {
+    for (const DevTerm& t : p->raw) {
+        if (!t.affine) continue;
+        if (t.dist != MC_DIST_NORMAL || t.op[0].kind != MC_OP_DATA) return false;
+        if (t.ax.kind != MC_OP_DATA || t.ax.xf != MC_XF_NONE) return false;
+        if (!(t.ab.kind == MC_OP_PSCALAR || t.ab.kind == MC_OP_CONST) || t.ab.xf != MC_XF_NONE)
+            return false;
+        const int k1 = t.op[1].kind, k2 = t.op[2].kind;
+        if (!(k1 == MC_OP_PVEC || k1 == MC_OP_GATHER || k1 == MC_OP_PSCALAR || k1 == MC_OP_CONST))
+            return false;
+        if (!(k2 == MC_OP_PSCALAR || k2 == MC_OP_CONST)) return false;
+    }
+    return true;
+}
+// The term interpreter (k_hmc_sl) takes neither transformed operands nor
+// affine locs: such sliced programs run on the lane-resident kernels only.
+inline bool interp_ok(const mc_program* p) { return !has_transform(p) && !has_affine(p); }
+
 inline LrCtx lrctx_of(const mc_program* p) {
     LrCtx c;
     std::memset(&c, 0, sizeof(c));
@@ -229,6 +253,7 @@ inline LrCtx lrctx_of(const mc_program* p) {
         c.shid[k] = L.shid[k];
     }
     c.has_xf = L.has_xf;
+    c.rep = L.rep;
     return c;
 }
 // ---------------------------------------------------------------------------
@@ -497,13 +522,13 @@ inline bool lanes_forms_enabled() {
             unsigned long long z[16 * 32] = {0};                                           \
             MC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mc_stamp_acc), z, sizeof(z)));          \
             MC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mc_stamp_cnt), z, sizeof(z)));          \
-            std::vector<unsigned long long> zw(1024 * 4, 0);                               \
+            std::vector<unsigned long long> zw(1024 * 16, 0);                               \
             MC_HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(mc_stamp_wg), zw.data(), zw.size() * 8)); \
         }                                                                                  \
         return MC_OK;                                                                      \
     }                                                                                      \
     extern "C" int WGNAME(unsigned long long* wg) {                                        \
-        MC_HIP_TRY(hipMemcpyFromSymbol(wg, HIP_SYMBOL(mc_stamp_wg), 1024 * 4 * 8));          \
+        MC_HIP_TRY(hipMemcpyFromSymbol(wg, HIP_SYMBOL(mc_stamp_wg), 1024 * 16 * 8));          \
         return MC_OK;                                                                      \
     }
 #endif

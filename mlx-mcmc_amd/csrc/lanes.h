@@ -56,6 +56,12 @@ struct LrTerm {
     int32_t lmin4[kLrMaxSlots];  // per slot: min (over lanes with elements) length / 4
     int32_t len_off;             // int32 [nslot][64] run lengths (slice block)
     int32_t sig;                 // LS_*: a specialised form, or LS_GENERIC
+    // LS_AFF (affine loc: loc + b * x): the slope's kind (SK_SHARED / SK_CONST),
+    // shared ordinal and constant, and the float offset of x's tile (its
+    // elements tiled as the value's)
+    int32_t kb, jb;
+    float cb;
+    int32_t xoff;
 };
 
 // Specialised term forms (Normal, broadcast scale, moment sums) with their
@@ -70,6 +76,9 @@ enum : int32_t {
     LS_DATA_SH_SH = 6,   // y ~ Normal(mu, sigma)              chunked likelihood
     LS_DSCALE = 7,       // theta ~ Normal(m, s_i), y_i ~ Normal(theta_g, s_i): a per-element
                          // data scale (tiles of 1/s^2 and log s), one of value / loc private
+    LS_AFF = 8,          // y ~ Normal(loc + b * x, sigma): an affine loc (mc_affine) over
+                         // data x; loc private (alpha[g]), shared or constant, b shared or
+                         // constant, a broadcast scale (lr_affine_term)
 };
 
 // A scalar term (constants and shared parameters only), compact for LDS.
@@ -112,9 +121,41 @@ struct LrCtx {
     float shid[kLrMaxShared];    // k_hmc_lf: the weights of the identity terms
                                  // over the raw parameter (its log-Jacobian)
     int32_t has_xf;              // a transform or an identity term (k_hmc_lf)
+    int32_t rep;                 // lanes per private parameter (1, 2, 4, 8 or 16):
+                                 // a parameter's elements are split over the
+                                 // `rep` lanes of its group (lanes j & ~(rep-1)
+                                 // .. + rep-1), every lane of the group holds
+                                 // its q, p, g; the group leader alone counts it
+                                 // in kinetic energies, U-turn dots and stores
 };
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Sum over the `rep` lanes of this lane's group (rep in {1, 2, 4, 8, 16},
+// uniform): an xor / mirror butterfly of DPP row operations, so every lane of
+// a group computes the same additions in the same order and holds the same
+// bits (a + b == b + a in IEEE arithmetic).  The private gradients of a
+// replicated layout (LrCtx::rep) are the sums of the lanes' partials.
+template <int LEVELS>
+MC_DEV void grp_levels(float& a, float& b) {
+    // quad_perm [1,0,3,2] (lanes 2i <-> 2i+1), quad_perm [2,3,0,1] (the halves
+    // of a quad), row_half_mirror (the quads of 8 lanes), row_mirror (the
+    // halves of a 16-lane row); two independent chains interleaved
+    if (LEVELS >= 1) { a += dpp_row<0xB1>(a); b += dpp_row<0xB1>(b); }
+    if (LEVELS >= 2) { a += dpp_row<0x4E>(a); b += dpp_row<0x4E>(b); }
+    if (LEVELS >= 3) { a += dpp_row<0x141>(a); b += dpp_row<0x141>(b); }
+    if (LEVELS >= 4) { a += dpp_row<0x140>(a); b += dpp_row<0x140>(b); }
+}
+// two values at once (one uniform switch, straight-line code per case)
+MC_DEV void grp_sum2(float& a, float& b, int rep) {
+    switch (rep) {
+        case 2: grp_levels<1>(a, b); break;
+        case 4: grp_levels<2>(a, b); break;
+        case 8: grp_levels<3>(a, b); break;
+        case 16: grp_levels<4>(a, b); break;
+        default: break;
+    }
+}
 
 MC_DEV f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
@@ -460,6 +501,95 @@ MC_DEV void lr_dscale_term(const MC_CONST LrTerm* T, const float* sd, int j, LrP
     }
 }
 
+// An affine-loc Normal term (LS_AFF; reference: the user's `alpha[g] + beta *
+// x` or `a + b * x` as the loc of Normal(...).log_prob(y), hmc.py:53-67
+// differentiated by mx.grad): per element, both chains packed,
+//   m = loc + b * x (two f32 roundings, as the tape's strided_generic),
+//   d = y - m, s1 += d, s2 = fma(d, d, s2), sx = fma(x, d, sx)
+// (5 packed ops + 1 for m), then with the scale's 1/s, 1/s^2, log s:
+//   log p += w (n (c0 - log s) - (0.5 s2) / s^2),
+//   d/dloc = w s1 / s^2 (private: complete in the lane; shared: a partial),
+//   d/db = w sx / s^2, d/ds = w (s2 / s^2 - n) / s.
+// The loc is private (the lane's slot parameter: a grouped term tiled by
+// group) or a chunk term's shared / constant value.
+template <int RS, int K1>
+MC_DEV void lr_affine_term(const MC_CONST LrTerm* T, const float* sd, int j, LrPriv<RS>& R,
+                           const LrShared& sh, float (&lpp)[2],
+                           float (&gshp)[kLrMaxShared][2]) {
+    const int nslot = T->nslot;
+    const f2 w = f2s(T->weight), c0 = f2s(T->c0), half = f2s(0.5f);
+    const int j1 = T->jsh[1], j2 = T->jsh[2], jb = T->jb;
+    const bool shs = T->kind[2] == SK_SHARED, shb = T->kb == SK_SHARED;
+    const int32_t* lens = (const int32_t*)sd + T->len_off;
+    const f2 um = (K1 == SK_SHARED) ? (f2){rl(sh.v, 2 * j1), rl(sh.v, 2 * j1 + 1)}
+                                    : f2s(T->cval[1]);
+    const f2 b = shb ? (f2){rl(sh.v, 2 * jb), rl(sh.v, 2 * jb + 1)} : f2s(T->cb);
+    const f2 is = shs ? (f2){rl(sh.is, 2 * j2), rl(sh.is, 2 * j2 + 1)} : f2s(T->cinv);
+    const f2 iv = shs ? (f2){rl(sh.iv, 2 * j2), rl(sh.iv, 2 * j2 + 1)} : f2s(T->cinv2);
+    const f2 lg = shs ? (f2){rl(sh.lg, 2 * j2), rl(sh.lg, 2 * j2 + 1)} : f2s(T->clogs);
+    f2 lp = {0.f, 0.f}, pm = {0.f, 0.f}, pb = {0.f, 0.f}, ps = {0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+        if (r >= nslot) break;
+        const int len = lens[r * 64 + j];
+        if (len <= 0) continue;
+        const int toff = T->toff[r] + 4 * j;
+        const float* yv = sd + T->doff[0] + toff;
+        const float* xv = sd + T->xoff + toff;
+        const f2 mm = (K1 == SK_PP) ? (f2){R.q[r][0], R.q[r][1]} : um;
+        f2 s1 = {0.f, 0.f}, s2 = {0.f, 0.f}, sx = {0.f, 0.f};
+        auto elem = [&](float y, float x) {
+            const f2 xx = f2s(x);
+            const f2 m = mm + b * xx;
+            const f2 d = f2s(y) - m;
+            s1 += d;
+            s2 = pk_fma(d, d, s2);
+            sx = pk_fma(xx, d, sx);
+        };
+        int u = 0;
+        for (; u + 4 <= len; u += 4) {
+            const float4 Y = *(const float4*)(yv + (u >> 2) * 256);
+            const float4 X = *(const float4*)(xv + (u >> 2) * 256);
+            elem(Y.x, X.x);
+            elem(Y.y, X.y);
+            elem(Y.z, X.z);
+            elem(Y.w, X.w);
+        }
+        for (; u < len; ++u) {
+            const int o = (u >> 2) * 256 + (u & 3);
+            elem(yv[o], xv[o]);
+        }
+        const f2 cnt = f2s((float)len);
+        lp += w * (cnt * (c0 - lg) - (half * s2) * iv);
+        const f2 t = w * (s1 * iv);
+        if (K1 == SK_PP) {
+            R.g[r][0] += t[0];
+            R.g[r][1] += t[1];
+        } else {
+            pm += t;
+        }
+        pb += w * (sx * iv);
+        ps += w * ((s2 * iv - cnt) * is);
+    }
+    lpp[0] += lp[0];
+    lpp[1] += lp[1];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        if (K1 == SK_SHARED) add4(gshp, j1, c, pm[c]);
+        if (shb) add4(gshp, jb, c, pb[c]);
+        if (shs) add4(gshp, j2, c, ps[c]);
+    }
+}
+
+// one affine term, by its loc's kind
+template <int RS>
+MC_DEV void lr_affine(const MC_CONST LrTerm* T, const float* sd, int j, LrPriv<RS>& R,
+                      const LrShared& sh, float (&lpp)[2], float (&gshp)[kLrMaxShared][2]) {
+    if (T->kind[1] == SK_PP) lr_affine_term<RS, SK_PP>(T, sd, j, R, sh, lpp, gshp);
+    else if (T->kind[1] == SK_SHARED) lr_affine_term<RS, SK_SHARED>(T, sd, j, R, sh, lpp, gshp);
+    else lr_affine_term<RS, SK_CONST>(T, sd, j, R, sh, lpp, gshp);
+}
+
 // Log p partial of this slice at the current point; private gradients
 // (complete) into R.g, this lane's shared-cotangent partials into gshp.
 template <int RS>
@@ -489,6 +619,9 @@ MC_DEV void lr_eval(const MC_CONST LrTerm* tt, int t0, int nact, const float* sd
                 continue;
             case LS_DSCALE:
                 lr_dscale_term<RS>(T, sd, j, R, sh, lpp, gshp);
+                continue;
+            case LS_AFF:
+                lr_affine<RS>(T, sd, j, R, sh, lpp, gshp);
                 continue;
             default:
                 break;
@@ -789,6 +922,8 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     for (int k = 1; k < kLrMaxShared; ++k) xg = (xk == k) ? P.shl[k] : xg;
     const int64_t xch_id = xc ? cc[1] : cc[0];
     const bool xlive = xon && (xc ? live[1] : live[0]);
+    const int rep = P.rep;                     // lanes per private parameter
+    const bool lead = (j & (rep - 1)) == 0;    // this lane counts its parameters
     int xxf = P.shxf[0];  // the lane's parameter's transform
 #pragma unroll
     for (int k = 1; k < kLrMaxShared; ++k) xxf = (xk == k) ? P.shxf[k] : xxf;
@@ -911,7 +1046,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             for (int c = 0; c < 2; ++c) {
                 const float z = normal_of(gk[r], cc[c]);
                 R.p[r][c] = z;
-                k0p[c] += z * z;
+                if (lead) k0p[c] += z * z;
             }
         }
         sh.p = xon ? normal_of(xg, xch_id) : 0.0f;
@@ -979,6 +1114,10 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             lr_finish<RS>(tt, nsweep, ndirect, R, sh, M, KC, lpp2, gshp);
             float lpp[2] = {lpp2[0], lpp2[1]};
             lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp);
+            if (rep > 1) {  // a replicated parameter's gradient: its lanes' partials
+#pragma unroll
+                for (int r = 0; r < RS; ++r) grp_sum2(R.g[r][0], R.g[r][1], rep);
+            }
             MC_STAMP(1);
             // the wave totals of the record, pair-indexed (2 item + chain)
             float rec[NPAIR];
@@ -996,7 +1135,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 for (int x = 0; x < 8; ++x) rec[x] = t8[x];
                 // the 4th shared parameter and the final kinetic partial
                 float k1p[2] = {0.f, 0.f};
-                if (l == L - 1) {
+                if (l == L - 1 && lead) {
 #pragma unroll
                     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -1187,7 +1326,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     float* out = samples + (cc[c] * cfg.sample_capacity + s) * (int64_t)D;
 #pragma unroll
                     for (int r = 0; r < RS; ++r)
-                        if (gk[r] >= 0) out[gk[r]] = R.q[r][c];
+                        if (gk[r] >= 0 && lead) out[gk[r]] = R.q[r][c];
                 }
                 if (slice == 0 && xlive)
                     samples[(xch_id * cfg.sample_capacity + s) * (int64_t)D + xg] = sh.q;
@@ -1204,7 +1343,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         if (!live[c]) continue;
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
-            if (gk[r] >= 0) {
+            if (gk[r] >= 0 && lead) {
                 st_q[cc[c] * D + gk[r]] = R.q[r][c];
                 st_g[cc[c] * D + gk[r]] = R.g[r][c];
             }

@@ -47,15 +47,9 @@
 // Results equal k_hmc_lr's up to fp32 summation order; runs are
 // bit-reproducible and independent of how chains are split over launches.
 #pragma once
-#include "lanes.h"
+#include <type_traits>
 
-// MC_LF_EARLY_POLL (default 0): 1 issues the exchange poll inside the
-// moment sweep (see k_hmc_lf): A/B on one box 83.2 vs 94.7 M steps/s for
-// polling after it (profiles/r4/ab1): a poll issued before the records have
-// landed costs a second round trip
-#ifndef MC_LF_EARLY_POLL
-#define MC_LF_EARLY_POLL 0
-#endif
+#include "lanes.h"
 
 namespace mc {
 
@@ -141,17 +135,7 @@ MC_DEV f2 lf_hi_minus(f2 xy, f2 th) {
 // parameter th) for both chains, packed FP32: d = x - th, s1 += d,
 // s2 = fma(d, d, s2), with the even and odd elements in separate packed
 // accumulators (two independent dependency chains each).
-//
-// hook(): called once, at the start of the 16-element round that begins at
-// group `cut` (uniform; a multiple of 4 below lmin4 - 4, else never) — the
-// kernel issues its exchange poll there, so the loads' round trip overlaps
-// the rest of the sweep.
-struct LfNoHook {
-    MC_DEV void operator()() const {}
-};
-template <typename Hook = LfNoHook>
-MC_DEV void lf_moments(const float* xv, int len, int lmin4, int lmax, f2 th, f2& s1, f2& s2,
-                       int cut = -1, Hook&& hook = Hook()) {
+MC_DEV void lf_moments(const float* xv, int len, int lmin4, int lmax, f2 th, f2& s1, f2& s2) {
     f2 a1[2] = {{0.f, 0.f}, {0.f, 0.f}}, a2[2] = {{0.f, 0.f}, {0.f, 0.f}};
     // a register pair's elements broadcast by swizzle (op_sel on the pair,
     // no copy of the odd register)
@@ -191,13 +175,11 @@ MC_DEV void lf_moments(const float* xv, int len, int lmin4, int lmax, f2 th, f2&
             round(A);
             u4 += 4;
             if (!more_b) break;
-            if (u4 == cut) hook();
             const bool more_a = u4 + 8 <= lmin4;
             load(A, min(u4 + 4, last));
             round(B);
             u4 += 4;
             if (!more_a) break;
-            if (u4 == cut) hook();
         }
     }
     // the groups every lane holds in full (uniform), then the ragged end:
@@ -362,6 +344,8 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     for (int k = 1; k < kLrMaxShared; ++k) xg = (xo == k) ? P.shl[k] : xg;
     const int64_t xch_id = xc ? cc[1] : cc[0];
     const bool xlive = xon && (xc ? live[1] : live[0]);
+    const int rep = P.rep;                   // lanes per private parameter (lanes.h)
+    const bool lead = (j & (rep - 1)) == 0;  // this lane counts its parameters
     // a transformed shared parameter (lanes.h LrCtx::shxf) and the identity
     // terms over its raw value: a uniform branch, so programs without them
     // run the same instructions as before
@@ -457,28 +441,13 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
              d_clogs = vpin(bc2(F.d_clogs));
     const f2 half = bc2(0.5f), one = bc2(1.0f);
     const float lp_const = vpin(P.lp_const);
-    // early poll (MC_LF_EARLY_POLL): the sweep issues the exchange poll at
-    // about 3/4 of the last slot with at least 8 full groups in every lane
-    // (uniform), so the loads' L2 round trip overlaps the rest of the sweep
-    // instead of following it; a step without such a slot polls after it
-    int cut_r = -1, cut_u4 = -1;
-#pragma unroll
-    for (int r = 0; r < RS; ++r)
-        if (!X1 && MC_LF_EARLY_POLL && lmin4[r] >= 8) {
-            cut_r = r;
-            // (the hook runs at a round start u4 with u4 + 4 <= lmin4)
-            cut_u4 = min(max(4, ((3 * lmin4[r]) / 4) & ~3), (lmin4[r] - 4) & ~3);
-        }
-    // the swept terms' moment sums at the current point, both chains; hook()
-    // at group cut_u4 of slot cut_r (every lane active there: lmin4 >= 8)
-    auto sweep = [&](f2 (&s1)[RS], f2 (&s2)[RS], auto&& hook) {
+    // the swept terms' moment sums at the current point, both chains
+    auto sweep = [&](f2 (&s1)[RS], f2 (&s2)[RS]) {
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             s1[r] = (f2){0.f, 0.f};
             s2[r] = (f2){0.f, 0.f};
-            if (len[r] > 0)
-                lf_moments(xv[r], len[r], lmin4[r], lmax[r], q[r], s1[r], s2[r],
-                           r == cut_r ? cut_u4 : -1, hook);
+            if (len[r] > 0) lf_moments(xv[r], len[r], lmin4[r], lmax[r], q[r], s1[r], s2[r]);
         }
     };
 
@@ -545,7 +514,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             if (gk[r] < 0) continue;  // (an empty slot's p stays 0: its g is always 0)
             const f2 z = {normal_of(gk[r], cc[0]), normal_of(gk[r], cc[1])};
             p[r] = z;
-            k0p += z * z;
+            if (lead) k0p += z * z;
         }
         sh.p = xon ? normal_of(xg, xch_id) : 0.0f;
         const float K0w[2] = {wave_sum(k0p[0]), wave_sum(k0p[1])};
@@ -597,10 +566,24 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         f2 M1[RS], M2[RS];
         drift_private(false);
         drift_shared(false);
-        sweep(M1, M2, LfNoHook());
-        for (int l = 0; l < L; ++l) {
+        sweep(M1, M2);
+        // one leapfrog step at the point q(l + 1), compiled per kind so that the
+        // intermediate steps carry none of the first / last steps' work (K0 /
+        // K1 items, log p) nor its uniform branches and their live masks:
+        // 0 first (l = 0 < L - 1), 1 intermediate, 2 last (l = L - 1 > 0),
+        // 3 the only step (L = 1).  Returns false on an exchange timeout.
+        auto step = [&](int l, auto kind) -> bool {
+            constexpr int KIND = decltype(kind)::value;
+            constexpr bool FIRST = KIND == 0 || KIND == 3, LAST = KIND == 2 || KIND == 3;
+            (void)l;
+            // no vector-memory operation is in flight here (the last poll was
+            // waited for): saying so explicitly keeps the compiler's wait-count
+            // state clean at the step's entry, where the kinds' paths merge —
+            // else it guards the sweep's first register writes with a
+            // vmcnt(0) that also waits for this step's own publish store
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
             MC_STAMP(0);
-            const bool lst = l == L - 1;  // log p: the last step only
+            constexpr bool lst = LAST;  // log p: the last step only
             // finish the swept term from its moment sums, evaluate the direct
             // term (k_hmc_lr's lr_finish; same arithmetic, both chains packed):
             // log p partial (last step), complete private gradients, cotangent
@@ -671,6 +654,15 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     }
                 }
             }
+            // a replicated parameter's gradient: the sum of its lanes' partials
+            if (rep > 1) {
+#pragma unroll
+                for (int r = 0; r < RS; ++r) {
+                    float a = g[r][0], b = g[r][1];
+                    grp_sum2(a, b, rep);
+                    g[r] = (f2){a, b};
+                }
+            }
             // the own prior of this lane's shared parameter (moment form with
             // the constant scale's reciprocals, as the sliced terms); its log p
             // enters slice 0's record
@@ -737,12 +729,12 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             }
             // the kinetic partials of the last step (uniform)
             float k1w[2] = {0.f, 0.f};
-            if (l == L - 1) {
+            if constexpr (LAST) {
                 f2 k1p = {0.f, 0.f};
 #pragma unroll
                 for (int r = 0; r < RS; ++r) {
                     const f2 pj = p[r] + h * g[r];
-                    k1p += pj * pj;
+                    if (lead) k1p += pj * pj;
                 }
                 k1w[0] = wave_sum(k1p[0]);
                 k1w[1] = wave_sum(k1p[1]);
@@ -763,11 +755,11 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 }
                 if (col == 2 * NRS || col == 2 * NRS + 1) {
                     const int c = col - 2 * NRS;
-                    if (row == 0 && l == 0) {
+                    if (FIRST && row == 0) {
                         pp = NV + c;
                         pv = c ? K0w[1] : K0w[0];
                     }
-                    if (row == 1 && l == L - 1) {
+                    if (LAST && row == 1) {
                         pp = NV + 2 + c;
                         pv = c ? k1w[1] : k1w[0];
                     }
@@ -784,9 +776,9 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             // or 3, and with the poll at either level, profiles/r3/ab/ab34)
             __builtin_amdgcn_s_setprio(1);
             // poll: pass ps reads pair 4 ps + perm[row] of slice col
-            const bool kstep = (l == 0) || (l == L - 1);
+            constexpr bool kstep = FIRST || LAST;
             const uint32_t need =
-                need_v | (l == 0 ? need_k0 : 0u) | (lst ? (need_k1 | need_lp) : 0u);
+                need_v | (FIRST ? need_k0 : 0u) | (LAST ? (need_k1 | need_lp) : 0u);
             float vals[NPASS];
 #pragma unroll
             for (int ps = 0; ps < NPASS; ++ps) vals[ps] = 0.0f;
@@ -803,14 +795,15 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     y[ps] = (ps < NPASS_V || kstep) ? granule_load(gp[par] + 4 * ps) : 0ull;
             };
             // while the records travel: the private parameters' next position
-            // and the swept terms' sums there (the first poll issued inside)
-            const bool early = cut_r >= 0 && l + 1 < L;
-            if (l + 1 < L) {
+            // and the swept terms' sums there (a poll issued inside the sweep
+            // costs a second round trip when the records have not landed yet:
+            // A/B 83.2 vs 94.7 M steps/s, profiles/r4/ab)
+            if constexpr (!LAST) {
                 drift_private(true);
-                sweep(M1, M2, poll_issue);
+                sweep(M1, M2);
             }
             MC_STAMP(8);
-            if (!X1 && !early) poll_issue();
+            if (!X1) poll_issue();
             auto poll_eval = [&]() {
                 bool ready = true;  // (bitwise: lane masks, no branches)
 #pragma unroll
@@ -837,7 +830,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             }
             if (!ok) {
                 __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
+                return false;
             }
             MC_STAMP(3);
             __builtin_amdgcn_s_setprio(0);
@@ -861,7 +854,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 }
             }
             // totals: the slice sum (the own priors are in slice 0's record)
-            if (lst) {
+            if constexpr (LAST) {
                 lpn[0] = rl(tot[0], 0) + lp_const;
                 lpn[1] = rl(tot[0], 16 * lf_row(1)) + lp_const;
             }
@@ -876,7 +869,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 if (hxf) gt = xf_chain(xxf, gt, sh.q, sh.v) + xid;
                 sh.g = xon ? gt : 0.0f;
             }
-            if (l == 0) {
+            if constexpr (FIRST) {
                 constexpr int p0 = NV, p1 = NV + 1;
                 if constexpr (X1) {
                     K0[0] = K0w[0];
@@ -886,7 +879,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     K0[1] = rl(tot[p1 / 4], 16 * lf_row(p1));
                 }
             }
-            if (l == L - 1) {
+            if constexpr (LAST) {
                 constexpr int p0 = NV + 2, p1 = NV + 3;
                 if constexpr (X1) {
                     K1[0] = k1w[0];
@@ -896,8 +889,16 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     K1[1] = rl(tot[p1 / 4], 16 * lf_row(p1));
                 }
             }
-            if (l + 1 < L) drift_shared(true);  // the shared parameters' next position
+            if constexpr (!LAST) drift_shared(true);  // the shared parameters' next position
             MC_STAMP(4);
+            return true;
+        };
+        if (L == 1) {
+            ok = step(0, std::integral_constant<int, 3>());
+        } else {
+            ok = step(0, std::integral_constant<int, 0>());
+            for (int l = 1; ok && l < L - 1; ++l) ok = step(l, std::integral_constant<int, 1>());
+            if (ok) ok = step(L - 1, std::integral_constant<int, 2>());
         }
         if (!ok) break;
         // ---- accept / adapt (identical in every slice of the block) ------------
@@ -960,7 +961,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     float* out = samples + (cc[c] * cfg.sample_capacity + s) * (int64_t)D;
 #pragma unroll
                     for (int r = 0; r < RS; ++r)
-                        if (gk[r] >= 0) out[gk[r]] = q[r][c];
+                        if (gk[r] >= 0 && lead) out[gk[r]] = q[r][c];
                 }
                 if (slice == 0 && xlive)
                     samples[(xch_id * cfg.sample_capacity + s) * (int64_t)D + xg] = sh.q;
@@ -977,7 +978,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         if (!live[c]) continue;
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
-            if (gk[r] >= 0) {
+            if (gk[r] >= 0 && lead) {
                 st_q[cc[c] * D + gk[r]] = q[r][c];
                 st_g[cc[c] * D + gk[r]] = g[r][c];
             }

@@ -182,6 +182,8 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
     for (int r = 0; r < RS; ++r) gk[r] = P.gidx[(int64_t)r * 64 + j];
     const int xk = j >> 1;
     const bool xon = j < 2 * Dsh;
+    const int rep = P.rep;                   // lanes per private parameter (lanes.h)
+    const bool lead = (j & (rep - 1)) == 0;  // this lane counts its parameters
     const bool xone = xon && (j & 1) == 0;  // counts the shared parameter once in sums
     int xg = P.shl[0];
 #pragma unroll
@@ -279,6 +281,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                 const MC_CONST LrTerm* T = tt + t;
                 switch (T->sig) {
                     case LS_DSCALE: lr_dscale_term<RS>(T, sd, j, R, sh, lpp, gshp); break;
+                    case LS_AFF: lr_affine<RS>(T, sd, j, R, sh, lpp, gshp); break;
                     case LS_DATA_PP_SH:
                         lr_normal_term<RS, SK_DATA, SK_PP, SK_SHARED>(T, sd, j, R, sh, lpp, gshp);
                         break;
@@ -301,6 +304,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
             }
         } else {
             lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp);
+        }
+        if (rep > 1) {  // a replicated parameter's gradient: its lanes' partials
+#pragma unroll
+            for (int r = 0; r < RS; ++r) grp_sum2(R.g[r][0], R.g[r][1], rep);
         }
         MC_STAMP(3);
         float slp[2] = {0.f, 0.f}, sg_self = 0.0f, sg_raw = 0.0f;
@@ -346,7 +353,8 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
     auto kinetic = [&]() {
         float k = 0.0f;
 #pragma unroll
-        for (int r = 0; r < RS; ++r) k += R.p[r][0] * R.p[r][0];
+        for (int r = 0; r < RS; ++r)
+            if (lead) k += R.p[r][0] * R.p[r][0];
         if (xone) k += sh.p * sh.p;
         return wave_sum(k);
     };
@@ -407,7 +415,8 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         {
             float k = 0.0f;
 #pragma unroll
-            for (int r = 0; r < RS; ++r) k += EM.p[r] * EM.p[r];
+            for (int r = 0; r < RS; ++r)
+                if (lead) k += EM.p[r] * EM.p[r];
             if (xone) k += Mrs * Mrs;
             K0 = wave_sum(k);
         }
@@ -447,6 +456,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
 #pragma unroll
             for (int r = 0; r <= RS; ++r) {
                 if (r == RS && !xone) break;
+                if (r < RS && !lead) continue;
                 const float d = qp[r] - qm[r];
                 a += d * rm[r];
                 b += d * rp[r];
@@ -514,7 +524,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     for (int r = 0; r < RS; ++r) {
 #pragma unroll
                         for (int hh = 0; hh < 2; ++hh) R.p[r][hh] = R.p[r][hh] + h * R.g[r][hh];
-                        k += R.p[r][0] * R.p[r][0];
+                        if (lead) k += R.p[r][0] * R.p[r][0];
                     }
                     float ws[2] = {lane_lp, k};
                     wave_sum2(ws);
@@ -705,7 +715,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                 float* out = samples + (c * cfg.sample_capacity + si) * (int64_t)D;
 #pragma unroll
                 for (int r = 0; r < RS; ++r)
-                    if (gk[r] >= 0) out[gk[r]] = Cq[r];
+                    if (gk[r] >= 0 && lead) out[gk[r]] = Cq[r];
                 if (xone) out[xg] = Cqs;
             }
         }
@@ -727,7 +737,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
 
 #pragma unroll
     for (int r = 0; r < RS; ++r) {
-        if (gk[r] >= 0) {
+        if (gk[r] >= 0 && lead) {
             st_q[c * D + gk[r]] = Cq[r];
             st_g[c * D + gk[r]] = Cg[r];
         }

@@ -24,8 +24,9 @@ extern "C" int mc_debug_lanes_forms(int on) {
 template <int NB>
 static int launch_hmc_sl(const mc_program* p, const mc_run_config* cfg, void* state,
                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
-    if (has_transform(p))
-        return fail(MC_ERR_UNSUPPORTED, "the term interpreter does not run transformed operands");
+    if (!interp_ok(p))
+        return fail(MC_ERR_UNSUPPORTED, "the term interpreter does not run transformed operands "
+                    "or affine locs");
     int64_t qo, go;
     mc_state_offsets(p, cfg->num_chains, &qo, &go);
     char* b = (char*)state;
@@ -86,7 +87,7 @@ extern "C" int64_t mc_hmc_workspace_bytes(const mc_program* p, int64_t C) {
     // so does a sliced program with transformed operands, which the term
     // interpreter does not take: mc_hmc_run)
     const int64_t x = (lanes1(p) || sliced(p)) ? sl_workspace_bytes(p, C) : 0;
-    if (sliced(p) && !has_transform(p)) return x;
+    if (sliced(p) && interp_ok(p)) return x;
     if (hmc_use_lds(p)) return x;
     return std::max(x, C * 5 * (int64_t)dpad_of(p->D) * 4);
 }
@@ -122,7 +123,7 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
     if (cfg->num_chains == 0 || cfg->iter_count == 0) return MC_OK;
     // L = 0 with transformed operands: the interpreter (k_hmc_sl) declines
     // them, so such a run takes the chain-per-workgroup tape (as lanes1 does)
-    const bool sl_tape = sliced(p) && !use_lanes(p, cfg) && has_transform(p);
+    const bool sl_tape = sliced(p) && !use_lanes(p, cfg) && !interp_ok(p);
     if ((sliced(p) && !sl_tape) || (lanes1(p) && use_lanes(p, cfg))) {
         const int64_t need = sl_workspace_bytes(p, cfg->num_chains);
         if (ws == nullptr || ws_bytes < need)

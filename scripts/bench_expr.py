@@ -57,6 +57,37 @@ init = {"a": np.float32(1.5), "b": np.float32(2.0), "sigma": np.float32(0.5)}
 for name, f in (("affine fused", fused), ("hand-written expression", handwritten)):
     r, tb, k = rate(f, init)
     print(f"regression N={N} {name}: {r / 1e6:.3f} M chain-steps/s (kernel {k}; build {tb:.2f} s)")
+# the varying-intercept regression alpha[g] + beta * x (G = 1000 groups of
+# ~100 observations): the affine loc on the lane-resident kernel (lanes.h
+# LS_AFF, 16 slices) and, for reference, on the tape (num_slices=1)
+G = 1000
+lpv, iv = W.varying_intercept(W.ns_product(), G, N)
+xv, yv, gv = W.varying_intercept_data(G, N)
+iv = dict(iv)
+iv["alpha"] = np.array([yv[gv == k].mean() - 0.7 * xv[gv == k].mean() if np.any(gv == k) else 1.0
+                        for k in range(G)], np.float32)
+for sl, name in ((0, "lane-resident (auto)"), (1, "tape (num_slices=1)")):
+    t0 = time.perf_counter()
+    prog = _trace.compile_model(lpv, iv, slices=sl)
+    tb = time.perf_counter() - t0
+    cs = _engine.ChainSet(prog, 256, prog.layout.flatten(iv), 1e-3, device=torch.device("cuda"))
+    smp = torch.empty((256, 1, prog.D), dtype=torch.float32, device="cuda")
+    cfg = dict(chain_offset=0, num_warmup=10 ** 6, num_samples=1, sample_begin=0,
+               sample_capacity=1, seed=0, step_size=1e-3, target_accept=0.8,
+               num_leapfrog_steps=10, adapt_step_size=False)
+    cs.run_hmc(samples=smp, iter_begin=0, iter_count=2, **cfg)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    it = 20 if sl == 0 else 2
+    e0.record()
+    cs.run_hmc(samples=smp, iter_begin=2, iter_count=it, **cfg)
+    e1.record()
+    torch.cuda.synchronize()
+    cs.check_status()
+    r = 256 * it * 10 / (e0.elapsed_time(e1) * 1e-3)
+    print(f"varying intercept G={G} N={N} {name}: {r / 1e6:.3f} M chain-steps/s "
+          f"(kernel {prog.slice_kernel}, {prog.num_slices} slices; build {tb:.2f} s)")
+    del cs, smp, prog
 lp, _ = W.two_predictor_regression(W.ns_product(), N)
 i2 = {"a": np.float32(0.5), "b1": np.float32(1.2), "b2": np.float32(-0.8),
       "log_sigma": np.float32(-0.5)}

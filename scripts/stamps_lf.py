@@ -67,3 +67,21 @@ for sec, name in SECS:
 print(f"  {'total':28s} " + " ".join(f"{x:7.0f}" for x in tot))
 print(f"  ticks per us (total / measured step incl. launch): "
       f"{tot.mean() / (dt / (ITERS * L) * 1e6):.0f}")
+wg = (ctypes.c_ulonglong * (1024 * 16))()
+lib.mc_debug_stamps_lanes_wg.argtypes = [ctypes.c_void_p]
+lib.mc_debug_stamps_lanes_wg(wg)
+wga = np.array(wg[:], dtype=np.float64).reshape(1024, 16) / steps
+S = prog.num_slices
+if S > 1:
+    # chain block 0's slices (XCD-aware placement: workgroup 8 r holds slice r
+    # when the grid is a multiple of 8 blocks), wave 0 of each
+    nwg = (C // (2 * nw)) * S
+    xcd = nwg % 8 == 0 and (nwg // 8) % S == 0
+    print("  block 0, wave 0, per slice: finish / publish / sweep / poll / spins / sums")
+    for sl in range(S):
+        w = 8 * sl if xcd else sl
+        print(f"    slice {sl:2d}: " + " ".join(f"{wga[w, k]:7.0f}" for k in (1, 2, 8, 7, 3, 4)))
+    allw = wga[:nwg]
+    print("  all workgroups, wave 0: mean / max of sweep, spins: "
+          f"{allw[:, 8].mean():.0f} / {allw[:, 8].max():.0f}, {allw[:, 3].mean():.0f} / "
+          f"{allw[:, 3].max():.0f}")

@@ -74,10 +74,10 @@ print("  section (cycles/step)         " + " ".join(f"  wave{w}" for w in range(
 for sec, name in SECS:
     vals = " ".join(f"{a[w, sec] / steps:7.0f}" for w in range(8))
     print(f"  {name:28s} {vals}")
-wg = (ctypes.c_ulonglong * (1024 * 4))()
+wg = (ctypes.c_ulonglong * (1024 * 16))()
 lib.mc_debug_stamps_lanes_wg.argtypes = [ctypes.c_void_p]
 lib.mc_debug_stamps_lanes_wg(wg)
-wga = np.array(wg[:], dtype=np.float64).reshape(1024, 4) / steps
+wga = np.array(wg[:], dtype=np.float64).reshape(1024, 16) / steps
 # chain block 0's slices (XCD-aware placement: workgroup 8 r holds slice r)
 print("  block 0, wave 0, per slice:  eval / publish / poll")
 for sl in range(prog.num_slices):

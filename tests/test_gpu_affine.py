@@ -30,7 +30,7 @@ def test_affine_tape_matches_autograd(gpu, model):
     from mlx_mcmc_amd import _engine, _trace
 
     lp_fn, init = MODELS[model](W.ns_product())
-    prog = _trace.compile_model(lp_fn, init)
+    prog = _trace.compile_model(lp_fn, init, slices=1)
     assert prog.num_slices == 1 and prog.slice_kernel == "unsliced"   # the tape kernels
     olp, oinit = MODELS[model](W.ns_oracle())
     M = S.EagerModel(olp, oinit)
@@ -51,6 +51,9 @@ def test_affine_tape_matches_autograd(gpu, model):
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_affine_hmc_trace_matches_oracle(gpu, seed):
+    """The regression a + b * x on the automatic plan: the one-slice
+    lane-resident kernel (lanes.h LS_AFF, a chunk term with shared loc and
+    slope) against the oracle's HMC trace."""
     import mlx_mcmc_amd as m
 
     lp, _ = W.linear_regression(W.ns_product())
@@ -118,7 +121,9 @@ def test_affine_regression_posterior(gpu):
     s, rate, info = m.hmc(lp, start, num_samples=500, num_warmup=300, step_size=0.01,
                           num_leapfrog_steps=10, key=m.random.key(1), num_chains=32,
                           progress=False, return_info=True)
-    assert info.extra["kernel"] == "unsliced"
+    # the automatic plan: the lane-resident kernel (an affine chunk term, lanes.h
+    # lr_affine_term with a shared loc and slope)
+    assert info.extra["kernel"] == "lanes"
     live = info.accept_rate > 0.05
     assert live.sum() >= 16
     for k, name in enumerate(("a", "b")):
@@ -153,3 +158,64 @@ def test_affine_varying_intercept_hmc_trace(gpu):
     same = compare_trace(gpu_c, ref_c, "varying intercept", verbose=True)
     acc = np.asarray(ref.trace["accepted"][:same])
     assert same >= 20 and acc.any()
+
+
+@pytest.mark.parametrize("G,N", [(20, 2000), (200, 100000)])
+def test_affine_varying_intercept_lanes(gpu, G, N):
+    """alpha[group] + beta * x on the lane-resident kernel (VERDICT r3 "Next
+    round" 4b: lanes.h LS_AFF, the private alpha_g's elements tiled in its
+    lane group with x beside y, beta and sigma shared): G = 20 (one slice, 20
+    private parameters: replicated lanes, rep = 2) against the oracle's HMC
+    trace; G = 200 / N = 100 K (16 slices, exchange) against the tape kernel
+    k_hmc on the same chains (decisions, ratios, H to a proven near-tie,
+    step sizes bit-identical)."""
+    import mlx_mcmc_amd as m
+    from mlx_mcmc_amd import _trace
+
+    lp, init = W.varying_intercept(W.ns_product(), G, N)
+    x, y, g = W.varying_intercept_data(G, N)
+    start = dict(init)
+    start["alpha"] = np.array([y[g == k].mean() - 0.7 * x[g == k].mean() for k in range(G)],
+                              np.float32)
+    prog = _trace.compile_model(lp, start)
+    assert prog.slice_kernel == "lanes" and prog.kernel_note == "", prog.kernel_note
+    if G == 20:
+        olp, _ = W.varying_intercept(W.ns_oracle(), G, N)
+        kw = dict(num_samples=30, num_warmup=30, step_size=0.01, num_leapfrog_steps=10)
+        s, rate, info = m.hmc(lp, start, key=m.random.key(1), progress=False, return_info=True,
+                              return_trace=True, **kw)
+        assert info.extra["kernel"] == "lanes"
+        ref = S.hmc(olp, start, seed=1, **kw)
+        n = 25
+        tr = info.trace
+        gpu_c = {"accepted": tr["accepted"][0][:n], "ratio": tr["accept_stat"][0][:n],
+                 "step_size": tr["step_size"][0][:n], "energy": tr["energy"][0][:n]}
+        ref_c = {k: np.asarray(ref.trace[k])[:n] for k in ("accepted", "ratio", "step_size",
+                                                            "energy")}
+        ref_c["log_u"] = log_u(1, 0, n)
+        same = compare_trace(gpu_c, ref_c, "varying intercept (lanes)", verbose=True)
+        acc = np.asarray(ref.trace["accepted"][:same])
+        assert same >= 20 and acc.any()
+        return
+    assert prog.num_slices == 16
+    kw = dict(num_samples=10, num_warmup=10, step_size=2e-3, num_leapfrog_steps=10,
+              key=m.random.key(3), num_chains=16, progress=False, return_info=True,
+              return_trace=True)
+    a, _, ia = m.hmc(lp, start, num_slices=1, **kw)
+    b, _, ib = m.hmc(lp, start, **kw)
+    assert ia.extra["kernel"] == "unsliced" and ib.extra["kernel"] == "lanes"
+    acc = ia.trace["accepted"].astype(bool)
+    assert acc.any()
+    full = 0
+    for c in range(16):
+        ref = {"accepted": ia.trace["accepted"][c], "ratio": ia.trace["accept_stat"][c],
+               "energy": ia.trace["energy"][c], "step_size": ia.trace["step_size"][c],
+               "log_u": log_u(3, c, 20)}
+        got = {"accepted": ib.trace["accepted"][c], "ratio": ib.trace["accept_stat"][c],
+               "energy": ib.trace["energy"][c], "step_size": ib.trace["step_size"][c]}
+        same = compare_trace(got, ref, f"varying intercept N={N} chain {c}")
+        full += same == 20
+        ns = max(0, same - 10)
+        for k in a:
+            np.testing.assert_allclose(b[k][c, :ns], a[k][c, :ns], rtol=1e-3, atol=1e-5)
+    assert full >= 10
