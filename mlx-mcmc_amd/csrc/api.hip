@@ -646,6 +646,7 @@ static void free_lanes(LanePlan& L) {
     if (L.d_blocks) (void)hipFree(L.d_blocks);
     if (L.d_gidx) (void)hipFree(L.d_gidx);
     if (L.d_sterms) (void)hipFree(L.d_sterms);
+    if (L.d_rng) (void)hipFree(L.d_rng);
     L = LanePlan();
 }
 
@@ -686,6 +687,72 @@ static int lanes_form(const LanePlan& L, int nT) {
     if (roles != L.Dsh) return -1;
     if ((o_sw >= 0 && (o_sw == o_dm || o_sw == o_ds)) || (o_dm >= 0 && o_dm == o_ds)) return -1;
     return (form == (LF_SW | LF_SWS | LF_DIR | LF_DM | LF_DS) || form == LF_DIR) ? form : -1;
+}
+
+// The lane RNG plan of k_hmc_lf (lanes_fast.h lf_rng_*).  A wave's draws per
+// iteration are the momentum normals of its two chains' private parameters
+// (normal g % 4 of Philox block g / 4, the tape kernels' mapping), of the
+// lanes' shared parameters (lane 2 k + c: parameter k of chain c), and one
+// accept uniform per chain.  Every lane of a slice holds the same parameters
+// in every wave, so the distinct (chain, block) pairs can be dealt to lanes
+// once: lane i computes one Philox block and both Box-Muller pairs of it, two
+// more lanes the chains' accept draws (their first Box-Muller log is the
+// accept log), and each lane fetches its normals from the lanes that hold
+// them — one Philox block and two Box-Muller pairs per lane and iteration
+// instead of three blocks and three pairs, plus two blocks and logs per lane
+// for the accept.  Per lane four words:
+//   x: job (0 none, 1 / 2 momentum block of chain 0 / 1, 3 / 4 accept draw
+//      of chain 0 / 1) | block << 3
+//   y: slots 0, 1: source lane of chain 0, chain 1 (6 bits each) and the
+//      component (2 bits), per slot 14 bits
+//   z: slots 2, 3 likewise
+//   w: the accept lane of chain 0 << 8 | of chain 1 << 14 | 1 << 30 (valid)
+// (the blocks of every shared parameter of both chains are among the jobs;
+// a lane finds its shared parameter's block lane once per launch)
+// Empty when more than 62 distinct blocks are needed (the kernel then draws
+// per lane).
+static void plan_lane_rng(LanePlan& L, int S) {
+    if (const char* e = std::getenv("MC_LANES_RNG"))  // 0: per-lane draws (A/B)
+        if (std::atoi(e) == 0) return;
+    std::vector<int32_t> rng((size_t)S * 64 * 4, 0);
+    for (int s = 0; s < S; ++s) {
+        std::map<std::pair<int, int32_t>, int> lane_of_block;  // (chain, block) -> lane
+        std::vector<std::pair<int, int32_t>> jobs;
+        auto job = [&](int c, int32_t b) {
+            const auto key = std::make_pair(c, b);
+            auto it = lane_of_block.find(key);
+            if (it != lane_of_block.end()) return it->second;
+            const int l = (int)jobs.size();
+            jobs.push_back(key);
+            lane_of_block[key] = l;
+            return l;
+        };
+        int32_t* R = &rng[(size_t)s * 64 * 4];
+        for (int j = 0; j < 64; ++j) {
+            for (int r = 0; r < L.rs && r < kLrMaxSlots; ++r) {
+                const int32_t g = L.gidx[((size_t)s * kLrMaxSlots + r) * 64 + j];
+                if (g < 0) continue;
+                if (g >= (1 << 28)) return;  // (block << 3 must fit the word)
+                const int l0 = job(0, g >> 2), l1 = job(1, g >> 2);
+                const int32_t v = l0 | (l1 << 6) | ((g & 3) << 12);
+                R[4 * j + 1 + (r >> 1)] |= v << (14 * (r & 1));
+            }
+            if (j < 2 * L.Dsh) {  // every shared parameter k = j / 2 of chain j % 2 (the
+                                  // kernel finds its block's lane: lane layouts differ)
+                const int32_t g = L.shl[j >> 1];
+                if (g >= (1 << 28)) return;
+                (void)job(j & 1, g >> 2);
+            }
+        }
+        if ((int)jobs.size() + 2 > 64) return;  // (no plan: per-lane draws)
+        const int acc0 = (int)jobs.size(), acc1 = acc0 + 1;
+        for (size_t i = 0; i < jobs.size(); ++i)
+            R[4 * i] = (jobs[i].first + 1) | (jobs[i].second << 3);
+        R[4 * acc0] = 3;
+        R[4 * acc1] = 4;
+        for (int j = 0; j < 64; ++j) R[4 * j + 3] |= (acc0 << 8) | (acc1 << 14) | (1 << 30);
+    }
+    L.rng.swap(rng);
 }
 
 static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartition& part,
@@ -993,6 +1060,7 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         kSlLdsBudget)
         return no("slice data exceed the LDS budget");
     if (L.data.empty()) L.data.assign(4, 0.0f);
+    plan_lane_rng(L, S);
     L.fast = (!any_rest && lf_generic == 0) ? 1 : 0;
     L.form = L.fast ? lanes_form(L, nT) : -1;
     L.ok = 1;
@@ -1011,6 +1079,7 @@ static hipError_t upload_lanes(LanePlan& LP) {
     if (e == hipSuccess) e = upload(&LP.d_blocks, LP.blocks);
     if (e == hipSuccess) e = upload(&LP.d_gidx, LP.gidx);
     if (e == hipSuccess && !LP.sterms.empty()) e = upload(&LP.d_sterms, LP.sterms);
+    if (e == hipSuccess && !LP.rng.empty()) e = upload(&LP.d_rng, LP.rng);
     return e;
 }
 

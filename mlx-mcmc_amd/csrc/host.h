@@ -91,6 +91,8 @@ struct LanePlan {
     int32_t shxf[kLrMaxShared] = {0, 0, 0, 0};  // transforms of the shared parameters
     float shid[kLrMaxShared] = {0.f, 0.f, 0.f, 0.f};  // raw identity weights (k_hmc_lf)
     int rep = 1;         // lanes per private parameter (lanes.h LrCtx::rep)
+    std::vector<int32_t> rng;  // [S][64][4] lane RNG plan (lanes_fast.h lf_rng_*), or empty
+    int32_t* d_rng = nullptr;
     int has_xf = 0;      // a shared parameter is transformed, or an identity term
                          // (no NUTS lanes, no term interpreter)
     std::string why;     // why it does not qualify
@@ -254,6 +256,7 @@ inline LrCtx lrctx_of(const mc_program* p) {
     }
     c.has_xf = L.has_xf;
     c.rep = L.rep;
+    c.rng = (const int4*)L.d_rng;
     return c;
 }
 // ---------------------------------------------------------------------------

@@ -121,6 +121,7 @@ struct LrCtx {
     float shid[kLrMaxShared];    // k_hmc_lf: the weights of the identity terms
                                  // over the raw parameter (its log-Jacobian)
     int32_t has_xf;              // a transform or an identity term (k_hmc_lf)
+    const int4* rng;             // [S][64] lane RNG plan (lf_rng_*), or nullptr
     int32_t rep;                 // lanes per private parameter (1, 2, 4, 8 or 16):
                                  // a parameter's elements are split over the
                                  // `rep` lanes of its group (lanes j & ~(rep-1)

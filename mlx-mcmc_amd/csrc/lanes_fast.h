@@ -375,6 +375,19 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         g[r] = (f2){R0.g[r][0], R0.g[r][1]};
         p[r] = (f2){0.f, 0.f};
     }
+    // the lane RNG plan (api.hip plan_lane_rng), when the planner made one
+    const bool rngp = P.rng != nullptr;
+    int4 rw = {0, 0, 0, 0};
+    if (rngp) rw = P.rng[(int64_t)slice * 64 + j];
+    const int racc0 = __builtin_amdgcn_readfirstlane((rw.w >> 8) & 63);
+    const int racc1 = __builtin_amdgcn_readfirstlane((rw.w >> 14) & 63);
+    // the lane holding this lane's shared parameter's Philox block (chain xc)
+    int sh_src = 0;
+    if (rngp) {
+        const int target = (xc + 1) | ((xg >> 2) << 3);
+        for (int i = 0; i < 64; ++i)
+            sh_src = (__builtin_amdgcn_readlane(rw.x, i) == target) ? i : sh_src;
+    }
     LrShared sh;
     sh.q = xon ? st_q[xch_id * D + xg] : 1.0f;
     sh.g = xon ? st_g[xch_id * D + xg] : 0.0f;
@@ -509,14 +522,55 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             return (gi & 1) ? z1 : z0;
         };
         f2 k0p = {0.f, 0.f};
+        float logu_acc[2] = {0.f, 0.f};  // the chains' accept logs (lane RNG plan)
+        if (rngp) {
+            // the lane RNG plan (api.hip plan_lane_rng): this lane's Philox
+            // block — a momentum block of one chain or a chain's accept draw —
+            // and both Box-Muller pairs of it; the accept lanes' first log is
+            // the accept log (mc_logf_unit of the same uniform transform the
+            // per-lane path uses); the normals are fetched from their lanes
+            const int kind = rw.x & 7;
+            const bool acl = kind >= 3;
+            const int csel = (kind == 2 || kind == 4) ? 1 : 0;
+            const mc_u32x4 rr =
+                mc_draw(cfg.seed, (uint32_t)(cfg.chain_offset + (csel ? cc[1] : cc[0])),
+                        (uint32_t)it, acl ? MC_RNG_TAG_ACCEPT : MC_RNG_TAG_MOMENTUM, 0,
+                        acl ? 0u : ((uint32_t)rw.x >> 3));
+            const float la = mc_logf_unit(acl ? mc_u01_f32(rr.x) : mc_u01_boxf(rr.x));
+            const float lb = mc_logf_unit(mc_u01_boxf(rr.z));
+            float z[4];
+            mc_box_muller_log(la, rr.y, &z[0], &z[1]);
+            mc_box_muller_log(lb, rr.w, &z[2], &z[3]);
+            logu_acc[0] = rl(la, racc0);
+            logu_acc[1] = rl(la, racc1);
+            auto fetch = [&](int src, int comp) {
+                float v = __shfl(z[0], src);
+                const float v1 = __shfl(z[1], src), v2 = __shfl(z[2], src), v3 = __shfl(z[3], src);
+                v = comp == 1 ? v1 : v;
+                v = comp == 2 ? v2 : v;
+                return comp == 3 ? v3 : v;
+            };
 #pragma unroll
-        for (int r = 0; r < RS; ++r) {
-            if (gk[r] < 0) continue;  // (an empty slot's p stays 0: its g is always 0)
-            const f2 z = {normal_of(gk[r], cc[0]), normal_of(gk[r], cc[1])};
-            p[r] = z;
-            if (lead) k0p += z * z;
+            for (int r = 0; r < RS; ++r) {
+                const int word = (r < 2 ? rw.y : rw.z) >> (14 * (r & 1));
+                const int comp = (word >> 12) & 3;
+                const f2 zz = {fetch(word & 63, comp), fetch((word >> 6) & 63, comp)};
+                if (gk[r] < 0) continue;  // (an empty slot's p stays 0: its g is always 0)
+                p[r] = zz;
+                if (lead) k0p += zz * zz;
+            }
+            const float zs = fetch(sh_src, xg & 3);
+            sh.p = xon ? zs : 0.0f;
+        } else {
+#pragma unroll
+            for (int r = 0; r < RS; ++r) {
+                if (gk[r] < 0) continue;  // (an empty slot's p stays 0: its g is always 0)
+                const f2 z = {normal_of(gk[r], cc[0]), normal_of(gk[r], cc[1])};
+                p[r] = z;
+                if (lead) k0p += z * z;
+            }
+            sh.p = xon ? normal_of(xg, xch_id) : 0.0f;
         }
-        sh.p = xon ? normal_of(xg, xch_id) : 0.0f;
         const float K0w[2] = {wave_sum(k0p[0]), wave_sum(k0p[1])};
         float k0s[2] = {0.f, 0.f};  // the shared parameters' part, in slot order
         {
@@ -917,9 +971,12 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             const float H0 = -lp[c] + 0.5f * (K0[c] + k0s[c]);
             const float H1 = -lpn[c] + 0.5f * (K1[c] + k1s[c]);
             const float ratio = -(H1 - H0);
-            const mc_u32x4 ru = mc_draw(cfg.seed, (uint32_t)(cfg.chain_offset + cc[c]),
-                                        (uint32_t)it, MC_RNG_TAG_ACCEPT, 0, 0);
-            const float logu = mc_logf_u01(mc_u01_f32(ru.x));
+            float logu = logu_acc[c];
+            if (!rngp) {
+                const mc_u32x4 ru = mc_draw(cfg.seed, (uint32_t)(cfg.chain_offset + cc[c]),
+                                            (uint32_t)it, MC_RNG_TAG_ACCEPT, 0, 0);
+                logu = mc_logf_u01(mc_u01_f32(ru.x));
+            }
             const bool accepted = logu < ratio;
             acc[c] = accepted;
             nacc[c] += accepted ? 1 : 0;

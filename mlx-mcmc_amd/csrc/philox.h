@@ -135,6 +135,19 @@ MC_HD void mc_box_muller(uint32_t a, uint32_t b, float* z0, float* z1) {
     *z1 = r * s;
 }
 
+// The same pair from the precomputed log of the first uniform (l1 =
+// mc_logf_unit(mc_u01_boxf(a))) and the second word: bit-identical to
+// mc_box_muller(a, b) (k_hmc_lf's lane RNG plan computes the log once and
+// shares it with an accept draw).
+MC_HD void mc_box_muller_log(float l1, uint32_t b, float* z0, float* z1) {
+    const float u2 = mc_u01_boxf(b);
+    const float r = sqrtf(-2.0f * l1);
+    float s, c;
+    mc_sincospif_unit(2.0f * u2, &s, &c);
+    *z0 = r * c;
+    *z1 = r * s;
+}
+
 // f32 log / exp "as IEEE would round them": evaluated in double, rounded once.
 MC_HD float mc_logf_ref(float x) { return (float)log((double)x); }
 // The log of an accept / slice uniform in (0, 1]: mc_logf_unit.
