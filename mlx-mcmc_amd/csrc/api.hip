@@ -35,10 +35,12 @@ static int choose_wpc(int64_t max_n) {
 // gradient directly.
 // prim_pool: index-pool offset of the sorted primary index; others: the
 // term's other vector operands, tiled beside it (DATA copied, PVEC turned
-// into identity gathers, GATHER indices copied); allow_split: long runs may be
-// split into virtual segments (expression terms keep whole runs).
+// into identity gathers, GATHER indices copied); tsplit: with fewer groups
+// than that, runs are split into ~tsplit virtual segments; nprim: partials per
+// virtual segment (an expression term keeps one per gathered leaf), so that
+// nprim x (virtual segments) fit the evaluator's 4T segment-partial floats.
 static int build_segments_ops(DevTerm& dt, int64_t prim_pool, const std::vector<DevOperand*>& others,
-                              bool allow_split, std::vector<float>& dpool,
+                              int64_t tsplit, int nprim, std::vector<float>& dpool,
                               std::vector<int32_t>& ipool, int T) {
     const int64_t n = dt.n;
     const int64_t ip = prim_pool;
@@ -51,10 +53,9 @@ static int build_segments_ops(DevTerm& dt, int64_t prim_pool, const std::vector<
         }
     const int64_t G = (int64_t)sstart.size();
     sstart.push_back(n);
-    // split only when there are fewer groups than lanes (then ~T virtual
-    // segments, one tile per wave); otherwise each lane owns whole groups
-    const int64_t Lt = (G >= (int64_t)T || !allow_split) ? INT64_MAX
-                                                         : std::max<int64_t>(1, (n + T - 1) / T);
+    // split only when there are fewer groups than tsplit (then <= 2 tsplit
+    // virtual segments); otherwise each lane owns whole groups
+    const int64_t Lt = (G >= tsplit) ? INT64_MAX : std::max<int64_t>(1, (n + tsplit - 1) / tsplit);
     struct V {
         int32_t k;
         int64_t start;
@@ -151,7 +152,7 @@ static int build_segments_ops(DevTerm& dt, int64_t prim_pool, const std::vector<
     ipool.insert(ipool.end(), lanes.begin(), lanes.end());
     dt.comb_base = (int64_t)ipool.size();
     if (split) ipool.insert(ipool.end(), comb.begin(), comb.end());
-    if (nv > 4 * (int64_t)T && split)
+    if (nv * nprim > 4 * (int64_t)T && split)
         return fail(MC_ERR_UNSUPPORTED, "internal: too many virtual segments");
     return MC_OK;
 }
@@ -163,7 +164,7 @@ static int build_segments(DevTerm& dt, std::vector<float>& dpool, std::vector<in
     for (int b = 0; b < 3; ++b)
         if (b != a) others.push_back(&dt.op[b]);
     if (dt.affine) others.push_back(&dt.ax);
-    return build_segments_ops(dt, dt.op[a].pool, others, true, dpool, ipool, T);
+    return build_segments_ops(dt, dt.op[a].pool, others, T, 1, dpool, ipool, T);
 }
 
 // ---------------------------------------------------------------------------
@@ -1405,13 +1406,14 @@ static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, 
     int64_t prim_pool = -1;
     if (!nonunique.empty()) {
         const int64_t p0 = en[nonunique[0]].leaf.pool;
-        for (int k : nonunique) {
+        for (size_t r = 0; r < nonunique.size(); ++r) {
+            const int k = nonunique[r];
             const int64_t pk = en[k].leaf.pool;
             if (pk != p0 && !std::equal(ipool.begin() + pk, ipool.begin() + pk + n,
                                         ipool.begin() + p0))
                 return fail(MC_ERR_UNSUPPORTED, "term %d: an expression gathers through two "
                             "different non-injective index arrays", t);
-            en[k].prim = 1;
+            en[k].prim = 1 + (int)r;  // 1 + its row of split-run partials
         }
         prim_pool = p0;
         dt.primary = 0;  // (a flag for expression terms: segmented)
@@ -1495,7 +1497,12 @@ static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, 
         for (int k = 0; k < nn; ++k)
             if (en[k].op == MC_EX_LEAF && !en[k].prim && is_vec_kind(en[k].leaf.kind))
                 others.push_back(&en[k].leaf);
-        const int rc = build_segments_ops(dt, prim_pool, others, false, dpool, ipool, 64 * wpc);
+        // long runs split as the fused terms' are, with one partial row per
+        // gathered leaf (nprim rows of <= 2 tsplit virtual segments: 4T floats)
+        const int T = 64 * wpc;
+        const int nprim = (int)nonunique.size();
+        const int64_t tsplit = std::max<int64_t>(1, std::min<int64_t>(T, 2 * T / nprim));
+        const int rc = build_segments_ops(dt, prim_pool, others, tsplit, nprim, dpool, ipool, T);
         if (rc) return rc;
     }
     dt.expr_base = (int32_t)gnodes.size();

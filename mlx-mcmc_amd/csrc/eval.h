@@ -852,10 +852,12 @@ MC_DEV void ex_bwd(int op, float x, float y, float z, float v, float c, float c0
 }
 
 // One expression term.  Strided (element i -> thread i mod nthr) or, with a
-// non-injective gather (T.primary >= 0), per group run of the segment-tiled
-// layout (build_segments; runs are never split for expression terms), the
-// gathered leaves read q[poff + k] and sum their cotangent in `part` over
-// the run.  Vector leaves deposit in their pass only (sweeps separated by a
+// non-injective gather (T.primary >= 0), per (virtual) segment of the
+// segment-tiled layout (build_segments_ops), the gathered leaves read
+// q[poff + k] and sum their cotangent in `part` over the run; runs split
+// into virtual segments (few groups, T.ncomb > 0) leave one partial per
+// gathered leaf in vpart (row prim - 1), added in order per group after a
+// barrier, as the fused terms' are.  Vector leaves deposit in their pass only (sweeps separated by a
 // group barrier: deterministic, no atomics); broadcast (PSCALAR) leaves sum
 // per thread and flush to their cotangent slots after pass 0.
 // NMAX: the node arrays' size.  Terms of <= 16 nodes run the NMAX = 16
@@ -866,11 +868,13 @@ MC_DEV void ex_bwd(int op, float x, float y, float z, float v, float c, float c0
 // load; 3 x 32 VGPRs are not affordable).
 template <int WPC, bool VALUE_ONLY, int NMAX>
 MC_DEV void eval_expr_n(const DevTerm& T, const DevCtx& P, const float* q, float* g,
-                        const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc) {
+                        const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc,
+                        float* vpart) {
     const MC_CONST DevExprNode* N = cptr(P.nodes) + T.expr_base;
     const int nn = T.expr_n;
     const float w = T.weight;
     const bool seg = T.primary >= 0;
+    const bool split = seg && T.ncomb > 0;
     float val[NMAX], adj[NMAX], part[NMAX];
     // the node descriptors, read once per term: lane k of these registers
     // holds node k (packed op / arguments / flags, leaf offsets, constant);
@@ -883,7 +887,7 @@ MC_DEV void eval_expr_n(const DevTerm& T, const DevCtx& P, const float* q, float
         if (ln < nn) {
             const MC_CONST DevExprNode* d = N + ln;
             dcode = (d->op & 31) | ((d->a + 1) << 5) | ((d->b + 1) << 11) | ((d->c + 1) << 17) |
-                    ((d->prim & 1) << 23) | ((d->pass & 15) << 24) | ((d->leaf.kind & 7) << 28);
+                    ((d->prim != 0 ? 1 : 0) << 23) | ((d->pass & 15) << 24) | ((d->leaf.kind & 7) << 28);
             dpoff = d->leaf.poff;
             dpool = (int)d->leaf.pool;
             dcval = d->leaf.cval;
@@ -978,8 +982,26 @@ MC_DEV void eval_expr_n(const DevTerm& T, const DevCtx& P, const float* q, float
                     if (N[k].prim) part[k] = 0.0f;
                 for (int u = 0; u < len; ++u) element(seg_elem(off, u, lane), kr);
                 if (!VALUE_ONLY && valid) {
-                    for (int k = 0; k < nn; ++k)
-                        if (N[k].prim && N[k].pass == pass) g[N[k].leaf.poff + kr] += part[k];
+                    for (int k = 0; k < nn; ++k) {
+                        if (!N[k].prim || N[k].pass != pass) continue;
+                        if (split) vpart[(N[k].prim - 1) * T.nvirt + v] = part[k];
+                        else g[N[k].leaf.poff + kr] += part[k];
+                    }
+                }
+            }
+            if (!VALUE_ONLY && split) {
+                // split runs: each group's virtual-segment partials in order
+                G.sync();
+                const int* comb = P.index + T.comb_base;
+                for (int c = G.tid; c < T.ncomb; c += G.T) {
+                    const int kc = comb[3 * c], vf = comb[3 * c + 1], vc = comb[3 * c + 2];
+                    for (int k = 0; k < nn; ++k) {
+                        if (!N[k].prim || N[k].pass != pass) continue;
+                        const float* vp = vpart + (N[k].prim - 1) * T.nvirt;
+                        float sum = vp[vf];
+                        for (int j = 1; j < vc; ++j) sum += vp[vf + j];
+                        g[N[k].leaf.poff + kc] += sum;
+                    }
                 }
             }
         }
@@ -1000,11 +1022,12 @@ MC_DEV void eval_expr_n(const DevTerm& T, const DevCtx& P, const float* q, float
 // one — all 19 op cases of every node executed for every element, 20x slower)
 template <int WPC, bool VALUE_ONLY>
 MC_DEV void eval_expr(const DevTerm& T, const DevCtx& P, const float* q, float* g,
-                      const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc) {
+                      const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc,
+                      float* vpart) {
     if (T.expr_n <= 16)
-        eval_expr_n<WPC, VALUE_ONLY, 16>(T, P, q, g, G, task, tid, nthr, lp_acc);
+        eval_expr_n<WPC, VALUE_ONLY, 16>(T, P, q, g, G, task, tid, nthr, lp_acc, vpart);
     else
-        eval_expr_n<WPC, VALUE_ONLY, kExMaxNodes>(T, P, q, g, G, task, tid, nthr, lp_acc);
+        eval_expr_n<WPC, VALUE_ONLY, kExMaxNodes>(T, P, q, g, G, task, tid, nthr, lp_acc, vpart);
 }
 
 // ---------------------------------------------------------------------------
@@ -1022,7 +1045,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
     const int nthr = task ? 64 : G.T;
     if constexpr (EX) {
         if (T.dist == MC_DIST_EXPR) {
-            eval_expr<WPC, VALUE_ONLY>(T, P, q, g, G, task, tid, nthr, lp_acc);
+            eval_expr<WPC, VALUE_ONLY>(T, P, q, g, G, task, tid, nthr, lp_acc, S.vpart);
             return;
         }
     }

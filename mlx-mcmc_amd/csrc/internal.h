@@ -74,7 +74,8 @@ struct DevTerm {
 // vector leaf deposits its cotangents (leaves with overlapping parameter
 // ranges deposit in different sweeps); `prim`: a leaf gathered through the
 // term's non-injective index (segmented terms: value q[poff + k] of the
-// lane's run, cotangent summed in a register and deposited once per run).
+// lane's run, cotangent summed in a register and deposited once per run);
+// prim = 1 + the leaf's row of split-run partials (0: not gathered so).
 struct DevExprNode {
     int32_t op, a, b, c;
     int32_t pass, prim;

@@ -483,6 +483,11 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     // publishing: lanes 16 r + n (n < NRS * 2) hold pair 8 (n / 2) + 4 (n % 2) + perm[r]
     const int pub_pair = (col < 2 * NRS) ? 8 * (col >> 1) + 4 * (col & 1) + lf_row(row) : -1;
     const bool pub_rec = pub_pair >= 0 && pub_pair < NV;
+    // an intermediate step's store: the pairs past the log-p pair, at their
+    // granule of either parity's line
+    const bool pub_mid = pub_rec && pub_pair >= 2;
+    const int pub_x = 2 * (col >> 1) + (col & 1);
+    const int pub_off = slice * 16 + max(pub_pair, 0);
     // poll passes by kind: record pairs every step, K0 / K1 pairs on the first / last
     uint32_t need_v = 0, need_lp = 0, need_k0 = 0, need_k1 = 0;
 #pragma unroll
@@ -590,32 +595,35 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         f2 lpn = lp;
         float K0[2] = {0.f, 0.f}, K1[2] = {0.f, 0.f};
         MC_STAMP(5);
+        // (the two half kicks of consecutive steps stay separate roundings, as
+        // the reference's; their common product h * g is formed once)
         auto drift_private = [&](bool second_half) {
 #pragma unroll
             for (int r = 0; r < RS; ++r) {
+                const f2 hg = h * g[r];
                 f2 pj = p[r];
-                if (second_half) pj = pj + h * g[r];  // end of the previous step
-                pj = pj + h * g[r];
+                if (second_half) pj = pj + hg;  // end of the previous step
+                pj = pj + hg;
                 p[r] = pj;
                 q[r] = q[r] + e * pj;
             }
         };
         auto drift_shared = [&](bool second_half) {
+            const float hg = xh * sh.g;
             float pj = sh.p;
-            if (second_half) pj = pj + xh * sh.g;
-            pj = pj + xh * sh.g;
+            if (second_half) pj = pj + hg;
+            pj = pj + hg;
             sh.p = pj;
             sh.q = sh.q + xe * pj;
             sh.v = sh.q;
             if (hxf) sh.v = xf_apply(xxf, sh.q);  // (mx.exp(log_sigma) ...: the terms' value)
-            // the shared scale's reciprocals and log (moment form): hardware
-            // v_rcp_f32 / v_log_f32 (<= 1 ulp) instead of the IEEE division
-            // and logf sequences — one dependent chain of ~40 VALU on every
-            // step's critical path becomes 5; the same bits in every slice,
-            // so the replicas stay identical
+            // the shared scale's reciprocals (moment form): hardware v_rcp_f32
+            // (<= 1 ulp) instead of the IEEE division — one dependent chain of
+            // ~40 VALU on every step's critical path becomes 2; the same bits in
+            // every slice, so the replicas stay identical.  Its log (v_log_f32)
+            // is taken on the last step only, where log p is formed.
             sh.is = __builtin_amdgcn_rcpf(sh.v);
             sh.iv = sh.is * sh.is;
-            sh.lg = __builtin_amdgcn_logf(sh.v) * 0.693147180559945f;  // log2 v * ln 2
         };
         f2 M1[RS], M2[RS];
         drift_private(false);
@@ -636,6 +644,8 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             // else it guards the sweep's first register writes with a
             // vmcnt(0) that also waits for this step's own publish store
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+            if constexpr (LAST)  // the shared scales' logs, for log p (log2 v * ln 2)
+                sh.lg = __builtin_amdgcn_logf(sh.v) * 0.693147180559945f;
             MC_STAMP(0);
             constexpr bool lst = LAST;  // log p: the last step only
             // finish the swept term from its moment sums, evaluate the direct
@@ -795,7 +805,14 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             }
             ++epoch;
             const int par = epoch & 1;
-            if (!X1) {
+            if constexpr (!X1 && !FIRST && !LAST) {
+                // an intermediate step: the record pairs only (addresses and
+                // the lane's pair fixed per launch)
+                float pv = xr[0];
+#pragma unroll
+                for (int x = 1; x < 2 * NRS; ++x) pv = (x == pub_x) ? xr[x] : pv;
+                if (pub_mid) granule_store(gline[par] + pub_off, epoch, pv);
+            } else if (!X1) {
                 // one store instruction: the record pairs, and the K items on the
                 // first / last step (lanes 2, 3 of rows 0 / 1)
                 int pp = -1;

@@ -14,3 +14,5 @@ for sh in large medium small; do
   timeout -k 10 120 python -u scripts/stamps_lf.py $sh 256 > gpurun_out/${TAG}_stamps_$sh.log 2>&1 || { echo "stamps $sh failed"; tail -20 gpurun_out/${TAG}_stamps_$sh.log; exit 1; }
   cat gpurun_out/${TAG}_stamps_$sh.log
 done
+timeout -k 10 120 python -u scripts/stamps_nuts.py > gpurun_out/${TAG}_stamps_nuts.log 2>&1 || { echo "stamps nuts failed"; tail -20 gpurun_out/${TAG}_stamps_nuts.log; exit 1; }
+cat gpurun_out/${TAG}_stamps_nuts.log
