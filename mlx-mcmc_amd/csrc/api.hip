@@ -1090,11 +1090,14 @@ static int64_t program_elements(const mc_program* p) {
     for (const DevTerm& t : p->raw) n += t.n;
     return n;
 }
-// The automatic slice count.  Programs of 2 K - 16 K elements are sliced (4
+// The automatic slice count.  Programs of 2 K - 8 K elements are sliced (4
 // ways) only when the lane-resident kernel takes them (measured at 256
 // chains: the D = 100 / N = 10 k and D = 10 / N = 1 k hierarchical models run
 // 2.1x / 1.7x faster than on the chain-per-workgroup kernel); smaller ones
 // stay unsliced (a per-step exchange costs more than the whole evaluation).
+// 8 - 64 K elements: 8 slices (one wave per SIMD, every CU busy at 256
+// chains; the D = 100 / N = 10 k model: 165 -> 185 M steps/s against 4
+// slices, 79 M with 16, profiles/r4/slices).
 static constexpr int64_t kLrAutoMinElements = 2048;
 static int auto_slices(const mc_program* p) {
     if (has_expr(p) || (has_affine(p) && !affine_lanes_ok(p)) ||
@@ -1102,7 +1105,7 @@ static int auto_slices(const mc_program* p) {
         return 1;
     const int64_t n = program_elements(p);
     if (n >= 65536) return 16;
-    if (n >= 16384) return 8;
+    if (n >= 8192) return 8;
     if (n >= kLrAutoMinElements) return 4;
     return 1;
 }
