@@ -109,13 +109,13 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
     // N(m, s_i), config 5): its per-slot constants in registers, read once per
     // launch (lr_dscale_term's arithmetic, no LDS or constant loads per leaf)
     int ddt = -1;
-    float dd_iv[RS], dd_ls[RS], dd_o[RS];
+    float dd_iv[RS], dd_ls[RS], dd_o[RS], dd_c0l[RS];
     bool dd_on[RS];
     int dd_ppo = 0, dd_ko = SK_CONST, dd_jo = 0;
     float dd_w = 0.f, dd_c0 = 0.f, dd_cv = 0.f;
 #pragma unroll
     for (int r = 0; r < RS; ++r) {
-        dd_iv[r] = dd_ls[r] = dd_o[r] = 0.0f;
+        dd_iv[r] = dd_ls[r] = dd_o[r] = dd_c0l[r] = 0.0f;
         dd_on[r] = false;
     }
     if constexpr (REG) {
@@ -139,6 +139,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
             dd_ls[r] = ds ? sd[T->doff[dd_ppo] + toff] : T->clogs;
             dd_iv[r] = ds ? sd[T->doff[2] + toff] : T->cinv2;
             dd_o[r] = dd_ko == SK_DATA ? sd[T->doff[oth] + toff] : 0.0f;
+            dd_c0l[r] = dd_c0 - dd_ls[r];  // (the f32 difference every leaf formed)
         }
     } else if constexpr (SPEC == 1) {
         for (int t = nfast; t < nact; ++t)
@@ -247,6 +248,32 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         if constexpr (SPEC >= 1) {
             // (REG: the one term, whichever list the planner put it in)
             for (int t = REG ? 0 : nfast; t < (REG ? 1 : nact); ++t) {
+                if (REG) {
+                    // the one term, register-resident.  With one chain per
+                    // wave the loc / value role of the parameter drops out:
+                    // d(theta) of -(theta - o)^2 / 2s^2 and of -(o - theta)^2 /
+                    // 2s^2 is the same -(theta - o) / s^2, the squares are equal
+                    // bitwise, and the cotangent 0 + -(w (d iv)) never keeps the
+                    // sign of a zero d — the same bits as the general form below
+                    const f2 w = f2s(dd_w), half = f2s(0.5f);
+                    f2 lpd = {0.f, 0.f};
+#pragma unroll
+                    for (int r = 0; r < RS; ++r) {
+                        if (!dd_on[r]) continue;
+                        const f2 th = {R.q[r][0], R.q[r][1]};
+                        const f2 other = dd_ko == SK_DATA ? f2s(dd_o[r]) : f2s(dd_cv);
+                        const f2 d = th - other;
+                        const f2 iv = f2s(dd_iv[r]);
+                        const f2 lpt = f2s(dd_c0l[r]) - (half * (d * d)) * iv;
+                        lpd += w * lpt;
+                        const f2 gp = (f2){0.f, 0.f} + -(w * (d * iv));
+                        R.g[r][0] = gp[0];
+                        R.g[r][1] = gp[1];
+                    }
+                    lpp[0] += lpd[0];
+                    lpp[1] += lpd[1];
+                    continue;
+                }
                 if (t == ddt) {  // the register-resident data-scale term
                     const f2 w = f2s(dd_w), c0 = f2s(dd_c0), half = f2s(0.5f);
                     const bool ko_sh = !REG && dd_ko == SK_SHARED;  // (REG: no shared)
@@ -495,14 +522,17 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
             const int nleaf = 1 << jd;
             for (int k = 0; k < nleaf; ++k) {
                 // leaf: leapfrog_step(theta, r, v*eps) + hamiltonian (nuts.py:160-164)
+                // (both packed halves in one instruction each: the same IEEE
+                // operations as the per-half form)
 #pragma unroll
-                for (int r = 0; r < RS; ++r)
-#pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        const float pj = R.p[r][hh] + h * R.g[r][hh];
-                        R.p[r][hh] = pj;
-                        R.q[r][hh] = R.q[r][hh] + e * pj;
-                    }
+                for (int r = 0; r < RS; ++r) {
+                    const f2 pj = (f2){R.p[r][0], R.p[r][1]} + f2s(h) * (f2){R.g[r][0], R.g[r][1]};
+                    const f2 qj = (f2){R.q[r][0], R.q[r][1]} + f2s(e) * pj;
+                    R.p[r][0] = pj[0];
+                    R.p[r][1] = pj[1];
+                    R.q[r][0] = qj[0];
+                    R.q[r][1] = qj[1];
+                }
                 {
                     const float pj = sh.p + h * sh.g;
                     sh.p = pj;
@@ -522,8 +552,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     float k = 0.0f;
 #pragma unroll
                     for (int r = 0; r < RS; ++r) {
-#pragma unroll
-                        for (int hh = 0; hh < 2; ++hh) R.p[r][hh] = R.p[r][hh] + h * R.g[r][hh];
+                        const f2 pj =
+                            (f2){R.p[r][0], R.p[r][1]} + f2s(h) * (f2){R.g[r][0], R.g[r][1]};
+                        R.p[r][0] = pj[0];
+                        R.p[r][1] = pj[1];
                         if (lead) k += R.p[r][0] * R.p[r][0];
                     }
                     float ws[2] = {lane_lp, k};
