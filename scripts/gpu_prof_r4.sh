@@ -19,7 +19,8 @@ K50="--steps 1000 --warmup 500 --iters-per-launch 50 --no-cpu-baseline --no-ess 
 K20="--steps 20 --warmup 20 --no-cpu-baseline --no-ess --clock-warm-kind gemm --clock-warm-ms 1000"
 run() {  # name, bench args (quoted), rocprof args...
   local n=$1 args=$2; shift 2
-  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$R/gpurun_out/${TAG}_$n" -o run -- python3 "$R/bench.py" $args > "$R/gpurun_out/${TAG}_$n.log" 2>&1 || { echo "$n failed rc=$?"; grep -v "^ *@" "$R/gpurun_out/${TAG}_$n.log" | tail -5; exit 1; }
+  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "/tmp/prof_${TAG}_$n" -o run -- python3 "$R/bench.py" $args > "$R/gpurun_out/${TAG}_$n.log" 2>&1 || { echo "$n failed rc=$?"; grep -v "^ *@" "$R/gpurun_out/${TAG}_$n.log" | tail -5; exit 1; }
+  python3 "$R/scripts/prof_filter.py" "/tmp/prof_${TAG}_$n" "$R/gpurun_out/${TAG}_$n" && rm -rf "/tmp/prof_${TAG}_$n"
 }
 run kt "$K50" --kernel-trace --stats
 run kt20 "$K20" --kernel-trace --stats
