@@ -170,19 +170,20 @@ MC_DEV float wave_sum(float x) {
     const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 48));
     return ((r0 + r1) + r2) + r3;
 }
-// Two wave_sums side by side (bit-identical to wave_sum of each): the two
-// DPP chains interleave, so a lone wave waits for one chain's latency.
-MC_DEV void wave_sum2(float (&x)[2]) {
+// N wave_sums side by side (bit-identical to wave_sum of each): the N DPP
+// chains interleave, so a lone wave waits for one chain's latency.
+template <int N>
+MC_DEV void wave_sumN(float (&x)[N]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) x[i] += dpp_row<0xB1>(x[i]);
+    for (int i = 0; i < N; ++i) x[i] += dpp_row<0xB1>(x[i]);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) x[i] += dpp_row<0x4E>(x[i]);
+    for (int i = 0; i < N; ++i) x[i] += dpp_row<0x4E>(x[i]);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) x[i] += dpp_row<0x141>(x[i]);
+    for (int i = 0; i < N; ++i) x[i] += dpp_row<0x141>(x[i]);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) x[i] += dpp_row<0x140>(x[i]);
+    for (int i = 0; i < N; ++i) x[i] += dpp_row<0x140>(x[i]);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < N; ++i) {
         const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[i]), 0));
         const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[i]), 16));
         const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x[i]), 32));
@@ -190,6 +191,7 @@ MC_DEV void wave_sum2(float (&x)[2]) {
         x[i] = ((r0 + r1) + r2) + r3;
     }
 }
+MC_DEV void wave_sum2(float (&x)[2]) { wave_sumN<2>(x); }
 
 // A chain group: WPC wavefronts that together own one chain.  With WPC == 1
 // several chains share a workgroup and never use the workgroup barrier.
