@@ -1208,7 +1208,8 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     ok = false;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
+                // (no s_sleep between polls: the round trip paces them, as in
+                // k_hmc_lf)
 #pragma unroll
                 for (int ps = 0; ps < NPASS; ++ps) {
                     if ((need >> ps) & 1u) {

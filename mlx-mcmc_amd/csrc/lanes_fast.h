@@ -895,7 +895,8 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                     ok = false;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
+                // (no s_sleep between polls: the round trip paces them; A/B
+                // medium 186.0 -> 188.8 M steps/s, large +0.3 %, profiles/r4/ab)
                 poll_issue();
                 ready = poll_eval();
             }
