@@ -15,6 +15,6 @@ for sh in small medium; do
 done
 timeout -k 10 300 python -u bench.py --workload nuts > gpurun_out/${TAG}_bench_nuts.json 2> gpurun_out/${TAG}_bench_nuts.err || { echo "bench nuts failed"; tail -20 gpurun_out/${TAG}_bench_nuts.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/${TAG}_bench_nuts.json'));print('nuts', d['value']/1e6, d['roofline']['frac'])"
-timeout -k 10 300 python -u bench.py --workload nuts --nuts-model hier --shape large > gpurun_out/${TAG}_bench_nuts_large.json 2> gpurun_out/${TAG}_bench_nuts_large.err || { echo "bench nuts large failed"; tail -20 gpurun_out/${TAG}_bench_nuts_large.err; exit 1; }
+timeout -k 10 300 python -u bench.py --workload nuts --nuts-model hier --shape large --chains 256 --steps 20 --warmup 20 > gpurun_out/${TAG}_bench_nuts_large.json 2> gpurun_out/${TAG}_bench_nuts_large.err || { echo "bench nuts large failed"; tail -20 gpurun_out/${TAG}_bench_nuts_large.err; exit 1; }
 python -c "import json;d=json.load(open('gpurun_out/${TAG}_bench_nuts_large.json'));print('nuts large', d['value']/1e6, d['roofline']['frac'])"
 echo final done
