@@ -298,12 +298,13 @@ def ess_block(samples, accept_n, K, elapsed):
     if d["n_constant"] or not np.isfinite(rh).all() or np.nanmax(rh) > 1.1:
         out["ess_per_sec"] = None
         out["ess_null_reason"] = (f"split R-hat max {np.nanmax(rh):.3g} > 1.1 over the {K} timed "
-                                  f"draws of {moving.size} moving chains (and {d['n_constant']} "
+                                  f"draws of {n_moving} moving chains (and {d['n_constant']} "
                                   "constant series): the draws are not yet from the posterior")
         return out
-    if np.any(d["ess"] <= 0):
+    # (counted over every rank: each rank takes the same branch)
+    if d["n_nonpositive_ess"] > 0:
         out["ess_per_sec"] = None
-        out["ess_null_reason"] = (f"the reference ESS rule gives {int(np.sum(d['ess'] <= 0))} "
+        out["ess_null_reason"] = (f"the reference ESS rule gives {d['n_nonpositive_ess']} "
                                   "non-positive per-chain ESS values (antithetic draws)")
         return out
     out["ess_per_sec"] = {"min": float(d["ess_sum"].min()) / elapsed,
@@ -372,12 +373,13 @@ def converged_ess(prog, C, q0, dev, L, args, chain_offset=0, world=1):
     if d["n_constant"] or not np.isfinite(rh).all() or np.nanmax(rh) > 1.1:
         out["ess_per_sec"] = None
         out["ess_null_reason"] = f"split R-hat max {np.nanmax(rh):.3g} > 1.1"
-    elif np.any(d["ess"] <= 0):
+    elif d["n_nonpositive_ess"] > 0:
         # the reference rule (examples/06_nuts_comparison.py:22-41) keeps the
         # first autocorrelation below 0.05 even when it is strongly negative
-        # (antithetic HMC draws), which makes n / (1 + 2 sum rho) negative
+        # (antithetic HMC draws), which makes n / (1 + 2 sum rho) negative;
+        # counted over every rank, so every rank takes this branch together
         out["ess_per_sec"] = None
-        out["ess_null_reason"] = (f"the reference ESS rule gives {int(np.sum(d['ess'] <= 0))} "
+        out["ess_null_reason"] = (f"the reference ESS rule gives {d['n_nonpositive_ess']} "
                                   "non-positive per-chain ESS values (antithetic draws)")
     else:
         e = d["ess_sum"]
@@ -515,6 +517,22 @@ def nuts_cpu_baseline(budget_s, args):
                        f"in {dt:.1f} s (a run in progress at the budget's end finishes)")}
 
 
+def nuts_kernel_name(prog) -> str:
+    k = prog.nuts_kernel(10)
+    if k == "sliced":
+        return (f"k_nuts_sl (sliced lane-resident NUTS, one chain per wave, "
+                f"{prog.num_slices} slices)")
+    if k == "lanes":
+        return ("k_nuts_lr (lane-resident, one chain per wave, register-only variant)"
+                if prog.nuts_register_only(10) else "k_nuts_lr (lane-resident, one chain per wave)")
+    return f"k_nuts<{prog.waves_per_chain}>"
+
+
+def nuts_waves_per_chain(prog) -> int:
+    k = prog.nuts_kernel(10)
+    return prog.num_slices if k == "sliced" else (1 if k == "lanes" else prog.waves_per_chain)
+
+
 def main_nuts(args):
     """BASELINE configs[4]: NUTS (depth 10, dual averaging) on the 100-dim
     kappa = 1000 Gaussian; value = leaves (leapfrog steps) of all chains per
@@ -531,7 +549,7 @@ def main_nuts(args):
     world, rank, local, dev = init_ranks()
     C, K, Wm, B = args.chains, args.steps, args.warmup, max(1, args.iters_per_launch)
     lp_fn, init, D, flops_per_leaf, label = nuts_model(args, W.ns_product())
-    prog = _trace.compile_model(lp_fn, init)
+    prog = _trace.compile_model(lp_fn, init, slices=args.slices)
     eps0 = args.nuts_step_size
     chains = _engine.ChainSet(prog, C, prog.layout.flatten(init), eps0, device=dev)
     samples = torch.empty((C, max(K, 1), D), dtype=torch.float32, device=dev)
@@ -595,13 +613,10 @@ def main_nuts(args):
             "roofline": {
                 "bound": "valu_fp32", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
-                "kernel": (("k_nuts_lr (lane-resident, one chain per wave, register-only "
-                            "variant)" if prog.nuts_register_only(10) else
-                            "k_nuts_lr (lane-resident, one chain per wave)")
-                           if prog.nuts_kernel(10) == "lanes" else f"k_nuts<{prog.waves_per_chain}>"),
+                "kernel": nuts_kernel_name(prog),
                 "launch_ms": launch_ms,
                 "iters_per_launch": B, "flops_per_leaf": flops_per_leaf,
-                "note": (f"{C} chains = {C * prog.waves_per_chain} waves on 1024 SIMDs; "
+                "note": (f"{C} chains = {C * nuts_waves_per_chain(prog)} waves on 1024 SIMDs; "
                          + ("F = 5N + 13D flops per leaf (one gradient of the hierarchical "
                             "model)" if hier else "F = 19 D flops per leaf")
                          + " (SURVEY 8d unit: one leaf)")},
@@ -777,6 +792,13 @@ def main():
                 "num_params": D, "num_obs": N, "leapfrog_steps": L, "chains_per_gpu": C,
                 "total_chains": total_chains, "parallelism": f"chains sharded {C}/GPU",
                 "waves_per_chain": prog.waves_per_chain, "slices": prog.num_slices,
+                "step_size0": args.step_size,
+                "step_size0_note": (
+                    "eps0 = the mean step size the reference's warmup rule (hmc.py:157-170) "
+                    "reaches on this model after W = 500 from eps0 = 0.01 (SURVEY 8d's "
+                    "setting), so short runs sample moving chains; HMC throughput does not "
+                    "depend on eps (L = 20 leapfrog steps per iteration either way)"
+                    if args.step_size == CONVERGED_EPS else "eps0 set on the command line"),
             },
             "roofline": {
                 "bound": "valu_fp32", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,

@@ -281,8 +281,11 @@ const char* mc_program_kernel_note(const mc_program* prog);
  * its register-only variant (no broadcast parameter, no scalar term, one
  * Normal term with at most one element per parameter and a data or constant
  * scale: the gradient from per-parameter registers), 0 when it runs k_nuts,
- * -1 on a null program.  All take the reference's decisions; they differ in
- * fp32 summation order only.                                                */
+ * 3 when it runs the sliced NUTS kernel k_nuts_sl (a program sliced onto the
+ * fast-form lane layout of k_hmc_lf: one chain per wave per slice, one record
+ * exchange per leaf; max_tree_depth <= 12 and the LDS arenas fit), -1 on a
+ * null program.  All take the reference's decisions; they differ in fp32
+ * summation order only.                                                     */
 int32_t mc_program_nuts_lanes(const mc_program* prog, int32_t max_tree_depth);
 
 /* Batched tape evaluation: for every point p, logp[p] = log density at
@@ -404,6 +407,11 @@ int mc_debug_lanes_fast(int on);
  * 1 forces the specialised variant (SPEC 1) where the program qualifies,
  * skipping the register-only one.  Trees agree up to fp32 summation order. */
 int mc_debug_nuts_variant(int variant);
+/* Test hook for the sliced NUTS kernel k_nuts_sl (csrc/nuts_sliced.h): 0
+ * runs sliced fast-form programs on k_nuts (the tape) instead, 1 on k_nuts_sl,
+ * -1 restores the default (MC_NUTS_SLICED from the environment, else on).
+ * Trees agree up to fp32 summation order.                                  */
+int mc_debug_nuts_sliced(int on);
 /* Test hooks (host code, no device): the samplers' Box-Muller pair from two
  * Philox words per pair (words [n][2] -> out [n][2] f32) and their f32 log
  * of a uniform in (0, 1] (philox.h mc_box_muller / mc_logf_unit).         */

@@ -214,6 +214,7 @@ SIGNATURES = [
     ("mc_debug_lanes_forms", ctypes.c_int, [ctypes.c_int]),
     ("mc_debug_lanes_fast", ctypes.c_int, [ctypes.c_int]),
     ("mc_debug_nuts_variant", ctypes.c_int, [ctypes.c_int]),
+    ("mc_debug_nuts_sliced", ctypes.c_int, [ctypes.c_int]),
     ("mc_box_muller_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     ("mc_logf_unit_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     ("mc_hmc_run", ctypes.c_int,

@@ -1099,9 +1099,11 @@ class Program:
         return {0: "unsliced", 1: "interpreter", 2: "lanes"}[k]
 
     def nuts_kernel(self, max_tree_depth: int = 10) -> str:
-        """"lanes" (k_nuts_lr) or "tape" (k_nuts): what mc_nuts_run will run."""
+        """"lanes" (k_nuts_lr), "sliced" (k_nuts_sl: a sliced fast-form
+        program, csrc/nuts_sliced.h) or "tape" (k_nuts): what mc_nuts_run will
+        run."""
         k = _lib.load().mc_program_nuts_lanes(self.handle, int(max_tree_depth))
-        return "lanes" if k >= 1 else "tape"
+        return {1: "lanes", 2: "lanes", 3: "sliced"}.get(k, "tape")
 
     def nuts_register_only(self, max_tree_depth: int = 10) -> bool:
         """True when mc_nuts_run runs k_nuts_lr's register-only variant."""

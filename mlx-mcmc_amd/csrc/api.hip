@@ -55,7 +55,6 @@ static int build_segments_ops(DevTerm& dt, int64_t prim_pool, const std::vector<
     sstart.push_back(n);
     // split only when there are fewer groups than tsplit (then <= 2 tsplit
     // virtual segments); otherwise each lane owns whole groups
-    const int64_t Lt = (G >= tsplit) ? INT64_MAX : std::max<int64_t>(1, (n + tsplit - 1) / tsplit);
     struct V {
         int32_t k;
         int64_t start;
@@ -64,21 +63,36 @@ static int build_segments_ops(DevTerm& dt, int64_t prim_pool, const std::vector<
     std::vector<V> vs;
     std::vector<int32_t> comb;
     bool split = false;
-    for (int64_t g = 0; g < G; ++g) {
-        const int64_t len = sstart[g + 1] - sstart[g];
-        const int64_t pieces = (Lt == INT64_MAX) ? 1 : (len + Lt - 1) / Lt;
-        if (pieces > 1) split = true;
-        const int64_t base = len / pieces, rem = len % pieces;
-        comb.push_back(sk[g]);
-        comb.push_back((int32_t)vs.size());
-        comb.push_back((int32_t)pieces);
-        int64_t st = sstart[g];
-        for (int64_t pc = 0; pc < pieces; ++pc) {
-            const int64_t pl = base + (pc < rem ? 1 : 0);
-            if (pl > INT32_MAX) return fail(MC_ERR_UNSUPPORTED, "segment too long");
-            vs.push_back({sk[g], st, (int32_t)pl});
-            st += pl;
+    auto plan_runs = [&](int64_t Lt) {
+        vs.clear();
+        comb.clear();
+        split = false;
+        for (int64_t g = 0; g < G; ++g) {
+            const int64_t len = sstart[g + 1] - sstart[g];
+            const int64_t pieces = (Lt == INT64_MAX) ? 1 : (len + Lt - 1) / Lt;
+            if (pieces > 1) split = true;
+            const int64_t base = len / pieces, rem = len % pieces;
+            comb.push_back(sk[g]);
+            comb.push_back((int32_t)vs.size());
+            comb.push_back((int32_t)pieces);
+            int64_t st = sstart[g];
+            for (int64_t pc = 0; pc < pieces; ++pc) {
+                const int64_t pl = base + (pc < rem ? 1 : 0);
+                if (pl > INT32_MAX) return fail(MC_ERR_UNSUPPORTED, "segment too long");
+                vs.push_back({sk[g], st, (int32_t)pl});
+                st += pl;
+            }
         }
+        return MC_OK;
+    };
+    int rc = plan_runs((G >= tsplit) ? INT64_MAX : std::max<int64_t>(1, (n + tsplit - 1) / tsplit));
+    if (rc) return rc;
+    // the split's partial rows (nprim per virtual segment) must fit the
+    // evaluator's 4T floats of segment scratch; tsplit keeps them within it,
+    // and should a plan not, the runs stay whole (no hard error)
+    if (split && (int64_t)vs.size() * nprim > 4 * (int64_t)T) {
+        rc = plan_runs(INT64_MAX);
+        if (rc) return rc;
     }
     const int64_t nv = (int64_t)vs.size();
     const int64_t ntiles = (nv + 63) / 64;
@@ -152,8 +166,6 @@ static int build_segments_ops(DevTerm& dt, int64_t prim_pool, const std::vector<
     ipool.insert(ipool.end(), lanes.begin(), lanes.end());
     dt.comb_base = (int64_t)ipool.size();
     if (split) ipool.insert(ipool.end(), comb.begin(), comb.end());
-    if (nv * nprim > 4 * (int64_t)T && split)
-        return fail(MC_ERR_UNSUPPORTED, "internal: too many virtual segments");
     return MC_OK;
 }
 
@@ -1887,6 +1899,13 @@ extern "C" int mc_program_create_expr(const mc_term* terms, int32_t n_terms,
         }
     }
 
+    // expression leaves address the pools with 32-bit offsets (eval.h reads
+    // them into lanes): every offset, tiled copies included, lies below the
+    // pools' final sizes, so bounding those bounds them all
+    if (!gnodes.empty() && (dpool.size() > (size_t)INT32_MAX || ipool.size() > (size_t)INT32_MAX))
+        return fail(MC_ERR_UNSUPPORTED,
+                    "expression terms: the data / index pools (%zu / %zu elements) exceed the "
+                    "2^31 elements their 32-bit leaf offsets address", dpool.size(), ipool.size());
     mc_program* p = new mc_program();
     p->D = n_params;
     p->nslots = nslot + 1;

@@ -28,6 +28,7 @@
 #include "lanes.h"
 #include "lanes_fast.h"
 #include "nuts_lanes.h"
+#include "nuts_sliced.h"
 #include "mh.h"
 #include "nuts.h"
 #include "philox.h"

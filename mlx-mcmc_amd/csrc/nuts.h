@@ -20,7 +20,9 @@
 // n += n', s = s' and no_u_turn(trajectory ends) (:275-276).
 // Slice (nuts.py:234-237): log u = f32(-H0) + f32 log U in double; in the
 // reference mode u = f32 exp(f32 log u) with gradual underflow and then
-// log u = f32 log u, so the slice is off (log u = -inf) once log u < ~-103.97
+// log u = f32 log u: u is the smallest denormal (log u ~ -103.28, SURVEY Q7's
+// ~-103.3) down to ln 2^-150 ~ -103.97 and 0 below it, where the slice is off
+// (log u = -inf)
 // (SURVEY Q7).  Dual averaging (nuts.py:298-319) runs in-kernel.
 //
 // Draw addressing: momentum (TAG_MOMENTUM), slice (TAG_SLICE), per depth j

@@ -1,5 +1,5 @@
 // run_nuts.hip — NUTS launches (k_nuts_lr, k_nuts) and mc_nuts_run.
-#include "host.h"
+#include "run_nuts_sl.h"
 
 
 // LDS floats per chain group of k_nuts: group scratch, pending words and,
@@ -18,6 +18,7 @@ static bool nuts_use_lds(const mc_program* p, int32_t max_depth) {
 
 extern "C" int64_t mc_nuts_workspace_bytes(const mc_program* p, int64_t C, int32_t max_depth) {
     if (!p || C < 0 || max_depth < 0 || max_depth > kMaxTreeDepth) return -1;
+    if (use_nuts_sliced(p, max_depth)) return nuts_sl_workspace_bytes(p, C, max_depth);
     if (nuts_use_lds(p, max_depth)) return 0;
     return C * nuts_arena_vectors(max_depth) * (int64_t)dpad_of(p->D) * 4;
 }
@@ -89,6 +90,7 @@ static bool lanes_register_only(const mc_program* p) {
 
 extern "C" int32_t mc_program_nuts_lanes(const mc_program* p, int32_t max_tree_depth) {
     if (!p) return -1;
+    if (use_nuts_sliced(p, max_tree_depth)) return 3;
     if (!use_nuts_lanes(p, max_tree_depth)) return 0;
     return lanes_register_only(p) ? 2 : 1;
 }
@@ -102,6 +104,11 @@ static bool lanes_specialised(const mc_program* p) {
     for (int t = 0; t < nact; ++t)
         if (L.terms[t].sig == LS_GENERIC) return false;
     return true;
+}
+
+extern "C" int mc_debug_nuts_sliced(int on) {
+    g_nuts_sliced = on < 0 ? -1 : (on ? 1 : 0);
+    return MC_OK;
 }
 
 static int g_nuts_variant = -1;  // mc_debug_nuts_variant
@@ -143,8 +150,16 @@ extern "C" int mc_nuts_run(const mc_program* p, const mc_run_config* cfg, void* 
     const int64_t need = mc_nuts_workspace_bytes(p, cfg->num_chains, cfg->max_tree_depth);
     if (need > 0 && (ws == nullptr || ws_bytes < need))
         return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
-    if (ws) ws_forget(ws);  // another kernel's data: a later sliced launch clears it
     hipStream_t st = (hipStream_t)stream;
+    if (use_nuts_sliced(p, cfg->max_tree_depth)) {
+        // (tags continue on this workspace: no ws_forget, nuts_sliced.h)
+        if (device_cus() <= 0) return fail(MC_ERR_HIP, "no HIP device");
+        constexpr int HIER = LF_SW | LF_SWS | LF_DIR | LF_DM | LF_DS;
+        return (p->lr.form == HIER && lanes_forms_enabled())
+                   ? nuts_sl_hier(p, cfg, state, samples, tr, ws, st)
+                   : nuts_sl_rt(p, cfg, state, samples, tr, ws, st);
+    }
+    if (ws) ws_forget(ws);  // another kernel's data: a later sliced launch clears it
     if (use_nuts_lanes(p, cfg->max_tree_depth)) {
         const bool n4 = p->lr.Dsh > 3;
         switch (p->lr.rs) {

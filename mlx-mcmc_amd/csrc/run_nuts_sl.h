@@ -1,0 +1,116 @@
+// run_nuts_sl.h — the sliced NUTS launch (k_nuts_sl, nuts_sliced.h), included
+// by run_nuts_sl.hip (the compile-time hierarchical form) and
+// run_nuts_sl_rt.hip (the run-time form): two translation units so the
+// instantiations compile in parallel.
+#pragma once
+#include "host.h"
+
+// chains (waves) per workgroup of k_nuts_sl
+constexpr int kNslWaves = 8;
+
+// LDS bytes of a k_nuts_sl workgroup: the slice block and scalar terms, then
+// per wave the first-leaf arena and the shared parameters' arena rows
+inline size_t nuts_sl_lds_bytes(const mc_program* p, int max_depth) {
+    return (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm) +
+           (size_t)kNslWaves *
+               ((size_t)nuts_sl_first_floats(p->lr.rs, max_depth) +
+                (size_t)nuts_sl_shared_rows(max_depth) * 4) * 4;
+}
+
+// waves per SIMD the kernel is compiled for: with more than 8 slices a chain
+// block of 8 chains spans more workgroups than there are CUs per two blocks,
+// so two workgroups share a CU (4 waves per SIMD, <= 128 VGPRs); with <= 8
+// one workgroup per CU (2 waves per SIMD).  MC_NUTS_SL_OCC=2|4 overrides.
+inline int nuts_sl_occ(const mc_program* p) {
+    if (const char* e = std::getenv("MC_NUTS_SL_OCC")) {
+        const int v = std::atoi(e);
+        if (v == 2 || v == 4) return v;
+    }
+    return 2;  // (4: the kernel spills at 128 VGPRs; measured slower)
+}
+
+// exchange lines (both parities) for every chain block of C chains
+inline int64_t nuts_sl_line_bytes(const mc_program* p, int64_t C) {
+    const int64_t groups = (C + kNslWaves - 1) / kNslWaves;
+    return 2 * groups * kNslWaves * (int64_t)p->lr.S * kNslLine * 8;
+}
+
+template <int RS, int NSH, int OCC, int FORM>
+inline int launch_nuts_sl(const mc_program* p, const mc_run_config* cfg, void* state,
+                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
+    auto kern = k_nuts_sl<RS, NSH, kNslWaves, OCC, FORM>;
+    int64_t qo, go;
+    mc_state_offsets(p, cfg->num_chains, &qo, &go);
+    char* b = (char*)state;
+    RunArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.cfg = *cfg;
+    const LrCtx ctx = lrctx_of(p);
+    const int maxj = cfg->max_tree_depth;
+    const size_t lds = nuts_sl_lds_bytes(p, maxj);
+    MC_HIP_TRY(allow_lds(kern, lds));
+    const int64_t C = cfg->num_chains;
+    const int64_t groups = (C + kNslWaves - 1) / kNslWaves;
+    const int S = p->lr.S;
+    const int64_t cap = resident_capacity(kern, 64 * kNslWaves, lds);
+    if (cap < S)
+        return fail(MC_ERR_UNSUPPORTED,
+                    "sliced NUTS: a chain block's %d workgroups must be co-resident, the device "
+                    "holds %lld of this kernel", S, (long long)cap);
+    const int64_t gpl = std::min(groups, cap / S);
+    const int64_t lines = nuts_sl_line_bytes(p, C);
+    int* status = (int*)ws;
+    unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
+    float* pool = (float*)((char*)ws + kSlStatusBytes + lines);
+    A.fault = g_exchange_fault;
+    // tags: one per leaf, at most iter_count * 2^maxj leaves per chain
+    const uint64_t per_launch = (uint64_t)cfg->iter_count * (1ull << maxj) + 1;
+    const int64_t nlaunch = (groups + gpl - 1) / gpl;
+    uint32_t base = 0;
+    if (ws_reserve(ws, per_launch * (uint64_t)nlaunch, (uint64_t)(kSlStatusBytes + lines), &base))
+        MC_HIP_TRY(hipMemsetAsync(ws, 0, kSlStatusBytes + lines, st));
+    ws_mark_status(ws);
+    for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
+        const int64_t ng = std::min(gpl, groups - g0);
+        const hipError_t e = launch_exchange(
+            kern, ng * S, 64 * kNslWaves, lds, st, ctx, A, g0 * kNslWaves, ng,
+            (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples, trace_of(tr), xch,
+            pool, status, base);
+        MC_HIP_TRY(e);
+        base += (uint32_t)per_launch;
+    }
+    return MC_OK;
+}
+
+// the compile-time hierarchical form (run_nuts_sl.hip) and the run-time form
+// (run_nuts_sl_rt.hip)
+int nuts_sl_hier(const mc_program* p, const mc_run_config* cfg, void* state, float* samples,
+                 const mc_trace* tr, void* ws, hipStream_t st);
+int nuts_sl_rt(const mc_program* p, const mc_run_config* cfg, void* state, float* samples,
+               const mc_trace* tr, void* ws, hipStream_t st);
+
+// The sliced NUTS kernel runs programs the automatic plan slices (S >= 2)
+// onto the fast-form lane layout (k_hmc_lf's programs), unless
+// MC_NUTS_SLICED=0 in the environment or mc_debug_nuts_variant(0) (A/B and
+// tests: k_nuts on the tape), the slice kernel is forced to the interpreter,
+// max_tree_depth is outside [1, kNslMaxDepth] or the LDS arenas do not fit.
+inline int g_nuts_sliced = -1;  // mc_debug_nuts_sliced; -1: MC_NUTS_SLICED
+inline bool nuts_sliced_enabled() {
+    if (g_nuts_sliced < 0) {
+        const char* e = std::getenv("MC_NUTS_SLICED");
+        g_nuts_sliced = (e && e[0] == '0') ? 0 : 1;
+    }
+    return g_nuts_sliced == 1;
+}
+inline bool use_nuts_sliced(const mc_program* p, int max_depth) {
+    return nuts_sliced_enabled() && p->sl.S >= 2 && p->lr.ok && p->lr.fast &&
+           lanes_fast_enabled() && p->lr.S >= 2 && p->lr.S <= kLrSlices &&
+           p->slice_kernel != 1 && max_depth >= 1 && max_depth <= kNslMaxDepth &&
+           nuts_sl_lds_bytes(p, max_depth) <= (size_t)kSlLdsBudget;
+}
+// status word, exchange lines, then the candidate pool of every chain
+inline int64_t nuts_sl_workspace_bytes(const mc_program* p, int64_t C, int max_depth) {
+    const int64_t groups = (C + kNslWaves - 1) / kNslWaves;
+    return kSlStatusBytes + nuts_sl_line_bytes(p, C) +
+           groups * kNslWaves * (int64_t)p->lr.S * nuts_sl_pool_floats(p->lr.rs, max_depth) * 4;
+}

@@ -1,0 +1,16 @@
+// run_nuts_sl_rt.hip — sliced NUTS, run-time form (k_nuts_sl<..., FORM = -1>):
+// fast-form programs whose slices differ in their terms or share roles.
+#include "run_nuts_sl.h"
+
+int nuts_sl_rt(const mc_program* p, const mc_run_config* cfg, void* state, float* samples,
+               const mc_trace* tr, void* ws, hipStream_t st) {
+    const bool n4 = p->lr.Dsh > 3;
+    switch (p->lr.rs) {
+        case 1: return n4 ? launch_nuts_sl<1, 4, 2, -1>(p, cfg, state, samples, tr, ws, st)
+                          : launch_nuts_sl<1, 3, 2, -1>(p, cfg, state, samples, tr, ws, st);
+        case 2: return n4 ? launch_nuts_sl<2, 4, 2, -1>(p, cfg, state, samples, tr, ws, st)
+                          : launch_nuts_sl<2, 3, 2, -1>(p, cfg, state, samples, tr, ws, st);
+        default: return n4 ? launch_nuts_sl<4, 4, 2, -1>(p, cfg, state, samples, tr, ws, st)
+                           : launch_nuts_sl<4, 3, 2, -1>(p, cfg, state, samples, tr, ws, st);
+    }
+}

@@ -98,8 +98,9 @@ def chain_diagnostics(samples, max_lag: int = MAX_LAG, group=None) -> Dict[str, 
     """ESS and split R-hat per element of a [C, S, D] buffer.
 
     Returns ``ess`` [C, D] (this rank's chains), ``ess_sum`` [D] (summed over
-    every chain of every rank), ``rhat`` [D] (NaN unless S >= 4) and
-    ``n_constant`` (series of zero variance over all ranks).  With an
+    every chain of every rank), ``rhat`` [D] (NaN unless S >= 4),
+    ``n_constant`` (series of zero variance over all ranks) and
+    ``n_nonpositive_ess`` (per-chain ESS values <= 0 over all ranks).  With an
     initialised process group (pass ``group=False`` to stay local) the chain
     sums are all-reduced over the ranks' shards.
     """
@@ -118,13 +119,16 @@ def chain_diagnostics(samples, max_lag: int = MAX_LAG, group=None) -> Dict[str, 
         _lib.check(lib.mc_stats_reduce(C, S, D, _lib.ptr(st), None, 0, _lib.ptr(red), stream))
     # [split chains, constant series]: a constant series scores ESS = n by
     # the reference rule, so callers need to know how many there are
+    # and non-positive per-chain ESS values (the reference rule on antithetic
+    # draws): every rank's count, so every rank takes the same branch on them
     counts = torch.stack([torch.tensor(2.0 * C, dtype=torch.float64, device=x.device),
-                          (st[_lib.MC_ST_M2] == 0).sum().to(torch.float64)])
+                          (st[_lib.MC_ST_M2] == 0).sum().to(torch.float64),
+                          (st[_lib.MC_ST_ESS] <= 0).sum().to(torch.float64)])
     _all_reduce(red, group)
     _all_reduce(counts, group)
     ess_sum = red[1].clone()
     rhat = torch.full((D,), float("nan"), dtype=torch.float64, device=x.device)
-    m_total, n_const = (int(v) for v in counts.tolist())
+    m_total, n_const, n_nonpos = (int(v) for v in counts.tolist())
     m = m_total
     if S >= 4 and m >= 2:
         center = red[0].contiguous()
@@ -136,7 +140,7 @@ def chain_diagnostics(samples, max_lag: int = MAX_LAG, group=None) -> Dict[str, 
         _lib.check(lib.mc_rhat(D, m, S, _lib.ptr(spread), _lib.ptr(rhat), stream))
     return {"ess": st[_lib.MC_ST_ESS].view(C, D).cpu().numpy(),
             "ess_sum": ess_sum.cpu().numpy(), "rhat": rhat.cpu().numpy(),
-            "n_constant": n_const}
+            "n_constant": n_const, "n_nonpositive_ess": n_nonpos}
 
 
 # ------------------------------------------------------------ summary -----

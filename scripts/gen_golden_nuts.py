@@ -10,6 +10,9 @@ test infrastructure, run here on the CPU and committed.
       The README "Large" hierarchical model (D = 1000, N = 100 K), chains 0,
       1, 2, seed 0, a fixed step size 2e-3 (adapt_step_size=False), W = 2,
       S = 10, max_tree_depth 10 (depths 7-8).
+  tests/golden/nuts_large_da_trace.npz
+      The same model and chains 0, 1 with dual averaging acting: eps0 = 2e-3,
+      W = 20, S = 5 (the sliced NUTS kernel's adaptation check).
   tests/golden/nuts_hier_trace.npz
       The small hierarchical model (workloads.hierarchical, G = 7, N = 1 K:
       broadcast mu, tau, sigma and private theta), chains 0, 2 and 5 (5: the
@@ -22,7 +25,7 @@ alpha, step size, H0, the f32 log U of the slice draw, and the decision
 margins (smallest slice gap |log u + H'|, divergence gap, relative U-turn
 dot; oracle/samplers.py nuts); the S stored draws [S, D].
 
-    python scripts/gen_golden_nuts.py [illcond hier large]
+    python scripts/gen_golden_nuts.py [illcond hier large large_da]
 """
 import json
 import os
@@ -44,6 +47,10 @@ RUNS = {
     "large": dict(chains=(0, 1, 2), cfg=dict(num_warmup=2, num_samples=10, step_size=2e-3,
                                           max_tree_depth=10, target_accept=0.65,
                                           adapt_step_size=False)),
+    # the same model with the reference's dual averaging acting (VERDICT r4
+    # "Next round" 1): W = 20 warmup iterations from eps0 = 2e-3, S = 5
+    "large_da": dict(chains=(0, 1), cfg=dict(num_warmup=20, num_samples=5, step_size=2e-3,
+                                             max_tree_depth=10, target_accept=0.65)),
 }
 SEED = 0
 KEYS = ("depth", "leaves", "alpha", "step_size", "energy", "slice_gap", "div_gap",
@@ -55,7 +62,7 @@ def model(name, ns):
 
     if name == "illcond":
         return W.illcond_normal(ns)
-    if name == "large":
+    if name in ("large", "large_da"):
         return W.hierarchical(ns, *W.SHAPES["large"])
     return W.hierarchical(ns, *W.SHAPES["small"])
 

@@ -63,6 +63,8 @@ def _fixture(name):
 def _model(name, ns):
     if name == "illcond":
         return W.illcond_normal(ns)
+    if name in ("medium", "large", "large_da"):
+        return W.hierarchical(ns, *W.SHAPES["large" if name.startswith("large") else name])
     return W.hierarchical(ns, *W.SHAPES["small"])
 
 
@@ -193,15 +195,17 @@ def test_nuts_trace_against_oracle(gpu, name, variant):
     assert max(depths_seen) >= 3, "real trees"
 
 
-def test_nuts_large_shape_against_oracle(gpu):
+@pytest.mark.parametrize("slices,kernel", [(0, "sliced"), (8, "sliced"), (1, "tape")])
+def test_nuts_large_shape_against_oracle(gpu, slices, kernel):
     """NUTS on the README "Large" model (D = 1000, N = 100 K; VERDICT r3
-    "Next round" 6): the kernel the automatic plan picks (k_nuts: the model
-    is sliced, not one lane-resident slice) against the oracle's trace at a
-    fixed step size (tests/golden/nuts_large_trace.npz, chains 0-2, depths
-    7-8): trees identical until a near-tie proven by the oracle's own margins
-    (slice / divergence gap or relative U-turn dot within the tie bound of
-    the iteration), H0 within the tie bound before it, alpha within its
-    relative error, stored draws within rtol 1e-4."""
+    "Next round" 6, r4 "Next round" 1): the sliced kernel k_nuts_sl on the
+    automatic plan (16 slices) and on 8 slices, and k_nuts on the tape,
+    against the oracle's trace at a fixed step size
+    (tests/golden/nuts_large_trace.npz, chains 0-2, depths 7-8): trees
+    identical until a near-tie proven by the oracle's own margins (slice /
+    divergence gap or relative U-turn dot within the tie bound of the
+    iteration), H0 within the tie bound before it, alpha within its relative
+    error, stored draws within rtol 1e-4."""
     import mlx_mcmc_amd as m
 
     fx = _fixture("large")
@@ -211,8 +215,10 @@ def test_nuts_large_shape_against_oracle(gpu):
                            step_size=cfg["step_size"], max_tree_depth=cfg["max_tree_depth"],
                            adapt_step_size=False, target_accept=cfg["target_accept"],
                            key=m.random.key(cfg["seed"]), num_chains=4, progress=False,
-                           return_info=True, return_trace=True, keep_on_device=True)
+                           return_info=True, return_trace=True, keep_on_device=True,
+                           num_slices=slices)
     print("large NUTS kernel:", info.extra["kernel"])
+    assert info.extra["kernel"] == kernel
     n = cfg["num_warmup"] + cfg["num_samples"]
     tr = info.trace
     D = info.device_samples.shape[-1]
@@ -247,3 +253,38 @@ def test_nuts_large_shape_against_oracle(gpu):
         assert same >= 6, f"chain {chain}: compared only {same}"
         assert fx["depth"][j][:same].max() >= 7
     print("large NUTS: identical trees over", total, "chain-iterations")
+
+
+@pytest.mark.parametrize("slices", [0, 8])
+def test_nuts_large_dual_averaging_against_oracle(gpu, slices):
+    """The Large model with the reference's dual averaging acting (VERDICT r4
+    "Next round" 1; tests/golden/nuts_large_da_trace.npz: eps0 = 2e-3, W = 20,
+    S = 5, chains 0 and 1) on the sliced kernel: the strict replay (the
+    oracle re-runs each chain with the GPU's own step sizes, trees identical
+    until a proven near-tie, the GPU's dual averaging recomputed from its own
+    acceptance statistics reproduces its step sizes) and the committed trace
+    (the oracle's own adaptation) identical for MIN_SAME iterations."""
+    import mlx_mcmc_amd as m
+
+    fx = _fixture("large_da")
+    cfg = fx["config"]
+    lp, init = W.hierarchical(W.ns_product(), *W.SHAPES["large"])
+    s, rate, info = m.nuts(lp, init, num_samples=cfg["num_samples"], num_warmup=cfg["num_warmup"],
+                           step_size=cfg["step_size"], max_tree_depth=cfg["max_tree_depth"],
+                           target_accept=cfg["target_accept"], key=m.random.key(cfg["seed"]),
+                           num_chains=4, progress=False, return_info=True, return_trace=True,
+                           keep_on_device=True, num_slices=slices)
+    assert info.extra["kernel"] == "sliced"
+    n = cfg["num_warmup"] + cfg["num_samples"]
+    tr = info.trace
+    depths = []
+    for j, chain in enumerate(fx["chains"]):
+        chain = int(chain)
+        same, d = _replay("large_da", fx, info, j, chain)
+        depths.extend(d.tolist())
+        same_fx = _first_flip(tr["tree_depth"][chain], tr["n_leapfrog"][chain], fx["depth"][j],
+                              fx["leaves"][j], n)
+        print(f"large_da chain {chain}: replay identical for {same} of {n}; committed trace "
+              f"for {same_fx}")
+        assert same_fx >= MIN_SAME, f"chain {chain}: trees diverge from the fixture at {same_fx}"
+    assert max(depths) >= 5, "real trees"
