@@ -412,6 +412,27 @@ int mc_debug_nuts_variant(int variant);
  * -1 restores the default (MC_NUTS_SLICED from the environment, else on).
  * Trees agree up to fp32 summation order.                                  */
 int mc_debug_nuts_sliced(int on);
+/* Expression terms (MC_DIST_EXPR) compiled per program (csrc/jit.hip):
+ * hiprtc compiles the tape kernels' expression instantiations with each
+ * term's node DAG as straight-line code (the interpreter's operations in its
+ * order: bit-identical results), at the first launch that needs them; code
+ * objects are cached per structure in the process and on disk ($MC_JIT_CACHE,
+ * else ~/.cache/mcmc355).  mc_debug_expr_jit: 0 keeps the interpreter, 1 the
+ * JIT, -1 the default (MC_EXPR_JIT from the environment, else on).
+ * mc_program_expr_jit: 1 when the program's expression terms run compiled,
+ * 0 when it has none or the JIT is off, -2 when their compilation failed (the
+ * interpreter runs; mc_program_kernel_note says why), -1 on a null program. */
+int mc_debug_expr_jit(int on);
+int32_t mc_program_expr_jit(const mc_program* prog);
+/* Test hooks without a device: mc_debug_program_host_only(1) makes the next
+ * programs built on this thread host tables only (never launch them);
+ * mc_debug_expr_jit_source copies the generated source of a program's
+ * expression terms (returns its length); mc_debug_expr_jit_compile compiles
+ * it into `kernel` (e.g. "mc::k_hmc<8, true, true>"), MC_OK or the
+ * compiler's log as the error.                                              */
+int mc_debug_program_host_only(int on);
+int64_t mc_debug_expr_jit_source(const mc_program* prog, char* buf, int64_t cap);
+int mc_debug_expr_jit_compile(const mc_program* prog, const char* kernel);
 /* Test hooks (host code, no device): the samplers' Box-Muller pair from two
  * Philox words per pair (words [n][2] -> out [n][2] f32) and their f32 log
  * of a uniform in (0, 1] (philox.h mc_box_muller / mc_logf_unit).         */

@@ -3,6 +3,9 @@
 // include/mcmc355.h (the sampler launches are in run_hmc.hip, run_mh.hip,
 // run_nuts.hip).
 #include "host.h"
+#include "jit.h"
+
+static thread_local bool g_program_host_only;
 #include "diag.h"  // (non-template kernels: this unit only)
 static bool is_vec_kind(int k) { return k == MC_OP_DATA || k == MC_OP_PVEC || k == MC_OP_GATHER; }
 static bool is_acc_vec(int k) { return k == MC_OP_PVEC || k == MC_OP_GATHER; }
@@ -1269,6 +1272,12 @@ extern "C" int32_t mc_program_num_slices(const mc_program* p) { return p ? p->sl
 
 extern "C" const char* mc_program_kernel_note(const mc_program* p) {
     if (!p) return "";
+    const std::string je = jit_error(p);
+    if (!je.empty()) {  // (the interpreter runs the expression terms)
+        static thread_local std::string buf;
+        buf = "expression JIT: compilation failed, the interpreter runs: " + je;
+        return buf.c_str();
+    }
     return (mc_program_slice_kernel(p) == 2) ? "" : p->note.c_str();
 }
 
@@ -1919,6 +1928,10 @@ extern "C" int mc_program_create_expr(const mc_term* terms, int32_t n_terms,
     p->ex = !gnodes.empty();
     p->h_data = dpool;
     p->h_index = ipool;
+    if (g_program_host_only) {  // test hook: the host tables only (no device)
+        *out = p;
+        return MC_OK;
+    }
     hipError_t e = hipSuccess;
     if (!dts.empty()) {
         e = hipMalloc(&p->d_terms, dts.size() * sizeof(DevTerm));
@@ -1960,8 +1973,18 @@ extern "C" int mc_program_create_expr(const mc_term* terms, int32_t n_terms,
     return MC_OK;
 }
 
+// Test hook (mc_debug_program_host_only): programs built after it is set keep
+// their host tables only — no device upload, no slice plan — for host-side
+// checks without a GPU (the expression JIT's code generation and compilation,
+// mc_debug_expr_jit_compile).  Such a program must not be launched.
+extern "C" int mc_debug_program_host_only(int on) {
+    g_program_host_only = on != 0;
+    return MC_OK;
+}
+
 extern "C" int mc_program_destroy(mc_program* p) {
     if (!p) return MC_OK;
+    jit_free(p);
     free_slices(p->sl);
     free_lanes(p->lr);
     if (p->d_terms) (void)hipFree(p->d_terms);

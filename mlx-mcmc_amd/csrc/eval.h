@@ -25,7 +25,9 @@
 // there is no per-element division.  This is the same arithmetic as the
 // per-element formulas up to fp32 rounding order.
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#endif
 #include "internal.h"
 
 #define MC_DEV __device__ __forceinline__
@@ -1018,6 +1020,17 @@ MC_DEV void eval_expr_n(const DevTerm& T, const DevCtx& P, const float* q, float
     }
 }
 
+#ifdef MC_JIT
+// The program's expression terms compiled to straight-line code (jit.hip:
+// generated per program, compiled by hiprtc into the tape kernels' EX
+// instantiations): the same operations in the same order as eval_expr_n's
+// node walk, so the results are bit-identical to the interpreter's.
+template <int WPC, bool VALUE_ONLY>
+MC_DEV void mc_jit_expr(const DevTerm& T, const DevCtx& P, const float* q, float* g,
+                        const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc,
+                        float* vpart);
+#endif
+
 // (only in the EX kernel instantiations: the node arrays would otherwise
 // raise the register count of every tape kernel.  Both variants are inlined:
 // a call in a kernel turned every uniform branch of it into an exec-masked
@@ -1026,6 +1039,10 @@ template <int WPC, bool VALUE_ONLY>
 MC_DEV void eval_expr(const DevTerm& T, const DevCtx& P, const float* q, float* g,
                       const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc,
                       float* vpart) {
+#ifdef MC_JIT
+    mc_jit_expr<WPC, VALUE_ONLY>(T, P, q, g, G, task, tid, nthr, lp_acc, vpart);
+    return;
+#endif
     if (T.expr_n <= 16)
         eval_expr_n<WPC, VALUE_ONLY, 16>(T, P, q, g, G, task, tid, nthr, lp_acc, vpart);
     else

@@ -134,6 +134,9 @@ struct mc_program {
     // why the automatic plan did not reach the lane-resident kernel ("" when it
     // did or was not asked to): mc_program_kernel_note
     std::string note;
+    // the expression-term JIT's compiled kernels (jit.hip JitState), created
+    // at the first launch that uses them
+    mutable void* jit = nullptr;
 };
 
 inline DevCtx ctx_of(const mc_program* p) {

@@ -1,0 +1,460 @@
+// jit.hip — expression terms compiled per program (VERDICT r4 "Next round" 3).
+//
+// The reference differentiates any MLX expression with mx.grad
+// (kernels/hmc.py:53-67); the engine records such terms as node DAGs
+// (MC_DIST_EXPR, eval.h eval_expr_n) and, by default, walks them with an
+// interpreter: ~23 instructions of decode / dispatch / indirect register
+// moves per node visit.  Here the DAG of every expression term
+// of a program becomes straight-line C++ — each node's forward value and
+// reverse step through the interpreter's own ex_fwd / ex_bwd with the op
+// folded to a constant, adjoints accumulated in the interpreter's order —
+// and hiprtc compiles the tape kernels' EX instantiations (k_hmc, k_nuts,
+// k_mh) with it (eval.h MC_JIT hook).  The arithmetic is the interpreter's,
+// operation for operation, so a JIT-compiled run is bit-identical to an
+// interpreted one (tests/test_gpu_expr_jit.py).
+//
+// The generated code depends only on the DAGs' structure (ops, argument
+// edges, leaf kinds, passes): leaf offsets, pools, slots and constants are
+// read from the program's node table at run time (scalar loads), so models of
+// the same structure share one code object whatever their data.  Code
+// objects are cached per (source, kernel, options) in the process and on disk
+// ($MC_JIT_CACHE, else ~/.cache/mcmc355; unwritable: in-process only).
+// MC_EXPR_JIT=0 in the environment (or mc_debug_expr_jit(0)) keeps the
+// interpreter; a failed compilation falls back to it with a kernel note.
+#include <hip/hiprtc.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <fstream>
+#include <sstream>
+
+#include "host.h"
+#include "jit.h"
+#include "jit_src.inc"
+
+namespace {
+
+int g_expr_jit = -1;  // mc_debug_expr_jit; -1: MC_EXPR_JIT from the environment
+
+struct JitState {
+    std::mutex mu;
+    bool have_src = false;
+    std::string src;
+    std::map<std::pair<std::string, int>, hipFunction_t> fns;  // (kernel, device)
+    std::vector<hipModule_t> mods;
+    std::string error;  // the last compilation failure ("" if none)
+};
+
+std::mutex g_cache_mu;
+// code objects by cache key, shared by every program of the process
+std::unordered_map<uint64_t, std::pair<std::string, std::string>> g_code;  // key -> (name, code)
+
+uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) {
+        h ^= b[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+uint64_t fnv1a(uint64_t h, const std::string& s) { return fnv1a(h, s.data(), s.size() + 1); }
+
+std::string cache_dir() {
+    if (const char* e = std::getenv("MC_JIT_CACHE")) return e;
+    if (const char* h = std::getenv("HOME")) return std::string(h) + "/.cache/mcmc355";
+    return "";
+}
+
+// One expression term's evaluator, the structure of eval_expr_n with the node
+// loops unrolled.  Node k's value is vK, its adjoint aK, its partial pK.
+void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
+    const int nn = T.expr_n;
+    const bool seg = T.primary >= 0;
+    auto is_part = [&](int k) {  // partial accumulators: broadcast and gathered (run) leaves
+        return N[k].op == MC_EX_LEAF && (N[k].leaf.kind == MC_OP_PSCALAR || N[k].prim != 0);
+    };
+    o << "template <int WPC, bool VALUE_ONLY>\n"
+      << "MC_DEV void jit_t" << T.expr_base
+      << "(const DevTerm& T, const DevCtx& P, const float* q, float* g, const Group<WPC>& G,\n"
+      << "    bool task, int tid, int nthr, float& lp_acc, float* vpart) {\n"
+      << "  (void)task; (void)tid; (void)nthr; (void)vpart; (void)G;\n"
+      << "  const MC_CONST DevExprNode* N = cptr(P.nodes) + T.expr_base;\n"
+      << "  const float w = T.weight;\n";
+    // the leaves' run-time fields (uniform: scalar loads)
+    for (int k = 0; k < nn; ++k) {
+        if (N[k].op == MC_EX_LEAF) {
+            const int kind = N[k].leaf.kind;
+            if (N[k].prim || kind == MC_OP_PSCALAR || kind == MC_OP_PVEC || kind == MC_OP_GATHER)
+                o << "  const int o" << k << " = N[" << k << "].leaf.poff;\n";
+            if (!N[k].prim && (kind == MC_OP_DATA || kind == MC_OP_GATHER))
+                o << "  const int64_t l" << k << " = N[" << k << "].leaf.pool;\n";
+            if (!N[k].prim && kind == MC_OP_CONST)
+                o << "  const float c" << k << " = N[" << k << "].leaf.cval;\n";
+            if (kind == MC_OP_PSCALAR) o << "  const int s" << k << " = N[" << k << "].leaf.slot;\n";
+        } else {
+            o << "  const float c" << k << " = N[" << k << "].leaf.cval;\n";
+        }
+    }
+    o << "  const int npass = VALUE_ONLY ? 1 : T.npass;\n"
+      << "  for (int pass = 0; pass < npass; ++pass) {\n";
+    for (int k = 0; k < nn; ++k)
+        if (is_part(k)) o << "    float p" << k << " = 0.0f;\n";
+    o << "    auto element = [&](int64_t e, int kr) {\n"
+      << "      (void)e; (void)kr;\n";
+    auto arg = [&](int a) { return a >= 0 ? "v" + std::to_string(a) : std::string("0.0f"); };
+    for (int k = 0; k < nn; ++k) {
+        const DevExprNode& d = N[k];
+        o << "      const float v" << k << " = ";
+        if (d.op == MC_EX_LEAF) {
+            const int kind = d.leaf.kind;
+            if (d.prim) o << "q[o" << k << " + kr]";
+            else if (kind == MC_OP_CONST) o << "c" << k;
+            else if (kind == MC_OP_PSCALAR) o << "q[o" << k << "]";
+            else if (kind == MC_OP_DATA) o << "P.data[l" << k << " + e]";
+            else if (kind == MC_OP_PVEC) o << "q[o" << k << " + e]";
+            else o << "q[o" << k << " + P.index[l" << k << " + e]]";
+        } else {
+            o << "ex_fwd(" << d.op << ", " << arg(d.a) << ", " << arg(d.b) << ", " << arg(d.c)
+              << ", c" << k << ")";
+        }
+        o << ";\n";
+    }
+    o << "      if (pass == 0) lp_acc += w * v" << nn - 1 << ";\n"
+      << "      if constexpr (VALUE_ONLY) return;\n";
+    for (int k = 0; k < nn; ++k) o << "      float a" << k << " = 0.0f;\n";
+    o << "      a" << nn - 1 << " = w;\n";
+    for (int k = nn - 1; k >= 0; --k) {
+        const DevExprNode& d = N[k];
+        if (d.op == MC_EX_LEAF) {
+            const int kind = d.leaf.kind;
+            if (is_part(k)) {
+                o << "      p" << k << " += a" << k << ";\n";
+            } else if (kind == MC_OP_PVEC || kind == MC_OP_GATHER) {
+                o << "      if (pass == " << (d.pass & 15) << ") g[";
+                if (kind == MC_OP_PVEC) o << "(int64_t)o" << k << " + e";
+                else o << "(int64_t)o" << k << " + P.index[l" << k << " + e]";
+                o << "] += a" << k << ";\n";
+            }
+            continue;
+        }
+        o << "      { float dx, dy, dz; ex_bwd(" << d.op << ", " << arg(d.a) << ", " << arg(d.b)
+          << ", " << arg(d.c) << ", v" << k << ", a" << k << ", c" << k << ", dx, dy, dz);\n"
+          << "        a" << d.a << " += dx;";
+        if (d.b >= 0) o << " a" << d.b << " += dy;";
+        if (d.c >= 0) o << " a" << d.c << " += dz;";
+        o << " }\n";
+    }
+    o << "    };\n";
+    if (!seg) {
+        o << "    for (int64_t i = tid; i < T.n; i += nthr) element(i, 0);\n";
+    } else {
+        o << "    const bool split = T.ncomb > 0;\n"
+          << "    const int wave = G.tid >> 6;\n"
+          << "    const int lane = G.tid & 63;\n"
+          << "    const MC_CONST int* tiles = cptr(P.index) + T.tile_base;\n"
+          << "    const int* lanes = P.index + T.lane_base;\n"
+          << "    for (int t = wave; t < T.ntiles; t += WPC) {\n"
+          << "      const int off = tiles[3 * t];\n"
+          << "      const int v = t * 64 + lane;\n"
+          << "      const bool valid = v < T.nvirt;\n"
+          << "      const int kr = valid ? lanes[2 * v] : 0;\n"
+          << "      const int len = valid ? lanes[2 * v + 1] : 0;\n";
+        for (int k = 0; k < nn; ++k)
+            if (N[k].op == MC_EX_LEAF && N[k].prim) o << "      p" << k << " = 0.0f;\n";
+        o << "      for (int u = 0; u < len; ++u) element(seg_elem(off, u, lane), kr);\n"
+          << "      if (!VALUE_ONLY && valid) {\n";
+        for (int k = 0; k < nn; ++k) {
+            if (N[k].op != MC_EX_LEAF || !N[k].prim) continue;
+            o << "        if (pass == " << N[k].pass << ") { if (split) vpart[" << (N[k].prim - 1)
+              << " * T.nvirt + v] = p" << k << "; else g[o" << k << " + kr] += p" << k << "; }\n";
+        }
+        o << "      }\n"
+          << "    }\n"
+          << "    if (!VALUE_ONLY && split) {\n"
+          << "      G.sync();\n"
+          << "      const int* comb = P.index + T.comb_base;\n"
+          << "      for (int c = G.tid; c < T.ncomb; c += G.T) {\n"
+          << "        const int kc = comb[3 * c], vf = comb[3 * c + 1], vc = comb[3 * c + 2];\n"
+          << "        (void)kc; (void)vf; (void)vc;\n";
+        for (int k = 0; k < nn; ++k) {
+            if (N[k].op != MC_EX_LEAF || !N[k].prim) continue;
+            o << "        if (pass == " << N[k].pass << ") {\n"
+              << "          const float* vp = vpart + " << (N[k].prim - 1) << " * T.nvirt;\n"
+              << "          float sum = vp[vf];\n"
+              << "          for (int j = 1; j < vc; ++j) sum += vp[vf + j];\n"
+              << "          g[o" << k << " + kc] += sum;\n"
+              << "        }\n";
+        }
+        o << "      }\n"
+          << "    }\n";
+    }
+    o << "    if (!VALUE_ONLY && pass == 0) {\n";
+    for (int k = 0; k < nn; ++k) {
+        if (N[k].op != MC_EX_LEAF || N[k].leaf.kind != MC_OP_PSCALAR) continue;
+        o << "      if (task) flush_slot_task(G, s" << k << ", p" << k << "); else flush_slot(G, s" << k
+          << ", p" << k << ");\n";
+    }
+    o << "    }\n"
+      << "    if (!VALUE_ONLY && pass + 1 < npass) G.sync();\n"
+      << "  }\n"
+      << "}\n\n";
+}
+
+// The program's generated source: every expression term's evaluator and
+// the dispatch the eval.h hook calls.
+std::string gen_source(const mc_program* p) {
+    std::ostringstream o;
+    o << "// generated by jit.hip for one program: do not edit\n"
+      << "#include \"hmc.h\"\n#include \"nuts.h\"\n#include \"mh.h\"\n"
+      << "namespace mc {\n";
+    std::vector<int32_t> bases;
+    for (const DevTerm& T : p->terms) {
+        if (T.dist != MC_DIST_EXPR) continue;
+        if (std::find(bases.begin(), bases.end(), T.expr_base) != bases.end()) continue;
+        bases.push_back(T.expr_base);
+        gen_term(o, T, p->nodes.data() + T.expr_base);
+    }
+    o << "template <int WPC, bool VALUE_ONLY>\n"
+      << "MC_DEV void mc_jit_expr(const DevTerm& T, const DevCtx& P, const float* q, float* g,\n"
+      << "    const Group<WPC>& G, bool task, int tid, int nthr, float& lp_acc, float* vpart) {\n"
+      << "  switch (T.expr_base) {\n";
+    for (int32_t b : bases)
+        o << "    case " << b << ": jit_t" << b
+          << "<WPC, VALUE_ONLY>(T, P, q, g, G, task, tid, nthr, lp_acc, vpart); break;\n";
+    o << "    default: break;\n  }\n}\n}  // namespace mc\n";
+    return o.str();
+}
+
+const char* const kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                             "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize",
+                             "-DMC_JIT=1"};
+constexpr int kNumOpts = (int)(sizeof(kOpts) / sizeof(kOpts[0]));
+
+uint64_t cache_key(const std::string& src, const std::string& kernel) {
+    uint64_t h = 1469598103934665603ull;
+    h = fnv1a(h, src);
+    h = fnv1a(h, kernel);
+    for (int i = 0; i < kNumOpts; ++i) h = fnv1a(h, std::string(kOpts[i]));
+    for (int i = 0; i < kJitNumHeaders; ++i) {
+        h = fnv1a(h, std::string(kJitHeaderNames[i]));
+        h = fnv1a(h, std::string(kJitHeaderTexts[i]));
+    }
+    return h;
+}
+
+bool disk_load(uint64_t key, std::string& name, std::string& code) {
+    const std::string dir = cache_dir();
+    if (dir.empty()) return false;
+    char fn[64];
+    std::snprintf(fn, sizeof fn, "/%016llx.co", (unsigned long long)key);
+    std::ifstream f(dir + fn, std::ios::binary);
+    if (!f) return false;
+    uint32_t n = 0;
+    if (!f.read((char*)&n, 4) || n == 0 || n > 4096) return false;
+    name.resize(n);
+    if (!f.read(&name[0], n)) return false;
+    std::ostringstream rest;
+    rest << f.rdbuf();
+    code = rest.str();
+    return !code.empty();
+}
+
+void disk_store(uint64_t key, const std::string& name, const std::string& code) {
+    const std::string dir = cache_dir();
+    if (dir.empty()) return;
+    // (mkdir -p of the last two levels; failures leave the cache in-process)
+    const size_t cut = dir.find_last_of('/');
+    if (cut != std::string::npos && cut > 0) (void)mkdir(dir.substr(0, cut).c_str(), 0755);
+    (void)mkdir(dir.c_str(), 0755);
+    char fn[96];
+    std::snprintf(fn, sizeof fn, "/%016llx.co", (unsigned long long)key);
+    const std::string path = dir + fn;
+    const std::string tmp = path + ".tmp." + std::to_string((long long)getpid());
+    {
+        std::ofstream f(tmp, std::ios::binary);
+        if (!f) return;
+        const uint32_t n = (uint32_t)name.size();
+        f.write((const char*)&n, 4);
+        f.write(name.data(), n);
+        f.write(code.data(), (std::streamsize)code.size());
+        if (!f) {
+            (void)unlink(tmp.c_str());
+            return;
+        }
+    }
+    (void)rename(tmp.c_str(), path.c_str());
+}
+
+// Compile `kernel` (a name expression of a template instantiation) with the
+// program's source: (lowered name, code object), or an error message.
+bool compile(const std::string& src, const std::string& kernel, std::string& name,
+             std::string& code, std::string& err) {
+    const std::string full = src;  // (the name expression instantiates the kernel)
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, full.c_str(), "mc_jit.hip", kJitNumHeaders, kJitHeaderTexts,
+                            kJitHeaderNames) != HIPRTC_SUCCESS) {
+        err = "hiprtcCreateProgram failed";
+        return false;
+    }
+    const std::string expr = "&" + kernel;
+    hiprtcAddNameExpression(prog, expr.c_str());
+    const hiprtcResult r = hiprtcCompileProgram(prog, kNumOpts, kOpts);
+    if (r != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n, '\0');
+        if (n) hiprtcGetProgramLog(prog, &log[0]);
+        err = "hiprtc: " + std::string(hiprtcGetErrorString(r)) + ": " + log.substr(0, 2000);
+        hiprtcDestroyProgram(&prog);
+        return false;
+    }
+    const char* lowered = nullptr;
+    if (hiprtcGetLoweredName(prog, expr.c_str(), &lowered) != HIPRTC_SUCCESS || !lowered) {
+        err = "hiprtcGetLoweredName failed";
+        hiprtcDestroyProgram(&prog);
+        return false;
+    }
+    name = lowered;
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    code.assign(n, '\0');
+    hiprtcGetCode(prog, &code[0]);
+    hiprtcDestroyProgram(&prog);
+    return n > 0;
+}
+
+JitState* state_of(const mc_program* p) {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!p->jit) p->jit = new JitState();
+    return (JitState*)p->jit;
+}
+
+}  // namespace
+
+bool jit_enabled() {
+    if (g_expr_jit < 0) {
+        const char* e = std::getenv("MC_EXPR_JIT");
+        g_expr_jit = (e && e[0] == '0') ? 0 : 1;
+    }
+    return g_expr_jit == 1;
+}
+
+void jit_free(mc_program* p) {
+    if (!p || !p->jit) return;
+    JitState* s = (JitState*)p->jit;
+    for (hipModule_t m : s->mods) (void)hipModuleUnload(m);
+    delete s;
+    p->jit = nullptr;
+}
+
+int jit_function(const mc_program* p, const std::string& kernel, hipFunction_t* fn) {
+    *fn = nullptr;
+    if (!p->ex || !jit_enabled()) return MC_OK;
+    JitState* s = state_of(p);
+    std::lock_guard<std::mutex> lk(s->mu);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto fkey = std::make_pair(kernel, dev);
+    auto it = s->fns.find(fkey);
+    if (it != s->fns.end()) {
+        *fn = it->second;
+        return MC_OK;
+    }
+    if (!s->error.empty()) return MC_OK;  // a failed compilation: the interpreter runs
+    if (!s->have_src) {
+        s->src = gen_source(p);
+        s->have_src = true;
+    }
+    const uint64_t key = cache_key(s->src, kernel);
+    std::string name, code;
+    bool have = false;
+    {
+        std::lock_guard<std::mutex> ck(g_cache_mu);
+        auto c = g_code.find(key);
+        if (c != g_code.end()) {
+            name = c->second.first;
+            code = c->second.second;
+            have = true;
+        }
+    }
+    if (!have && disk_load(key, name, code)) have = true;
+    if (!have) {
+        std::string err;
+        if (!compile(s->src, kernel, name, code, err)) {
+            s->error = err;
+            return MC_OK;
+        }
+        disk_store(key, name, code);
+    }
+    {
+        std::lock_guard<std::mutex> ck(g_cache_mu);
+        g_code[key] = std::make_pair(name, code);
+    }
+    hipModule_t mod;
+    hipError_t e = hipModuleLoadData(&mod, code.data());
+    if (e != hipSuccess)
+        return fail(MC_ERR_HIP, "expression JIT: hipModuleLoadData failed: %s", hipGetErrorString(e));
+    s->mods.push_back(mod);
+    hipFunction_t f;
+    e = hipModuleGetFunction(&f, mod, name.c_str());
+    if (e != hipSuccess)
+        return fail(MC_ERR_HIP, "expression JIT: hipModuleGetFunction failed: %s",
+                    hipGetErrorString(e));
+    s->fns[fkey] = f;
+    *fn = f;
+    return MC_OK;
+}
+
+int jit_launch(const mc_program* p, const std::string& kernel, unsigned grid, unsigned block,
+               size_t lds, hipStream_t st, void** args, bool* used) {
+    *used = false;
+    hipFunction_t f = nullptr;
+    const int rc = jit_function(p, kernel, &f);
+    if (rc != MC_OK || f == nullptr) return rc;
+    MC_HIP_TRY(hipModuleLaunchKernel(f, grid, 1, 1, block, 1, 1, (unsigned)lds, st, args, nullptr));
+    *used = true;
+    return MC_OK;
+}
+
+std::string jit_error(const mc_program* p) {
+    if (!p->jit) return "";
+    JitState* s = (JitState*)p->jit;
+    std::lock_guard<std::mutex> lk(s->mu);
+    return s->error;
+}
+
+std::string jit_source(const mc_program* p) { return p->ex ? gen_source(p) : std::string(); }
+
+extern "C" int mc_debug_expr_jit(int on) {
+    g_expr_jit = on < 0 ? -1 : (on ? 1 : 0);
+    return MC_OK;
+}
+
+extern "C" int32_t mc_program_expr_jit(const mc_program* p) {
+    if (!p) return -1;
+    if (!p->ex || !jit_enabled()) return 0;
+    return jit_error(p).empty() ? 1 : -2;
+}
+
+// Test hooks (host only, no device): the generated source of a program's
+// expression terms, and its compilation into `kernel` (a name expression);
+// the compiler's log is the error message on failure.
+extern "C" int64_t mc_debug_expr_jit_source(const mc_program* p, char* buf, int64_t cap) {
+    if (!p) return -1;
+    const std::string s = jit_source(p);
+    if (buf && cap > 0) {
+        const size_t n = std::min<size_t>((size_t)cap - 1, s.size());
+        std::memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    return (int64_t)s.size();
+}
+
+extern "C" int mc_debug_expr_jit_compile(const mc_program* p, const char* kernel) {
+    if (!p || !kernel) return fail(MC_ERR_INVALID, "NULL argument");
+    if (!p->ex) return fail(MC_ERR_INVALID, "the program has no expression terms");
+    std::string name, code, err;
+    if (!compile(jit_source(p), kernel, name, code, err)) return fail(MC_ERR_UNSUPPORTED, "%s", err.c_str());
+    return MC_OK;
+}

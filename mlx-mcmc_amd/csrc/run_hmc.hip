@@ -1,5 +1,6 @@
 // run_hmc.hip — HMC launches (k_hmc_lf, k_hmc_lr, k_hmc_sl, k_hmc) and mc_hmc_run.
 #include "host.h"
+#include "jit.h"
 
 extern "C" int mc_workspace_release(const void* ws) {
     if (ws) ws_forget(ws);
@@ -106,6 +107,18 @@ static int launch_hmc(const mc_program* p, const mc_run_config* cfg, void* state
     A.scratch_floats = scratch_of(p);
     const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
     const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
+    if constexpr (EX) {  // the program's expression terms compiled (jit.hip)
+        DevCtx ctx = ctx_of(p);
+        mc_chain_scalars* scal = (mc_chain_scalars*)b;
+        float *sq = (float*)(b + qo), *sg = (float*)(b + go);
+        TraceDev td = trace_of(tr);
+        void* args[] = {&ctx, &A, &scal, &sq, &sg, &samples, &td, &ws};
+        bool used = false;
+        const int rc = jit_launch(p, "mc::k_hmc<" + std::to_string(WPC) + ", " +
+                                         (LDS ? "true" : "false") + ", true>",
+                                  (unsigned)grid, block_of(WPC), lds, st, args, &used);
+        if (rc != MC_OK || used) return rc;
+    }
     MC_HIP_TRY(allow_lds(k_hmc<WPC, LDS, EX>, lds));
     hipLaunchKernelGGL((k_hmc<WPC, LDS, EX>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
                        ctx_of(p), A, (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go),

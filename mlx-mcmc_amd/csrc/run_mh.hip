@@ -1,5 +1,6 @@
 // run_mh.hip — Metropolis-Hastings launches (k_mh) and mc_mh_run.
 #include "host.h"
+#include "jit.h"
 
 // ---- Metropolis-Hastings (metropolis.py:6-101) --------------------------------
 static int64_t mh_lds_floats(const mc_program* p, bool lds_arena) {
@@ -29,6 +30,18 @@ static int launch_mh(const mc_program* p, const mc_run_config* cfg, float scale,
     A.scratch_floats = scratch_of(p);
     const size_t lds = (size_t)cpb_of(WPC) * A.lds_floats * 4;
     const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
+    if constexpr (EX) {  // the program's expression terms compiled (jit.hip)
+        DevCtx ctx = ctx_of(p);
+        mc_chain_scalars* scal = (mc_chain_scalars*)b;
+        float* sq = (float*)(b + qo);
+        TraceDev td = trace_of(tr);
+        void* args[] = {&ctx, &A, &scale, &scal, &sq, &samples, &td, &ws};
+        bool used = false;
+        const int rc = jit_launch(p, "mc::k_mh<" + std::to_string(WPC) + ", " +
+                                         (LDS ? "true" : "false") + ", true>",
+                                  (unsigned)grid, block_of(WPC), lds, st, args, &used);
+        if (rc != MC_OK || used) return rc;
+    }
     MC_HIP_TRY(allow_lds(k_mh<WPC, LDS, EX>, lds));
     hipLaunchKernelGGL((k_mh<WPC, LDS, EX>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
                        ctx_of(p), A, scale, (mc_chain_scalars*)b, (float*)(b + qo), samples,

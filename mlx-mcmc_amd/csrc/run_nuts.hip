@@ -1,5 +1,6 @@
 // run_nuts.hip — NUTS launches (k_nuts_lr, k_nuts) and mc_nuts_run.
 #include "run_nuts_sl.h"
+#include "jit.h"
 
 
 // LDS floats per chain group of k_nuts: group scratch, pending words and,
@@ -44,6 +45,21 @@ static int launch_nuts(const mc_program* p, const mc_run_config* cfg, void* stat
         lds += dbytes;
     }
     const int64_t grid = (cfg->num_chains + cpb_of(WPC) - 1) / cpb_of(WPC);
+    // the program's expression terms compiled (jit.hip), with at most the
+    // default 64 KB of dynamic LDS (module kernels launch without the
+    // attribute allow_lds sets)
+    if (EX && lds <= 64 * 1024) {
+        DevCtx ctx = ctx_of(p);
+        mc_chain_scalars* scal = (mc_chain_scalars*)b;
+        float *sq = (float*)(b + qo), *sg = (float*)(b + go);
+        TraceDev td = trace_of(tr);
+        void* args[] = {&ctx, &A, &scal, &sq, &sg, &samples, &td, &ws};
+        bool used = false;
+        const int rc = jit_launch(p, "mc::k_nuts<" + std::to_string(WPC) + ", " +
+                                         (LDS ? "true" : "false") + ", true>",
+                                  (unsigned)grid, block_of(WPC), lds, st, args, &used);
+        if (rc != MC_OK || used) return rc;
+    }
     MC_HIP_TRY(allow_lds(k_nuts<WPC, LDS, EX>, lds));
     hipLaunchKernelGGL((k_nuts<WPC, LDS, EX>), dim3((unsigned)grid), dim3(block_of(WPC)), lds, st,
                        ctx_of(p), A, (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go),
