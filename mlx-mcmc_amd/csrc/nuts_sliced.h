@@ -66,6 +66,7 @@ __host__ __device__ constexpr int64_t nuts_sl_pool_floats(int rs, int maxj) {
 // (d = (x0, x1) - (th, th), s1 += d, s2 = fma(d, d, s2)), two register pairs
 // per float4 (four independent dependency chains), the LDS loads of the next
 // 16 elements issued before this round's arithmetic (lf_moments' pipeline).
+template <int PIPE = 4>
 MC_DEV void nsl_moments(const float* xv, int len, int lmin4, int lmax, float th, float& s1,
                         float& s2) {
     f2 a1[2] = {{0.f, 0.f}, {0.f, 0.f}}, a2[2] = {{0.f, 0.f}, {0.f, 0.f}};
@@ -79,28 +80,31 @@ MC_DEV void nsl_moments(const float* xv, int len, int lmin4, int lmax, float th,
         a2[1] = pk_fma(d1, d1, a2[1]);
     };
     int u4 = 0;
-    if (lmin4 >= 4) {
-        float4 A[4], B[4];
-        auto load = [&](float4 (&X)[4], int g) {
+    // (PIPE float4 groups per round: 4 with two waves per SIMD, 2 with four,
+    // where the other waves hide more of the load latency and the registers
+    // are half as many)
+    if (lmin4 >= PIPE) {
+        float4 A[PIPE], B[PIPE];
+        auto load = [&](float4 (&X)[PIPE], int g) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) X[q] = *(const float4*)(xv + (g + q) * 256);
+            for (int q = 0; q < PIPE; ++q) X[q] = *(const float4*)(xv + (g + q) * 256);
         };
-        auto round = [&](const float4 (&X)[4]) {
+        auto round = [&](const float4 (&X)[PIPE]) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) quad(X[q]);
+            for (int q = 0; q < PIPE; ++q) quad(X[q]);
         };
-        const int last = lmin4 - 4;
+        const int last = lmin4 - PIPE;
         load(A, 0);
         for (;;) {
-            const bool more_b = u4 + 8 <= lmin4;
-            load(B, min(u4 + 4, last));
+            const bool more_b = u4 + 2 * PIPE <= lmin4;
+            load(B, min(u4 + PIPE, last));
             round(A);
-            u4 += 4;
+            u4 += PIPE;
             if (!more_b) break;
-            const bool more_a = u4 + 8 <= lmin4;
-            load(A, min(u4 + 4, last));
+            const bool more_a = u4 + 2 * PIPE <= lmin4;
+            load(A, min(u4 + PIPE, last));
             round(B);
-            u4 += 4;
+            u4 += PIPE;
             if (!more_a) break;
         }
     }
@@ -242,8 +246,11 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
     xid = xon ? xid : 0.0f;
     const LrOwn own = lr_own_prior(P.n_sterms, sst, xon ? 2 * xo : 64, Dsh);
     const bool own_lp = own.on && slice == 0;
-    const float o_m = vpin(own.m), o_cinv2 = vpin(own.cinv2), o_c0l = vpin(own.c0l),
-                o_wn = vpin(own.wn);
+    // (uniform constants pinned in VGPRs with two waves per SIMD — a spilled
+    // SGPR costs a readlane per use; with four the VGPRs are the scarcer)
+    auto pin = [](float x) { return OCC <= 2 ? vpin(x) : x; };
+    const float o_m = pin(own.m), o_cinv2 = pin(own.cinv2), o_c0l = pin(own.c0l),
+                o_wn = pin(own.wn);
 
     int gk[RS];
     const float* xv[RS];
@@ -269,35 +276,30 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
         pdir[r] = DIR && r < tt[nsweep].nslot &&
                   ((const int32_t*)sd)[tt[nsweep].len_off + r * 64 + j] > 0;
     }
-    const float sw_w = vpin(F.sw_w), sw_c0 = vpin(F.sw_c0), sw_cinv = vpin(F.sw_cinv),
-                sw_cinv2 = vpin(F.sw_cinv2), sw_clogs = vpin(F.sw_clogs);
-    const float d_w = vpin(F.d_w), d_c0 = vpin(F.d_c0), d_m = vpin(F.d_m), d_cinv = vpin(F.d_cinv),
-                d_cinv2 = vpin(F.d_cinv2), d_clogs = vpin(F.d_clogs);
+    const float sw_w = pin(F.sw_w), sw_c0 = pin(F.sw_c0), sw_cinv = pin(F.sw_cinv),
+                sw_cinv2 = pin(F.sw_cinv2), sw_clogs = pin(F.sw_clogs);
+    const float d_w = pin(F.d_w), d_c0 = pin(F.d_c0), d_m = pin(F.d_m), d_cinv = pin(F.d_cinv),
+                d_cinv2 = pin(F.d_cinv2), d_clogs = pin(F.d_clogs);
     const float lp_const = P.lp_const;
 
-    // the current sample (theta0 of the next iteration)
-    float Cq[RS], Cg[RS];
-#pragma unroll
-    for (int r = 0; r < RS; ++r) {
-        Cq[r] = gk[r] >= 0 ? st_q[c * D + gk[r]] : 0.0f;
-        Cg[r] = gk[r] >= 0 ? st_g[c * D + gk[r]] : 0.0f;
-    }
+    // the current sample (theta0 of the next iteration): its private part
+    // stays in the chain state (st_q / st_g: only this lane reads or writes
+    // these entries — the top-level accept copies the candidate there), the
+    // shared part in the holder lanes (every slice needs it)
     float Cqs = xon ? st_q[c * D + xg] : 1.0f, Cgs = xon ? st_g[c * D + xg] : 0.0f;
 
     // exchange lines: one record of kNslLine granules per (wave, slice, parity)
-    unsigned long long* gline[2];
-#pragma unroll
-    for (int par = 0; par < 2; ++par)
-        gline[par] = xch + (((int64_t)par * n_groups + grp) * NW + wave) * S * kNslLine;
+    // (line of parity par: + par * pstride granules; an array of the two
+    // pointers indexed by the parity went to scratch)
+    unsigned long long* const gline0 = xch + ((int64_t)grp * NW + wave) * S * kNslLine;
+    const int64_t pstride = (int64_t)n_groups * NW * S * kNslLine;
     // poll lanes: CW-lane column groups, lane (row, col) reads pair
     // (64 / CW) pass + row of slice col
     const int CW = S > 8 ? 16 : 8;
     const int IP = 64 / CW;
     const int prow = j / CW, pcol = j % CW;
     const bool poll_lane = pcol < S;
-    unsigned long long* gp[2];
-#pragma unroll
-    for (int par = 0; par < 2; ++par) gp[par] = gline[par] + min(pcol, S - 1) * kNslLine + prow;
+    unsigned long long* const gp0 = gline0 + min(pcol, S - 1) * kNslLine + prow;
     // publishing (lf_rs8's reduce-scatter): lane 16 r + x (x < 2 NG) holds
     // pair 8 (x / 2) + 4 (x % 2) + perm[r] in xr[x]
     const int row16 = j >> 4, col16 = j & 15;
@@ -344,8 +346,10 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             const float z = gk[r] >= 0 ? normal_of(gk[r]) : 0.0f;
-            Mq[r] = Pq[r] = Cq[r];
-            Mg[r] = Pg[r] = Cg[r];
+            const float cq = gk[r] >= 0 ? st_q[c * D + gk[r]] : 0.0f;
+            const float cg = gk[r] >= 0 ? st_g[c * D + gk[r]] : 0.0f;
+            Mq[r] = Pq[r] = cq;
+            Mg[r] = Pg[r] = cg;
             Mp[r] = Pp[r] = z;
             if (lead) k0p += z * z;
         }
@@ -389,7 +393,7 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
             const int v = (mc_u01_f32(rd.x) < 0.5f) ? 1 : -1;
             const double ve = (double)v * eps;
             const float h = (float)(0.5 * ve), e = (float)ve;
-            const float xh = vpin(h), xe = vpin(e);
+            const float xh = pin(h), xe = pin(e);
 #pragma unroll
             for (int r = 0; r < RS; ++r) {
                 q[r] = v > 0 ? Pq[r] : Mq[r];
@@ -438,7 +442,7 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
 #pragma unroll
                     for (int r = 0; r < RS; ++r) {
                         M1[r] = M2[r] = 0.0f;
-                        if (len[r] > 0) nsl_moments(xv[r], len[r], lmin4[r], lmax[r], q[r], M1[r], M2[r]);
+                        if (len[r] > 0) nsl_moments<OCC >= 4 ? 2 : 4>(xv[r], len[r], lmin4[r], lmax[r], q[r], M1[r], M2[r]);
                     }
                 }
                 MC_STAMP(0);
@@ -591,7 +595,7 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                     float pv = xr[0];
 #pragma unroll
                     for (int x = 1; x < 8; ++x) pv = (x == col16) ? xr[x] : pv;
-                    granule_store(gline[par] + slice * kNslLine + pub_pair, epoch, pv);
+                    granule_store(gline0 + par * pstride + slice * kNslLine + pub_pair, epoch, pv);
                 }
                 // park the leaf's private part: candidate pool (q, g) and, when
                 // it opens a subtree, that subtree's first leaf (q, r)
@@ -633,41 +637,55 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                             sq_[r] = bq + ee * sp_[r];
                             M1[r] = M2[r] = 0.0f;
                             if (len[r] > 0)
-                                nsl_moments(xv[r], len[r], lmin4[r], lmax[r], sq_[r], M1[r], M2[r]);
+                                nsl_moments<OCC >= 4 ? 2 : 4>(xv[r], len[r], lmin4[r], lmax[r], sq_[r],
+                                                              M1[r], M2[r]);
                         }
                         spec = true;
                     }
                 }
                 MC_STAMP(8);
                 // ---- poll: every slice's record of this leaf --------------------
+                // (in chunks of 4 passes, one round trip each: 2 groups with
+                // 16 slices, 4 with 8 — the records of leaves with up to 4
+                // merges; the registers of 8 passes spilled at 4 waves per SIMD)
                 const int npass = (8 * NG) / IP;
-                unsigned long long y[8];
-                auto poll_issue = [&]() {
+                unsigned long long* const gpp = gp0 + par * pstride;
+                float tot[8];
 #pragma unroll
-                    for (int ps = 0; ps < 8; ++ps)
-                        y[ps] = ps < npass ? granule_load(gp[par] + IP * ps) : 0ull;
-                };
-                float vals[8];
-                auto poll_eval = [&]() {
-                    bool ready = true;
+                for (int ch = 0; ch < 2; ++ch) {
+                    if (4 * ch >= npass) {
 #pragma unroll
-                    for (int ps = 0; ps < 8; ++ps) {
-                        const bool nd = poll_lane && ps < npass;
-                        vals[ps] = nd ? __uint_as_float((uint32_t)y[ps]) : 0.0f;
-                        ready = ready & (!nd | ((uint32_t)(y[ps] >> 32) == epoch));
+                        for (int ps = 0; ps < 4; ++ps) tot[4 * ch + ps] = 0.0f;
+                        continue;
                     }
-                    return ready;
-                };
-                poll_issue();
-                bool ready = poll_eval();
-                uint32_t spins = 0;
-                while (__ballot(!ready)) {
-                    if (++spins > kSpinLimit) {
-                        ok = false;
-                        break;
-                    }
+                    unsigned long long y[4];
+                    auto poll_issue = [&]() {
+#pragma unroll
+                        for (int ps = 0; ps < 4; ++ps)
+                            y[ps] = 4 * ch + ps < npass ? granule_load(gpp + IP * (4 * ch + ps)) : 0ull;
+                    };
+                    auto poll_eval = [&]() {
+                        bool ready = true;
+#pragma unroll
+                        for (int ps = 0; ps < 4; ++ps) {
+                            const bool nd = poll_lane && 4 * ch + ps < npass;
+                            tot[4 * ch + ps] = nd ? __uint_as_float((uint32_t)y[ps]) : 0.0f;
+                            ready = ready & (!nd | ((uint32_t)(y[ps] >> 32) == epoch));
+                        }
+                        return ready;
+                    };
                     poll_issue();
-                    ready = poll_eval();
+                    bool ready = poll_eval();
+                    uint32_t spins = 0;
+                    while (__ballot(!ready)) {
+                        if (++spins > kSpinLimit) {
+                            ok = false;
+                            break;
+                        }
+                        poll_issue();
+                        ready = poll_eval();
+                    }
+                    if (!ok) break;
                 }
                 __builtin_amdgcn_s_setprio(0);
                 if (!ok) {
@@ -676,15 +694,19 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                 }
                 MC_STAMP(3);
                 // slice sums: a fixed CW-lane DPP tree per pass
-                float tot[8];
 #pragma unroll
-                for (int ps = 0; ps < 8; ++ps) tot[ps] = ps < npass ? nsl_colsum(vals[ps], CW) : 0.0f;
-                auto item = [&](int Pi) {
-                    float t = tot[0];
+                for (int ps = 0; ps < 8; ++ps) tot[ps] = ps < npass ? nsl_colsum(tot[ps], CW) : 0.0f;
+                // the record's totals into one register, lane P holding item P
+                // (an item read by a run-time index then is one readlane; a
+                // select over the pass registers became a scratch array)
+                float rec = 0.0f;
 #pragma unroll
-                    for (int ps = 1; ps < 8; ++ps) t = (Pi / IP == ps) ? tot[ps] : t;
-                    return rl(t, item_lane(Pi));
-                };
+                for (int ps = 0; ps < 8; ++ps) {
+                    if (ps >= npass) break;
+                    const float v = __shfl(tot[ps], item_lane(j));
+                    rec = (j / IP == ps) ? v : rec;
+                }
+                auto item = [&](int Pi) { return rl(rec, Pi); };
                 const float lpl = item(0) + lp_const;
                 // the shared parameters' gradient (cotangent total + own prior,
                 // through the transform's VJP) and second half kick
@@ -731,8 +753,13 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                 const int n_leaf = (logu <= (double)(-Hl)) ? 1 : 0;
                 const bool s_leaf = logu < (double)(1000.0f - Hl);
                 {
-                    const double a = (double)mc_expf_ref(-Hl + H0);
-                    alpha_sum += (a < 1.0) ? a : 1.0;
+                    // alpha = min(1, f32 exp(H0 - H')) (nuts.py:173; NaN -> 1, Q8) with
+                    // ocml's f32 exp (<= 1 ulp from the correctly rounded value
+                    // mc_expf_ref gives; the oracle replay's alpha bar is the
+                    // tie bound's relative error, >> 1 ulp) — a double exp per
+                    // leaf held ~20 VGPRs of f64 coefficients and spilled them
+                    const float a = expf(-Hl + H0);
+                    alpha_sum += (double)((a < 1.0f) ? a : 1.0f);
                 }
                 n_alpha += 1;
                 if (!s_leaf) divergent += 1;
@@ -847,8 +874,11 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                 if ((double)mc_u01_f32(rd.y) * den < (double)cn) {
 #pragma unroll
                     for (int r = 0; r < RS; ++r) {
-                        Cq[r] = *pool_at(cand, 0, r);
-                        Cg[r] = *pool_at(cand, 1, r);
+                        const float cq = *pool_at(cand, 0, r), cg = *pool_at(cand, 1, r);
+                        if (gk[r] >= 0 && lead) {
+                            st_q[c * D + gk[r]] = cq;
+                            st_g[c * D + gk[r]] = cg;
+                        }
                     }
                     if (xon) {
                         const int pr = 2 * MAXJ + 2 * cand;
@@ -892,7 +922,7 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                 float* out = samples + (c * cfg.sample_capacity + si) * (int64_t)D;
 #pragma unroll
                 for (int r = 0; r < RS; ++r)
-                    if (gk[r] >= 0 && lead) out[gk[r]] = Cq[r];
+                    if (gk[r] >= 0 && lead) out[gk[r]] = st_q[c * D + gk[r]];
                 if (slice == 0 && xon) out[xg] = Cqs;
             }
         }
@@ -911,15 +941,10 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
         MC_STAMP(15);
     }
     MC_STAMP_FLUSH
-    if (!ok) return;  // a timed-out chain keeps its state (mc_workspace_status reports it)
+    // a timed-out chain keeps its scalars and shared parameters (its private
+    // parameters hold the last accepted draw; mc_workspace_status reports it)
+    if (!ok) return;
 
-#pragma unroll
-    for (int r = 0; r < RS; ++r) {
-        if (gk[r] >= 0 && lead) {
-            st_q[c * D + gk[r]] = Cq[r];
-            st_g[c * D + gk[r]] = Cg[r];
-        }
-    }
     if (slice == 0 && xon) {
         st_q[c * D + xg] = Cqs;
         st_g[c * D + xg] = Cgs;

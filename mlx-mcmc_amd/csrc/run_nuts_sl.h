@@ -26,7 +26,7 @@ inline int nuts_sl_occ(const mc_program* p) {
         const int v = std::atoi(e);
         if (v == 2 || v == 4) return v;
     }
-    return 2;  // (4: the kernel spills at 128 VGPRs; measured slower)
+    return 2;
 }
 
 // exchange lines (both parities) for every chain block of C chains

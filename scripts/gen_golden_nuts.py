@@ -11,7 +11,7 @@ test infrastructure, run here on the CPU and committed.
       1, 2, seed 0, a fixed step size 2e-3 (adapt_step_size=False), W = 2,
       S = 10, max_tree_depth 10 (depths 7-8).
   tests/golden/nuts_large_da_trace.npz
-      The same model and chains 0, 1 with dual averaging acting: eps0 = 2e-3,
+      The same model and chains 0, 1 with dual averaging acting: eps0 = 2e-4,
       W = 20, S = 5 (the sliced NUTS kernel's adaptation check).
   tests/golden/nuts_hier_trace.npz
       The small hierarchical model (workloads.hierarchical, G = 7, N = 1 K:
@@ -48,8 +48,12 @@ RUNS = {
                                           max_tree_depth=10, target_accept=0.65,
                                           adapt_step_size=False)),
     # the same model with the reference's dual averaging acting (VERDICT r4
-    # "Next round" 1): W = 20 warmup iterations from eps0 = 2e-3, S = 5
-    "large_da": dict(chains=(0, 1), cfg=dict(num_warmup=20, num_samples=5, step_size=2e-3,
+    # "Next round" 1): W = 20 warmup iterations from eps0 = 2e-4, S = 5 (the
+    # first update moves eps to 10 eps0 e^(...) ~ 4e-3 and it settles near
+    # 1e-3; from eps0 = 2e-3 it jumps to 0.034, where a leapfrog step
+    # amplifies fp32 rounding differences ~300-fold and any two
+    # implementations separate within two iterations)
+    "large_da": dict(chains=(0, 1), cfg=dict(num_warmup=20, num_samples=5, step_size=2e-4,
                                              max_tree_depth=10, target_accept=0.65)),
 }
 SEED = 0

@@ -64,7 +64,7 @@ def test_sliced_medium_against_oracle(gpu, slices):
                target_accept=0.65, seed=3)
     depths = []
     for chain in (0, 5):
-        same, d = _replay("medium", {"config": cfg}, info, 0, chain)
+        same, d, _ = _replay("medium", {"config": cfg}, info, 0, chain)
         depths.extend(d.tolist())
     assert max(depths) >= 3, "real trees"
 
