@@ -108,7 +108,9 @@ def parse():
     ap.add_argument("--nuts-step-size", type=float, default=None,
                     help="NUTS initial step size (dual averaging adapts it over the warmup; "
                          "default 0.1 illcond, 2e-3 hier)")
-    ap.add_argument("--workload", default="hmc", choices=["hmc", "nuts"],
+    ap.add_argument("--mh-scale", type=float, default=1e-3,
+                    help="--workload mh: the random-walk proposal scale")
+    ap.add_argument("--workload", default="hmc", choices=["hmc", "nuts", "mh"],
                     help="hmc: the headline (BASELINE configs[2]/[3]); nuts: BASELINE "
                          "configs[4] (NUTS depth 10 + dual averaging, 100-dim kappa = 1000 "
                          "Gaussian, 64 chains per GPU; a measurement line, not the headline)")
@@ -637,10 +639,134 @@ def main_nuts(args):
         dist.destroy_process_group()
 
 
+def mh_cpu_baseline(budget_s, args, scale):
+    """The oracle's MH (metropolis.py restated: one log density per
+    iteration, torch CPU) on the same model, one chain, one thread."""
+    import torch
+
+    import workloads as W
+    from oracle import samplers as S
+
+    torch.set_num_threads(1)
+    G, N = W.SHAPES[args.shape]
+    lp, init = W.hierarchical(W.ns_oracle(), G, N)
+    iters, t0, runs = 0, time.perf_counter(), 0
+    while time.perf_counter() - t0 < budget_s:
+        S.metropolis_hastings(lp, init, num_samples=20, proposal_scale=scale, random_seed=runs,
+                              record=False)
+        iters += 20
+        runs += 1
+    dt = time.perf_counter() - t0
+    return {"value": iters / dt, "unit": "chain-iterations/s", "cores": 1, "kind": "port",
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": (f"oracle/samplers.py metropolis_hastings (torch-CPU log density), 1 chain, "
+                       f"1 thread: {runs} runs of 20 iterations on the same hierarchical "
+                       f"'{args.shape}' model, {iters} iterations in {dt:.1f} s")}
+
+
+def main_mh(args):
+    """Random-walk Metropolis-Hastings (metropolis.py:6-101, the MCMC.run
+    default) on the hierarchical model of --shape: value = chain-iterations
+    (proposals evaluated) of all chains per second over the timed launches;
+    a measurement line for the sliced MH kernel (k_mh_sl), not the headline."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    _ensure_pkg()
+    import workloads as W
+    from mlx_mcmc_amd import _engine, _lib, _trace
+    from mlx_mcmc_amd.distributed import max_over_ranks, shard, sum_over_ranks
+
+    world, rank, local, dev = init_ranks()
+    C, K, Wm, B = args.chains, args.steps, args.warmup, max(1, args.iters_per_launch)
+    G, N = W.SHAPES[args.shape]
+    lp_fn, init = W.hierarchical(W.ns_product(), G, N)
+    prog = _trace.compile_model(lp_fn, init, slices=args.slices)
+    D = prog.D
+    scale = args.mh_scale
+    chains = _engine.ChainSet(prog, C, prog.layout.flatten(init), scale, device=dev)
+    samples = torch.empty((C, max(K, 1), D), dtype=torch.float32, device=dev)
+    chain_offset, _ = shard(C * world, world, rank)
+    cfg = dict(chain_offset=chain_offset, num_warmup=Wm, num_samples=K, sample_begin=0,
+               sample_capacity=K, seed=args.seed)
+
+    def launches(first, count):
+        return [(first + i, min(B, count - i)) for i in range(0, count, B)]
+
+    clock_warm(args.clock_warm_ms, dev)
+    for it0, n in launches(0, Wm):
+        chains.run_mh(proposal_scale=scale, samples=samples, iter_begin=it0, iter_count=n, **cfg)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    timed = launches(Wm, K)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in timed]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for (it0, n), (e0, e1) in zip(timed, ev):
+        e0.record(stream)
+        chains.run_mh(proposal_scale=scale, samples=samples, iter_begin=it0, iter_count=n, **cfg)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    check(chains, "MH timed region")
+    sc = chains.scalars()
+    full = [a.elapsed_time(b) for (a, b), (_, n) in zip(ev, timed) if n == B] or \
+           [a.elapsed_time(b) for (a, b), _ in zip(ev, timed)]
+    launch_ms = float(np.mean(full)) if K else float("nan")
+    iters_per_launch = min(B, K)
+    elapsed = max_over_ranks(elapsed, device=dev)
+    total = sum_over_ranks(float(C * K), device=dev)
+    if rank == 0:
+        value = total / elapsed
+        # F = 3N + 10D flops per chain-iteration: the swept term's sum of
+        # squares (d = x - theta, fma: 3 per element), the proposal (2 per
+        # parameter), the direct term (~8 per parameter)
+        flops = 3 * N + 10 * D
+        achieved = C * iters_per_launch * flops / (launch_ms * 1e-3) / 1e12
+        kern = ("k_mh_sl (sliced lane-resident MH, one chain per wave, "
+                f"{prog.num_slices} slices)" if _lib.load().mc_program_mh_sliced(prog.handle) == 1
+                else f"k_mh<{prog.waves_per_chain}>")
+        out = {
+            "metric": f"MH chain-iterations/sec (all chains), hierarchical '{args.shape}' D={D}, N={N}",
+            "value": value, "unit": "chain-iterations/s", "n_gpus": world, "steps": K,
+            "warmup": Wm, "ms_per_step": elapsed * 1e3 / max(K, 1), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (fixed-seed hierarchical Normal data, SURVEY §8d)",
+            "config": {"workload": (f"random-walk MH (metropolis.py) on the hierarchical "
+                                    f"'{args.shape}' model, proposal scale {scale}, {C} chains "
+                                    f"per GPU"),
+                       "num_params": D, "num_obs": N, "chains_per_gpu": C,
+                       "total_chains": C * world, "parallelism": f"chains sharded {C}/GPU"},
+            "roofline": {"bound": "valu_fp32", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
+                         "kernel": kern, "launch_ms": launch_ms,
+                         "iters_per_launch": iters_per_launch, "flops_per_iteration": flops},
+            "accept_rate": float(np.mean(sc["n_accept"] / np.maximum(sc["n_total"], 1))),
+            "clock_warm_ms": args.clock_warm_ms,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb = mh_cpu_baseline(min(args.cpu_seconds, 15.0), args, scale)
+            cb["gpu_over_cpu"] = value / cb["value"]
+            out["cpu_baseline"] = cb
+        print(json.dumps(out), flush=True)
+    del chains, prog, samples
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.workload == "nuts":
         return main_nuts(args)
+    if args.workload == "mh":
+        return main_mh(args)
     import numpy as np
     import torch
     import torch.distributed as dist

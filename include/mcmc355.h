@@ -412,6 +412,14 @@ int mc_debug_nuts_variant(int variant);
  * -1 restores the default (MC_NUTS_SLICED from the environment, else on).
  * Trees agree up to fp32 summation order.                                  */
 int mc_debug_nuts_sliced(int on);
+/* The sliced Metropolis-Hastings kernel k_mh_sl (csrc/mh_sliced.h):
+ * mc_program_mh_sliced is 1 when mc_mh_run runs it (a program sliced onto
+ * the fast-form lane layout: one wave per chain and slice, one log-p record
+ * exchange per iteration), 0 when it runs k_mh on the tape, -1 on a null
+ * program; mc_debug_mh_sliced: 0 forces k_mh, 1 allows k_mh_sl, -1 the
+ * default (MC_MH_SLICED from the environment, else on).                    */
+int32_t mc_program_mh_sliced(const mc_program* prog);
+int mc_debug_mh_sliced(int on);
 /* Expression terms (MC_DIST_EXPR) compiled per program (csrc/jit.hip):
  * hiprtc compiles the tape kernels' expression instantiations with each
  * term's node DAG as straight-line code (the interpreter's operations in its

@@ -215,6 +215,8 @@ SIGNATURES = [
     ("mc_debug_lanes_fast", ctypes.c_int, [ctypes.c_int]),
     ("mc_debug_nuts_variant", ctypes.c_int, [ctypes.c_int]),
     ("mc_debug_nuts_sliced", ctypes.c_int, [ctypes.c_int]),
+    ("mc_debug_mh_sliced", ctypes.c_int, [ctypes.c_int]),
+    ("mc_program_mh_sliced", ctypes.c_int32, [_VP]),
     ("mc_debug_expr_jit", ctypes.c_int, [ctypes.c_int]),
     ("mc_program_expr_jit", ctypes.c_int32, [_VP]),
     ("mc_debug_program_host_only", ctypes.c_int, [ctypes.c_int]),

@@ -148,9 +148,9 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
     static_assert(NSH <= kLrMaxShared, "shared parameters");
     constexpr bool CF = FORM >= 0;
     static_assert(!CF || lf_nroles(FORM) == NSH, "record slots of a compile-time form");
-    // record positions: group 0 = lp, K, the NSH cotangents, the top-level
-    // dots (a, b); K0 in group 0's last pair when NSH <= 3, else group 1's
-    // first; group g >= 1: the dots of merge levels 4 (g - 1) .. + 3
+    // record positions: group 0 = lp, K, the NSH cotangents, dot slot 0 (a,
+    // b); K0 in group 0's last pair when NSH <= 3, else group 1's first; group
+    // g >= 1: dot slots 4 (g - 1) + 1 .. + 4 (the dots lambda below)
     constexpr int IT_TOPA = 2 + NSH, IT_TOPB = 3 + NSH;
     constexpr int IT_K0 = NSH <= 3 ? 7 : 8;
     if (A.fault && blockIdx.x == gridDim.x - 1) return;  // test hook: never publishes
@@ -434,10 +434,14 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                     sh.p = sh.p + xh * sh.g;
                     sh.q = sh.q + xe * sh.p;
                 }
+                // the shared scales' reciprocals and logs from the hardware
+                // v_rcp_f32 / v_log_f32 (<= 1 ulp; the same bits in every
+                // slice), as k_hmc_lf: the IEEE division and ocml logf were a
+                // dependent chain of ~40 instructions on the leaf's critical path
                 sh.v = hxf ? xf_apply(xxf, sh.q) : sh.q;
-                sh.is = 1.0f / sh.v;
+                sh.is = __builtin_amdgcn_rcpf(sh.v);
                 sh.iv = sh.is * sh.is;
-                sh.lg = logf(sh.v);
+                sh.lg = __builtin_amdgcn_logf(sh.v) * 0.693147180559945f;
                 if (!spec) {
 #pragma unroll
                     for (int r = 0; r < RS; ++r) {
@@ -517,8 +521,42 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                 const bool last = k == nleaf - 1;
                 const int m = last ? jd : ctz_u32((uint32_t)(k + 1));
                 // ---- the record: wave totals, reduce-scattered ----------------
-                const int ngd = (m + 3) >> 2;  // dot groups
-                const int NG = max(1 + ngd, (NSH > 3 && first_leaf) ? 2 : 1);
+                // dot slots: the top-level pair first when the leaf completes
+                // its subtree, then one pair per merge level; slot 0 sits in
+                // group 0 (IT_TOPA / IT_TOPB), slot d >= 1 in group 1 + (d-1)/4
+                // — three leaves in four then need one group
+                const int nd = m + (last ? 1 : 0);
+                const int NG = max(1 + (nd + 2) / 4, (NSH > 3 && first_leaf) ? 2 : 1);
+                // U-turn dot partials of dot slot d (private parameters): the
+                // top level (nuts.py:276, d = q+ - q- against r- and r+) or
+                // merge level l (nuts.py:214, the level-(l+1) subtree's first
+                // leaf against this end)
+                auto dots = [&](int d, float& a, float& b) {
+                    a = b = 0.0f;
+                    if (d >= nd) return;
+                    const int l = d - (last ? 1 : 0);
+                    if (l < 0) {
+#pragma unroll
+                        for (int r = 0; r < RS; ++r) {
+                            if (!lead) continue;
+                            const float oq = v > 0 ? Mq[r] : Pq[r], op = v > 0 ? Mp[r] : Pp[r];
+                            const float dd = v > 0 ? q[r] - oq : oq - q[r];
+                            a += dd * (v > 0 ? op : p[r]);
+                            b += dd * (v > 0 ? p[r] : op);
+                        }
+                        return;
+                    }
+                    const int k0 = k + 1 - (2 << l);
+                    const int slot = (k0 == 0) ? jd : ctz_u32((uint32_t)k0);
+#pragma unroll
+                    for (int r = 0; r < RS; ++r) {
+                        const float bq = *first_at(slot, 0, r), br = *first_at(slot, 1, r);
+                        if (!lead) continue;
+                        const float dd = v > 0 ? q[r] - bq : bq - q[r];
+                        a += dd * (v > 0 ? br : p[r]);
+                        b += dd * (v > 0 ? p[r] : br);
+                    }
+                };
                 float xr[8];
 #pragma unroll
                 for (int x = 0; x < 8; ++x) xr[x] = 0.0f;
@@ -538,20 +576,7 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                             vv[2 + kk] = ((F.sw_ks == kk ? cs : 0.0f) + (F.d_km == kk ? cm : 0.0f)) +
                                          (F.d_ks == kk ? cd : 0.0f);
                     }
-                    if (last) {
-                        // top level (nuts.py:276): d = q+ - q-, against r- and r+
-                        float a = 0.0f, b = 0.0f;
-#pragma unroll
-                        for (int r = 0; r < RS; ++r) {
-                            if (!lead) continue;
-                            const float oq = v > 0 ? Mq[r] : Pq[r], op = v > 0 ? Mp[r] : Pp[r];
-                            const float d = v > 0 ? q[r] - oq : oq - q[r];
-                            a += d * (v > 0 ? op : p[r]);
-                            b += d * (v > 0 ? p[r] : op);
-                        }
-                        vv[IT_TOPA] = a;
-                        vv[IT_TOPB] = b;
-                    }
+                    dots(0, vv[IT_TOPA], vv[IT_TOPB]);
                     if (IT_K0 < 8 && first_leaf) vv[IT_K0 & 7] = k0p;
                     lf_rs8(vv, xx);
                     xr[0] = xx[0];
@@ -562,26 +587,7 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                     if (gd >= NG) break;
                     float vv[8], xx[2];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        // merge level l: the level-(l+1) subtree's first leaf
-                        // (nuts.py:214: no_u_turn over the merged subtree)
-                        const int l = 4 * (gd - 1) + i;
-                        float a = 0.0f, b = 0.0f;
-                        if (l < m) {
-                            const int k0 = k + 1 - (2 << l);
-                            const int slot = (k0 == 0) ? jd : ctz_u32((uint32_t)k0);
-#pragma unroll
-                            for (int r = 0; r < RS; ++r) {
-                                const float bq = *first_at(slot, 0, r), br = *first_at(slot, 1, r);
-                                if (!lead) continue;
-                                const float d = v > 0 ? q[r] - bq : bq - q[r];
-                                a += d * (v > 0 ? br : p[r]);
-                                b += d * (v > 0 ? p[r] : br);
-                            }
-                        }
-                        vv[2 * i] = a;
-                        vv[2 * i + 1] = b;
-                    }
+                    for (int i = 0; i < 4; ++i) dots(4 * (gd - 1) + i + 1, vv[2 * i], vv[2 * i + 1]);
                     if (IT_K0 >= 8 && gd == 1 && first_leaf) vv[0] = k0p;
                     lf_rs8(vv, xx);
                     xr[2 * gd] = xx[0];
@@ -650,6 +656,7 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                 // merges; the registers of 8 passes spilled at 4 waves per SIMD)
                 const int npass = (8 * NG) / IP;
                 unsigned long long* const gpp = gp0 + par * pstride;
+                float mdraw = 0.0f;
                 float tot[8];
 #pragma unroll
                 for (int ch = 0; ch < 2; ++ch) {
@@ -675,6 +682,18 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                         return ready;
                     };
                     poll_issue();
+                    if (ch == 0) {
+                        // while the records travel: the uniforms of this leaf's
+                        // merges (TAG_MERGE / jd, level << 20 | k; lane l holds
+                        // level l's), scalar Philox off the critical path
+                        for (int l = 0; l < m; ++l) {
+                            const mc_u32x4 rm = mc_draw(cfg.seed, chain_id, (uint32_t)it,
+                                                        MC_RNG_TAG_MERGE, (uint32_t)jd,
+                                                        ((uint32_t)l << 20) | (uint32_t)k);
+                            const float u = mc_u01_f32(rm.x);
+                            mdraw = (j == l) ? u : mdraw;
+                        }
+                    }
                     bool ready = poll_eval();
                     uint32_t spins = 0;
                     while (__ballot(!ready)) {
@@ -786,12 +805,9 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                 for (int l = 0; l < m; ++l) {
                     const int pidx = __builtin_amdgcn_readlane(pend_idx, l);
                     const int pn = __builtin_amdgcn_readlane(pend_n, l);
-                    const mc_u32x4 rm = mc_draw(cfg.seed, chain_id, (uint32_t)it,
-                                                MC_RNG_TAG_MERGE, (uint32_t)jd,
-                                                ((uint32_t)l << 20) | (uint32_t)k);
                     const double den = (double)(pn + cn) > 1.0 ? (double)(pn + cn) : 1.0;
                     // U < cn / den as U * den < cn (exact, nuts.h)
-                    const bool take_second = (double)mc_u01_f32(rm.x) * den < (double)cn;
+                    const bool take_second = (double)rl(mdraw, l) * den < (double)cn;
                     if (take_second) {
                         freemask |= (1u << pidx);
                     } else {
@@ -815,8 +831,10 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                         ash += rl(as, kk);
                         bsh += rl(bs, kk);
                     }
-                    const int ia = 8 + 2 * l;
-                    const float da = item(ia) + ash, db = item(ia + 1) + bsh;
+                    const int dsl = l + (last ? 1 : 0);  // its dot slot
+                    const int ia = dsl == 0 ? IT_TOPA : 8 + 2 * (dsl - 1);
+                    const int ib = dsl == 0 ? IT_TOPB : ia + 1;
+                    const float da = item(ia) + ash, db = item(ib) + bsh;
                     if (!(da >= 0.0f && db >= 0.0f)) {
                         s_sub = false;
                         break;

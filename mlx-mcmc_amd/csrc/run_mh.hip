@@ -1,6 +1,7 @@
 // run_mh.hip — Metropolis-Hastings launches (k_mh) and mc_mh_run.
 #include "host.h"
 #include "jit.h"
+#include "run_mh_sl.h"
 
 // ---- Metropolis-Hastings (metropolis.py:6-101) --------------------------------
 static int64_t mh_lds_floats(const mc_program* p, bool lds_arena) {
@@ -10,8 +11,19 @@ static bool mh_use_lds(const mc_program* p) {
     return cpb_of(p->wpc) * mh_lds_floats(p, true) * 4 <= kLdsArenaBudget;
 }
 
+extern "C" int mc_debug_mh_sliced(int on) {
+    g_mh_sliced = on < 0 ? -1 : (on ? 1 : 0);
+    return MC_OK;
+}
+
+extern "C" int32_t mc_program_mh_sliced(const mc_program* p) {
+    if (!p) return -1;
+    return use_mh_sliced(p) ? 1 : 0;
+}
+
 extern "C" int64_t mc_mh_workspace_bytes(const mc_program* p, int64_t C) {
     if (!p || C < 0) return -1;
+    if (use_mh_sliced(p)) return mh_sl_workspace_bytes(p, C);
     if (mh_use_lds(p)) return 0;
     return C * 2 * (int64_t)dpad_of(p->D) * 4;
 }
@@ -57,6 +69,14 @@ extern "C" int mc_mh_run(const mc_program* p, const mc_run_config* cfg, double p
     if (rc) return rc;
     if (!std::isfinite(proposal_scale)) return fail(MC_ERR_INVALID, "proposal_scale not finite");
     if (cfg->num_chains == 0 || cfg->iter_count == 0) return MC_OK;
+    if (use_mh_sliced(p)) {
+        const int64_t need = mh_sl_workspace_bytes(p, cfg->num_chains);
+        if (ws == nullptr || ws_bytes < need)
+            return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
+        if (device_cus() <= 0) return fail(MC_ERR_HIP, "no HIP device");
+        return mh_sliced_run(p, cfg, (float)proposal_scale, state, samples, tr, ws,
+                             (hipStream_t)stream);
+    }
     const bool lds = mh_use_lds(p);
     const int64_t need = mc_mh_workspace_bytes(p, cfg->num_chains);
     if (!lds && (ws == nullptr || ws_bytes < need))

@@ -1,0 +1,66 @@
+// run_mh_sl.hip — the sliced Metropolis-Hastings launch (k_mh_sl, mh_sliced.h)
+// for programs sliced onto the fast-form lane layout.
+#include "run_mh_sl.h"
+
+template <int RS, int NSH, int OCC, int FORM>
+static int launch_mh_sl(const mc_program* p, const mc_run_config* cfg, float scale, void* state,
+                        float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
+    auto kern = k_mh_sl<RS, NSH, kNslWaves, OCC, FORM>;
+    int64_t qo, go;
+    mc_state_offsets(p, cfg->num_chains, &qo, &go);
+    char* b = (char*)state;
+    RunArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.cfg = *cfg;
+    const LrCtx ctx = lrctx_of(p);
+    const size_t lds = (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm);
+    MC_HIP_TRY(allow_lds(kern, lds));
+    const int64_t C = cfg->num_chains;
+    const int64_t groups = (C + kNslWaves - 1) / kNslWaves;
+    const int S = p->lr.S;
+    const int64_t cap = resident_capacity(kern, 64 * kNslWaves, lds);
+    if (cap < S)
+        return fail(MC_ERR_UNSUPPORTED,
+                    "sliced MH: a chain block's %d workgroups must be co-resident, the device "
+                    "holds %lld of this kernel", S, (long long)cap);
+    const int64_t gpl = std::min(groups, cap / S);
+    const int64_t lines = mh_sl_line_bytes(p, C);
+    int* status = (int*)ws;
+    unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
+    A.fault = g_exchange_fault;
+    const uint64_t per_launch = (uint64_t)cfg->iter_count + 1;  // one exchange per iteration
+    const int64_t nlaunch = (groups + gpl - 1) / gpl;
+    uint32_t base = 0;
+    if (ws_reserve(ws, per_launch * (uint64_t)nlaunch, (uint64_t)(kSlStatusBytes + lines), &base))
+        MC_HIP_TRY(hipMemsetAsync(ws, 0, kSlStatusBytes + lines, st));
+    ws_mark_status(ws);
+    for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
+        const int64_t ng = std::min(gpl, groups - g0);
+        const hipError_t e = launch_exchange(kern, ng * S, 64 * kNslWaves, lds, st, ctx, A, scale,
+                                             g0 * kNslWaves, ng, (mc_chain_scalars*)b,
+                                             (float*)(b + qo), samples, trace_of(tr), xch, status,
+                                             base);
+        MC_HIP_TRY(e);
+        base += (uint32_t)per_launch;
+    }
+    return MC_OK;
+}
+
+int mh_sliced_run(const mc_program* p, const mc_run_config* cfg, float scale, void* state,
+                  float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
+    constexpr int HIER = LF_SW | LF_SWS | LF_DIR | LF_DM | LF_DS;
+    const bool hier = p->lr.form == HIER && lanes_forms_enabled();
+    const bool o4 = nuts_sl_occ(p) == 4;
+    const bool n4 = p->lr.Dsh > 3;
+#define MC_MH_SL(RS_)                                                                          \
+    if (hier) return o4 ? launch_mh_sl<RS_, 3, 4, HIER>(p, cfg, scale, state, samples, tr, ws, st) \
+                        : launch_mh_sl<RS_, 3, 2, HIER>(p, cfg, scale, state, samples, tr, ws, st); \
+    return n4 ? launch_mh_sl<RS_, 4, 2, -1>(p, cfg, scale, state, samples, tr, ws, st)             \
+              : launch_mh_sl<RS_, 3, 2, -1>(p, cfg, scale, state, samples, tr, ws, st)
+    switch (p->lr.rs) {
+        case 1: MC_MH_SL(1);
+        case 2: MC_MH_SL(2);
+        default: MC_MH_SL(4);
+    }
+#undef MC_MH_SL
+}

@@ -17,16 +17,18 @@ inline size_t nuts_sl_lds_bytes(const mc_program* p, int max_depth) {
                 (size_t)nuts_sl_shared_rows(max_depth) * 4) * 4;
 }
 
-// waves per SIMD the kernel is compiled for: with more than 8 slices a chain
-// block of 8 chains spans more workgroups than there are CUs per two blocks,
-// so two workgroups share a CU (4 waves per SIMD, <= 128 VGPRs); with <= 8
-// one workgroup per CU (2 waves per SIMD).  MC_NUTS_SL_OCC=2|4 overrides.
+// waves per SIMD the kernel is compiled for: with more than 8 slices two
+// workgroups share a CU (4 waves per SIMD, <= 128 VGPRs), so 256 chains of 16
+// slices run at once (4096 waves); with <= 8 one workgroup per CU (2 waves
+// per SIMD).  Large shape, 256 chains, 16 slices: 21.7 M leaf-steps/s at 4
+// waves per SIMD, 14.3 M at 2 (two launches of 128 chains); 8 slices at 2:
+// 18.5 M.  MC_NUTS_SL_OCC=2|4 overrides.
 inline int nuts_sl_occ(const mc_program* p) {
     if (const char* e = std::getenv("MC_NUTS_SL_OCC")) {
         const int v = std::atoi(e);
         if (v == 2 || v == 4) return v;
     }
-    return 2;
+    return p->lr.S > 8 ? 4 : 2;
 }
 
 // exchange lines (both parities) for every chain block of C chains

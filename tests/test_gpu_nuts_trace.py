@@ -286,9 +286,11 @@ def test_nuts_large_dual_averaging_against_oracle(gpu, slices):
                               fx["leaves"][j], n)
         print(f"large_da chain {chain}: replay identical for {same} of {n} (states within the "
               f"separation bound for {sep}); committed trace for {same_fx}")
-        # the committed trace's states separate from any other implementation's
-        # (the oracle's own, at another torch thread count, included) within a
-        # few iterations of eps ~ 4e-3: it is compared while the replay's states agree
-        assert same_fx >= min(MIN_SAME, sep), (
-            f"chain {chain}: trees diverge from the fixture at {same_fx}")
+        # the committed trace separates from any other run of the same
+        # restatement within a few iterations of eps ~ 4e-3 — the oracle's own
+        # at 4 torch threads instead of 1 agrees with it for 3 iterations
+        # (chain 0: depths 10, 6, 7, then 4 vs 3): the first 3, which hold the
+        # depth-10 tree and the first dual-averaging jump, are pinned; the
+        # strict replay above is the comparison beyond them
+        assert same_fx >= min(3, sep), f"chain {chain}: trees diverge from the fixture at {same_fx}"
     assert max(depths) >= 5, "real trees"
