@@ -356,17 +356,39 @@ MC_DEV ElemOut elem_identity(float v) {
     return o;
 }
 
+// The fused distributions a kernel build evaluates (bit d: MC_DIST d): all
+// of them, but the expression JIT (jit.hip gen_source) compiles only its
+// program's, so that Gamma / Beta's float64 gammaln stays out of kernels that
+// never run it.
+#ifndef MC_JIT_DISTS
+#define MC_JIT_DISTS 0x3Fu
+#endif
+constexpr bool dist_on(int d) { return ((MC_JIT_DISTS >> d) & 1u) != 0; }
+
 // Every distribution: logs = f32 log of operand slot 2 (scale / rate / beta;
 // unused by Beta), lg = the gammaln normaliser (Gamma, Beta; see lgamma_norm).
 MC_DEV ElemOut elem_eval(int dist, float c0, float v, float m, float s, float logs, float lg) {
     switch (dist) {
-        case MC_DIST_NORMAL: return elem_normal(c0, v, m, s, logs);
-        case MC_DIST_HALFNORMAL: return elem_halfnormal(c0, v, s, logs);
-        case MC_DIST_EXPONENTIAL: return elem_exponential(v, s, logs);
-        case MC_DIST_GAMMA: return elem_gamma(v, m, s, logs, lg);
-        case MC_DIST_IDENTITY: return elem_identity(v);
-        default: return elem_beta(v, m, s, lg);
+        case MC_DIST_NORMAL:
+            if constexpr (dist_on(MC_DIST_NORMAL)) return elem_normal(c0, v, m, s, logs);
+            break;
+        case MC_DIST_HALFNORMAL:
+            if constexpr (dist_on(MC_DIST_HALFNORMAL)) return elem_halfnormal(c0, v, s, logs);
+            break;
+        case MC_DIST_EXPONENTIAL:
+            if constexpr (dist_on(MC_DIST_EXPONENTIAL)) return elem_exponential(v, s, logs);
+            break;
+        case MC_DIST_GAMMA:
+            if constexpr (dist_on(MC_DIST_GAMMA)) return elem_gamma(v, m, s, logs, lg);
+            break;
+        case MC_DIST_IDENTITY:
+            if constexpr (dist_on(MC_DIST_IDENTITY)) return elem_identity(v);
+            break;
+        default:
+            if constexpr (dist_on(MC_DIST_BETA)) return elem_beta(v, m, s, lg);
+            break;
     }
+    return ElemOut{0.0f, 0.0f, 0.0f, 0.0f};
 }
 
 // The gammaln normaliser as the reference forms it (float64 scipy gammaln of
@@ -377,6 +399,12 @@ __host__ __device__ inline float lgamma_norm(int dist, float a, float b) {
     if (dist == MC_DIST_BETA)
         return (float)(lgamma((double)a) + lgamma((double)b) - lgamma((double)a + (double)b));
     return 0.0f;
+}
+
+// lgamma_norm in a kernel: compiled only where Gamma / Beta are (dist_on)
+MC_DEV float lg_norm_dev(int dist, float a, float b) {
+    if constexpr (!dist_on(MC_DIST_GAMMA) && !dist_on(MC_DIST_BETA)) return 0.0f;
+    return lgamma_norm(dist, a, b);
 }
 
 // Does the normaliser vary per element (a vector shape operand)?
@@ -546,7 +574,7 @@ MC_DEV void strided_generic(const DevTerm& T, const DevCtx& P, const float* q, f
         }
         const float s = fetch(T.op[2], i, us, q, P);
         const float logs = scale_vec ? logf(s) : ulogs;
-        const float lg = lgv ? lgamma_norm(T.dist, m, s) : ulg;
+        const float lg = lgv ? lg_norm_dev(T.dist, m, s) : ulg;
         const ElemOut e = elem_eval(T.dist, T.c0, v, m, s, logs, lg);
         if (mask & PASS_LP) lp_acc += w * e.lp;
         if (mask & PASS_VALUE) accum(T.op[0], i, w * e.dv, pv, g, q, P);
@@ -743,7 +771,7 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
                 if (aff) m = m + ub * xa;
                 const float s = seg_fetch(T.op[2], e, us, th, a == 2, q, P);
                 const float logs = (scale_vec || a == 2) ? logf(s) : ulogs;
-                const float lg = lgv ? lgamma_norm(T.dist, m, s) : ulg;
+                const float lg = lgv ? lg_norm_dev(T.dist, m, s) : ulg;
                 const ElemOut o = elem_eval(T.dist, T.c0, vv, m, s, logs, lg);
                 if (mask & PASS_LP) lp_acc += w * o.lp;
                 if (mask & PASS_VALUE) {
@@ -777,14 +805,106 @@ MC_DEV void seg_generic(const DevTerm& T, const DevCtx& P, const float* q, float
 // ---------------------------------------------------------------------------
 constexpr int kExMaxNodes = MC_EXPR_MAX_NODES;
 
+// The fused-term evaluation paths of eval_term (the strided moment sums per
+// operand-kind code 0..11 — MC_JIT_SU bits — and the other three paths): a
+// build compiles every one; the expression JIT (jit.hip) only those its
+// program's fused terms take.
+enum : uint32_t {
+    MC_PATH_STRIDED_GENERIC = 1u,
+    MC_PATH_SEG_NORMAL = 2u,
+    MC_PATH_SEG_GENERIC = 4u,
+};
+#ifndef MC_JIT_PATHS
+#define MC_JIT_PATHS 7u
+#endif
+#ifndef MC_JIT_SU
+#define MC_JIT_SU 0xFFFu
+#endif
+
+// Division in expression nodes: the reciprocal unit's 1/y refined by one
+// Newton step of the quotient, q + (x - y q) / y ~ q + (x - y q) r — within
+// an ulp of the IEEE quotient (the residual x - y q is exact in an FMA),
+// at 5 VALU beside the reciprocal instead of the ~10 of the scaled IEEE
+// sequence (v_div_scale / v_div_fmas / v_div_fixup).  An element loop's
+// uniform divisor keeps its reciprocal in a register.  Special operands
+// fall back to q = x * (1/y) (a NaN residual: infinities, 0/0), which is
+// the IEEE result for them.  Divisors beyond 2^126 in magnitude (their
+// reciprocal is subnormal) are outside its range.
+MC_DEV float ex_div(float x, float y) {
+    const float r = __builtin_amdgcn_rcpf(y);
+    const float q = x * r;
+    const float e = __builtin_fmaf(-y, q, x);
+    const float q1 = __builtin_fmaf(e, r, q);
+    return q1 == q1 ? q1 : q;
+}
+
+// log(1 + x) from the rounded sum u = 1 + x: log(u) * (x / (u - 1))
+// (the quotient corrects the rounding of u; exact for u - 1 == x), x where
+// u rounds to 1, and log(u) for u = inf.  A few ulp, against log1pf's ~40
+// instructions.
+MC_DEV float ex_log1p(float x) {
+    const float u = 1.0f + x;
+    const float d = u - 1.0f;
+    const float l = logf(u);
+    if (d == 0.0f) return x;
+    return __builtin_isinf(u) ? l : l * ex_div(x, d);
+}
+
+// The distribution nodes' element formulas: elem_normal / elem_halfnormal /
+// elem_exponential's operations with their divisions through ex_div.
+MC_DEV ElemOut ex_normal(float c0, float v, float m, float s, float logs) {
+    const float var = s * s;
+    const float d = v - m;
+    const float d2 = d * d;
+    ElemOut o;
+    o.lp = (c0 - logs) - ex_div(0.5f * d2, var);
+    const float t = ex_div(d, var);
+    o.dv = -t;
+    o.dm = t;
+    o.ds = ex_div(d2, var * s) - ex_div(1.0f, s);
+    return o;
+}
+MC_DEV ElemOut ex_halfnormal(float c0, float v, float s, float logs) {
+    ElemOut o;
+    if (v >= 0.0f) {
+        const float var = s * s;
+        const float v2 = v * v;
+        o.lp = (c0 - logs) - ex_div(0.5f * v2, var);
+        o.dv = -ex_div(v, var);
+        o.ds = ex_div(v2, var * s) - ex_div(1.0f, s);
+    } else {
+        o.lp = -__builtin_inff();
+        o.dv = 0.0f;
+        o.ds = 0.0f;
+    }
+    o.dm = 0.0f;
+    return o;
+}
+MC_DEV ElemOut ex_exponential(float v, float r, float logr) {
+    ElemOut o;
+    if (v >= 0.0f) {
+        o.lp = logr - r * v;
+        o.dv = -r;
+        o.ds = ex_div(1.0f, r) - v;
+    } else {
+        o.lp = -__builtin_inff();
+        o.dv = 0.0f;
+        o.ds = 0.0f;
+    }
+    o.dm = 0.0f;
+    return o;
+}
+
 // Forward value of a non-leaf node (x, y, z: its argument values; c0: the
 // distribution nodes' f32 normaliser, as elem_normal / elem_halfnormal).
+// Divisions go through ex_div, log1p through ex_log1p; exp / log / sqrt /
+// pow / tanh are ocml's.
 MC_DEV float ex_fwd(int op, float x, float y, float z, float c0) {
     switch (op) {
         case MC_EX_ADD: return x + y;
         case MC_EX_SUB: return x - y;
         case MC_EX_MUL: return x * y;
-        case MC_EX_DIV: return x / y;
+        case MC_EX_DIV: return ex_div(x, y);
         case MC_EX_NEG: return -x;
         case MC_EX_EXP: return expf(x);
         case MC_EX_LOG: return logf(x);
@@ -792,12 +912,12 @@ MC_DEV float ex_fwd(int op, float x, float y, float z, float c0) {
         case MC_EX_SQUARE: return x * x;
         case MC_EX_POW: return powf(x, y);
         case MC_EX_ABS: return fabsf(x);
-        case MC_EX_LOG1P: return log1pf(x);
+        case MC_EX_LOG1P: return ex_log1p(x);
         case MC_EX_TANH: return tanhf(x);
-        case MC_EX_SIGMOID: return 1.0f / (1.0f + expf(-x));
-        case MC_EX_NORMAL_LP: return elem_normal(c0, x, y, z, logf(z)).lp;
-        case MC_EX_HALFNORMAL_LP: return elem_halfnormal(c0, x, z, logf(z)).lp;
-        case MC_EX_EXPONENTIAL_LP: return elem_exponential(x, z, logf(z)).lp;
+        case MC_EX_SIGMOID: return ex_div(1.0f, 1.0f + expf(-x));
+        case MC_EX_NORMAL_LP: return ex_normal(c0, x, y, z, logf(z)).lp;
+        case MC_EX_HALFNORMAL_LP: return ex_halfnormal(c0, x, z, logf(z)).lp;
+        case MC_EX_EXPONENTIAL_LP: return ex_exponential(x, z, logf(z)).lp;
         case MC_EX_WHERE: return x != 0.0f ? y : z;
         default: return 0.0f;
     }
@@ -814,35 +934,35 @@ MC_DEV void ex_bwd(int op, float x, float y, float z, float v, float c, float c0
         case MC_EX_ADD: dx = c; dy = c; break;
         case MC_EX_SUB: dx = c; dy = -c; break;
         case MC_EX_MUL: dx = c * y; dy = c * x; break;
-        case MC_EX_DIV: dx = c / y; dy = -((c * x) / (y * y)); break;
+        case MC_EX_DIV: dx = ex_div(c, y); dy = -ex_div(c * x, y * y); break;
         case MC_EX_NEG: dx = -c; break;
         case MC_EX_EXP: dx = c * v; break;
-        case MC_EX_LOG: dx = c / x; break;
-        case MC_EX_SQRT: dx = c / (2.0f * v); break;
+        case MC_EX_LOG: dx = ex_div(c, x); break;
+        case MC_EX_SQRT: dx = ex_div(c, 2.0f * v); break;
         case MC_EX_SQUARE: dx = c * (2.0f * x); break;
         case MC_EX_POW:
             dx = c * (y * powf(x, y - 1.0f));
             dy = c * (v * logf(x));
             break;
         case MC_EX_ABS: dx = x > 0.0f ? c : (x < 0.0f ? -c : 0.0f); break;
-        case MC_EX_LOG1P: dx = c / (1.0f + x); break;
+        case MC_EX_LOG1P: dx = ex_div(c, 1.0f + x); break;
         case MC_EX_TANH: dx = c * (1.0f - v * v); break;
         case MC_EX_SIGMOID: dx = c * (v * (1.0f - v)); break;
         case MC_EX_NORMAL_LP: {
-            const ElemOut e = elem_normal(c0, x, y, z, logf(z));
+            const ElemOut e = ex_normal(c0, x, y, z, logf(z));
             dx = c * e.dv;
             dy = c * e.dm;
             dz = c * e.ds;
             break;
         }
         case MC_EX_HALFNORMAL_LP: {
-            const ElemOut e = elem_halfnormal(c0, x, z, logf(z));
+            const ElemOut e = ex_halfnormal(c0, x, z, logf(z));
             dx = c * e.dv;
             dz = c * e.ds;
             break;
         }
         case MC_EX_EXPONENTIAL_LP: {
-            const ElemOut e = elem_exponential(x, z, logf(z));
+            const ElemOut e = ex_exponential(x, z, logf(z));
             dx = c * e.dv;
             dz = c * e.ds;
             break;
@@ -940,7 +1060,7 @@ MC_DEV void eval_expr_n(const DevTerm& T, const DevCtx& P, const float* q, float
             }
             if (pass == 0) lp_acc += w * val[nn - 1];
             if constexpr (VALUE_ONLY) return;
-            for (int k = 0; k < nn; ++k) adj[k] = 0.0f;
+            for (int k = 0; k < nn; ++k) adj[k] = -0.0f;  // (-0 + x == x: jit.hip gen_term)
             adj[nn - 1] = w;
             for (int k = nn - 1; k >= 0; --k) {
                 const float ck = adj[k];
@@ -1068,6 +1188,11 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
             return;
         }
     }
+    // (a JIT build names the fused-term paths its program takes, jit.hip
+    // gen_source: the others are compiled out — registers and code)
+    constexpr uint32_t su_codes = MC_JIT_SU;
+    constexpr uint32_t paths = MC_JIT_PATHS;
+    if constexpr (paths == 0 && su_codes == 0) return;
     const float uv = uniform_value(T.op[0], q);
     const float um = uniform_value(T.op[1], q);
     const float us = uniform_value(T.op[2], q);
@@ -1081,7 +1206,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
     const float ulg = lg_per_element(T.dist, T.op[1].kind, T.op[2].kind)
                           ? 0.0f
                           : ((T.op[1].kind == MC_OP_PSCALAR || T.op[2].kind == MC_OP_PSCALAR)
-                                 ? lgamma_norm(T.dist, um, us)
+                                 ? lg_norm_dev(T.dist, um, us)
                                  : T.clg);
 
     MC_STAMP(20);
@@ -1102,7 +1227,8 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                 switch (code) {
 #define MC_SU(c, D_, V_, L_)                                                                \
     case c:                                                                                 \
-        strided_uscale<D_, V_, L_>(T, P, q, g, tid, nthr, mask, uv, um, var, M);            \
+        if constexpr ((su_codes >> c) & 1u)                                                 \
+            strided_uscale<D_, V_, L_>(T, P, q, g, tid, nthr, mask, uv, um, var, M);        \
         break;
                     MC_SU(0, MC_DIST_NORMAL, 0, 0)
                     MC_SU(1, MC_DIST_NORMAL, 0, 1)
@@ -1120,7 +1246,7 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                     default:
                         break;
                 }
-            } else {
+            } else if constexpr ((paths & MC_PATH_STRIDED_GENERIC) != 0) {
                 strided_generic(T, P, q, g, tid, nthr, mask, uv, um, us, ulogs, ulg, lp_acc, pv,
                                 pm, ps, pb);
             }
@@ -1133,11 +1259,13 @@ MC_DEV void eval_term(const DevTerm& T, const DevCtx& P, const float* q, float* 
                               !T.affine && prim_xf == MC_XF_NONE;
             if (fast) {
                 moments = true;
-                if (T.primary == 1)
-                    seg_normal_uscale<WPC, 1>(T, P, q, g, G, mask, var, M, vpart);
-                else
-                    seg_normal_uscale<WPC, 0>(T, P, q, g, G, mask, var, M, vpart);
-            } else {
+                if constexpr ((paths & MC_PATH_SEG_NORMAL) != 0) {
+                    if (T.primary == 1)
+                        seg_normal_uscale<WPC, 1>(T, P, q, g, G, mask, var, M, vpart);
+                    else
+                        seg_normal_uscale<WPC, 0>(T, P, q, g, G, mask, var, M, vpart);
+                }
+            } else if constexpr ((paths & MC_PATH_SEG_GENERIC) != 0) {
                 seg_generic<WPC>(T, P, q, g, G, mask, uv, um, us, ulogs, ulg, lp_acc, pv, pm,
                                  ps, pb, vpart);
             }

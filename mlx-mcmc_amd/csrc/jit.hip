@@ -99,7 +99,26 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
       << "  for (int pass = 0; pass < npass; ++pass) {\n";
     for (int k = 0; k < nn; ++k)
         if (is_part(k)) o << "    float p" << k << " = 0.0f;\n";
-    o << "    auto element = [&](int64_t e, int kr) {\n"
+    // data leaves and gather indices are the element's arguments, so that
+    // an unrolled loop issues every load of its elements first
+    std::string params, args_of_e;  // "float dK, int xK" / "P.data[lK + e], P.index[lK + e]"
+    for (int k = 0; k < nn; ++k) {
+        const DevExprNode& d = N[k];
+        if (d.op != MC_EX_LEAF || d.prim) continue;
+        if (d.leaf.kind == MC_OP_DATA) {
+            params += ", float d" + std::to_string(k);
+            args_of_e += ", P.data[l" + std::to_string(k) + " + @]";
+        } else if (d.leaf.kind == MC_OP_GATHER) {
+            params += ", int x" + std::to_string(k);
+            args_of_e += ", P.index[l" + std::to_string(k) + " + @]";
+        }
+    }
+    auto args_at = [&](const std::string& e) {
+        std::string a = args_of_e;
+        for (size_t at; (at = a.find('@')) != std::string::npos;) a.replace(at, 1, e);
+        return a;
+    };
+    o << "    auto element = [&](int64_t e, int kr" << params << ") {\n"
       << "      (void)e; (void)kr;\n";
     auto arg = [&](int a) { return a >= 0 ? "v" + std::to_string(a) : std::string("0.0f"); };
     for (int k = 0; k < nn; ++k) {
@@ -110,9 +129,9 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
             if (d.prim) o << "q[o" << k << " + kr]";
             else if (kind == MC_OP_CONST) o << "c" << k;
             else if (kind == MC_OP_PSCALAR) o << "q[o" << k << "]";
-            else if (kind == MC_OP_DATA) o << "P.data[l" << k << " + e]";
+            else if (kind == MC_OP_DATA) o << "d" << k;
             else if (kind == MC_OP_PVEC) o << "q[o" << k << " + e]";
-            else o << "q[o" << k << " + P.index[l" << k << " + e]]";
+            else o << "q[o" << k << " + x" << k << "]";
         } else {
             o << "ex_fwd(" << d.op << ", " << arg(d.a) << ", " << arg(d.b) << ", " << arg(d.c)
               << ", c" << k << ")";
@@ -121,7 +140,9 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
     }
     o << "      if (pass == 0) lp_acc += w * v" << nn - 1 << ";\n"
       << "      if constexpr (VALUE_ONLY) return;\n";
-    for (int k = 0; k < nn; ++k) o << "      float a" << k << " = 0.0f;\n";
+    // (adjoints start at -0: -0 + x == x for every x, so a first contribution
+    // needs no add; the interpreter starts them at -0 too)
+    for (int k = 0; k < nn; ++k) o << "      float a" << k << " = -0.0f;\n";
     o << "      a" << nn - 1 << " = w;\n";
     for (int k = nn - 1; k >= 0; --k) {
         const DevExprNode& d = N[k];
@@ -132,7 +153,7 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
             } else if (kind == MC_OP_PVEC || kind == MC_OP_GATHER) {
                 o << "      if (pass == " << (d.pass & 15) << ") g[";
                 if (kind == MC_OP_PVEC) o << "(int64_t)o" << k << " + e";
-                else o << "(int64_t)o" << k << " + P.index[l" << k << " + e]";
+                else o << "(int64_t)o" << k << " + x" << k;
                 o << "] += a" << k << ";\n";
             }
             continue;
@@ -146,7 +167,37 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
     }
     o << "    };\n";
     if (!seg) {
-        o << "    for (int64_t i = tid; i < T.n; i += nthr) element(i, 0);\n";
+        // four elements per trip, their loads first (the element order, and
+        // so every sum, is the strided loop's)
+        o << "    int64_t i = tid;\n"
+          << "    const int64_t st = nthr;\n"
+          << "    for (; i + 3 * st < T.n; i += 4 * st) {\n"
+          << "      const int64_t e0 = i, e1 = i + st, e2 = i + 2 * st, e3 = i + 3 * st;\n";
+        {
+            std::string decl[4];
+            for (int u = 0; u < 4; ++u) {
+                const std::string e = "e" + std::to_string(u);
+                const std::string a = args_at(e);
+                // a, ", x, y" -> named temporaries t<u>_<n>
+                std::string names;
+                size_t pos = 0;
+                int n = 0;
+                while ((pos = a.find(", ", pos)) != std::string::npos) {
+                    size_t nxt = a.find(", ", pos + 2);
+                    const std::string ex = a.substr(pos + 2, nxt == std::string::npos ? std::string::npos : nxt - pos - 2);
+                    const bool isint = ex.rfind("P.index", 0) == 0;
+                    o << "      const " << (isint ? "int" : "float") << " t" << u << "_" << n << " = " << ex << ";\n";
+                    names += ", t" + std::to_string(u) + "_" + std::to_string(n);
+                    ++n;
+                    pos += 2;
+                }
+                decl[u] = names;
+            }
+            for (int u = 0; u < 4; ++u)
+                o << "      element(e" << u << ", 0" << decl[u] << ");\n";
+        }
+        o << "    }\n"
+          << "    for (; i < T.n; i += st) element(i, 0" << args_at("i") << ");\n";
     } else {
         o << "    const bool split = T.ncomb > 0;\n"
           << "    const int wave = G.tid >> 6;\n"
@@ -161,7 +212,8 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
           << "      const int len = valid ? lanes[2 * v + 1] : 0;\n";
         for (int k = 0; k < nn; ++k)
             if (N[k].op == MC_EX_LEAF && N[k].prim) o << "      p" << k << " = 0.0f;\n";
-        o << "      for (int u = 0; u < len; ++u) element(seg_elem(off, u, lane), kr);\n"
+        o << "      for (int u = 0; u < len; ++u) { const int64_t e = seg_elem(off, u, lane); "
+          << "element(e, kr" << args_at("e") << "); }\n"
           << "      if (!VALUE_ONLY && valid) {\n";
         for (int k = 0; k < nn; ++k) {
             if (N[k].op != MC_EX_LEAF || !N[k].prim) continue;
@@ -202,9 +254,49 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
 
 // The program's generated source: every expression term's evaluator and
 // the dispatch the eval.h hook calls.
+// eval.h eval_term's choice of path for a fused term (the same predicates):
+// a strided moment-sum code 0..11 as bit `code` of *su, else a path bit.
+bool host_is_vec(int kind) {
+    return kind == MC_OP_DATA || kind == MC_OP_PVEC || kind == MC_OP_GATHER;
+}
+int host_fast_kind(const DevOperand& o) {
+    if (o.xf != MC_XF_NONE && host_is_vec(o.kind)) return -1;
+    return o.kind == MC_OP_DATA ? 1 : (o.kind == MC_OP_PVEC ? 2 : (host_is_vec(o.kind) ? -1 : 0));
+}
+void fused_paths(const mc_program* p, uint32_t* paths, uint32_t* su, uint32_t* dists) {
+    *paths = 0;
+    *su = 0;
+    *dists = 0;
+    for (const DevTerm& T : p->terms) {
+        if (T.dist == MC_DIST_EXPR) continue;
+        *dists |= 1u << T.dist;
+        const bool normal = T.dist == MC_DIST_NORMAL;
+        const bool moment_dist = normal || T.dist == MC_DIST_HALFNORMAL;
+        const bool scale_vec = host_is_vec(T.op[2].kind);
+        if (T.primary < 0) {
+            const int fv = host_fast_kind(T.op[0]);
+            const int fl = normal ? host_fast_kind(T.op[1]) : 0;
+            if (moment_dist && !scale_vec && fv >= 0 && fl >= 0 && !T.affine)
+                *su |= 1u << (normal ? (fv * 3 + fl) : (9 + fv));
+            else
+                *paths |= MC_PATH_STRIDED_GENERIC;
+        } else {
+            const int other_kind = T.primary == 1 ? T.op[0].kind : T.op[1].kind;
+            const int prim_xf = T.op[T.primary].xf;
+            const bool fast = normal && !scale_vec && T.primary <= 1 && other_kind == MC_OP_DATA &&
+                              !T.affine && prim_xf == MC_XF_NONE;
+            *paths |= fast ? MC_PATH_SEG_NORMAL : MC_PATH_SEG_GENERIC;
+        }
+    }
+}
+
 std::string gen_source(const mc_program* p) {
     std::ostringstream o;
+    uint32_t paths = 0, su = 0, dists = 0;
+    fused_paths(p, &paths, &su, &dists);
     o << "// generated by jit.hip for one program: do not edit\n"
+      << "#define MC_JIT_PATHS " << paths << "u\n#define MC_JIT_SU " << su << "u\n"
+      << "#define MC_JIT_DISTS " << dists << "u\n"
       << "#include \"hmc.h\"\n#include \"nuts.h\"\n#include \"mh.h\"\n"
       << "namespace mc {\n";
     std::vector<int32_t> bases;

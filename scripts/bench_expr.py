@@ -4,18 +4,23 @@ events around the launches, L = 10, 256 chains), plus the host-side trace +
 program build time.  The linear regression written two ways — the affine
 fused loc and the same likelihood as a hand-written expression — plus the
 two-predictor and logistic models."""
+import os
 import sys
 import time
-sys.path[:0] = ["."]
+sys.path[:0] = [os.path.dirname(os.path.dirname(os.path.abspath(__file__)))]
 import numpy as np
 import torch
 import mlx_mcmc_amd as m
 import mlx_mcmc_amd.core as mx
 import workloads as W
-from mlx_mcmc_amd import _engine, _trace
+from mlx_mcmc_amd import _engine, _lib, _trace
+
+LIB = _lib.load()
 
 
-def rate(lp, init, chains=256, L=10, eps=1e-3, iters=20):
+def rate(lp, init, chains=256, L=10, eps=1e-3, iters=20, jit=-1):
+    """jit: -1 the default (expression terms compiled), 0 the interpreter."""
+    LIB.mc_debug_expr_jit(jit)
     t0 = time.perf_counter()
     prog = _trace.compile_model(lp, init)
     t_build = time.perf_counter() - t0
@@ -32,6 +37,8 @@ def rate(lp, init, chains=256, L=10, eps=1e-3, iters=20):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1)
+    cs.check_status()
+    LIB.mc_debug_expr_jit(-1)
     return chains * iters * L / (ms * 1e-3), t_build, prog.slice_kernel
 
 
@@ -91,8 +98,12 @@ for sl, name in ((0, "lane-resident (auto)"), (1, "tape (num_slices=1)")):
 lp, _ = W.two_predictor_regression(W.ns_product(), N)
 i2 = {"a": np.float32(0.5), "b1": np.float32(1.2), "b2": np.float32(-0.8),
       "log_sigma": np.float32(-0.5)}
-r, tb, k = rate(lp, i2)
-print(f"two-predictor N={N} expression: {r / 1e6:.3f} M chain-steps/s (build {tb:.2f} s)")
+for jit, nm in ((0, "interpreter"), (-1, "JIT")):
+    r, tb, k = rate(lp, i2, jit=jit)
+    print(f"two-predictor N={N} expression ({nm}): {r / 1e6:.3f} M chain-steps/s "
+          f"(build {tb:.2f} s)")
 lp, _ = W.logistic_regression(W.ns_product(), N)
-r, tb, k = rate(lp, {"a": np.float32(-0.3), "b": np.float32(1.1)})
-print(f"logistic N={N} expression: {r / 1e6:.3f} M chain-steps/s (build {tb:.2f} s)")
+for jit, nm in ((0, "interpreter"), (-1, "JIT")):
+    r, tb, k = rate(lp, {"a": np.float32(-0.3), "b": np.float32(1.1)}, jit=jit)
+    print(f"logistic N={N} expression ({nm}): {r / 1e6:.3f} M chain-steps/s "
+          f"(build {tb:.2f} s)")
