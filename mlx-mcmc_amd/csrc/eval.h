@@ -838,16 +838,41 @@ MC_DEV float ex_div(float x, float y) {
     return q1 == q1 ? q1 : q;
 }
 
+// exp and log in expression nodes: the transcendental unit (v_exp_f32 /
+// v_log_f32, base 2) with the conversion to base e done in extended
+// precision where it matters, ~1-2 ulp (ocml's expf / logf: ~1 ulp, about
+// twice the instructions for their range and subnormal handling).
+//   exp: t = x log2(e) rounded, its residual x log2(e) - t from an FMA plus
+//        the low part of log2(e); exp2(t) (1 + residual ln 2).  Infinite or
+//        zero exp2(t) (|x| beyond the range, +-inf) is returned as is.
+//        Subnormal results are the unit's.
+//   log: log2 of the argument (a subnormal one scaled by 2^32 first) times
+//        ln 2; 0 -> -inf, negative -> NaN, inf -> inf.
+MC_DEV float ex_exp(float x) {
+    const float L = 1.44269502162933349609375f;     // f32 log2(e)
+    const float Llo = 1.925963033500011079e-8f;      // log2(e) - L
+    const float t = x * L;
+    const float lo = __builtin_fmaf(x, L, -t) + x * Llo;
+    const float r = __builtin_amdgcn_exp2f(t);
+    const float c = lo * 0.693147180559945309f;
+    return (r == 0.0f || __builtin_isinf(r)) ? r : __builtin_fmaf(r, c, r);
+}
+MC_DEV float ex_log(float x) {
+    const bool sub = x < 1.17549435e-38f;  // subnormal, zero or negative
+    const float r = __builtin_amdgcn_logf(sub ? x * 4294967296.0f : x);
+    return (sub ? r - 32.0f : r) * 0.693147180559945309f;
+}
+
 // log(1 + x) from the rounded sum u = 1 + x: log(u) * (x / (u - 1))
 // (the quotient corrects the rounding of u; exact for u - 1 == x), x where
-// u rounds to 1, and log(u) for u = inf.  A few ulp, against log1pf's ~40
-// instructions.
+// u rounds to 1, and log(u) for u = inf.  A few ulp, branch-free, against
+// log1pf's ~40 instructions.
 MC_DEV float ex_log1p(float x) {
     const float u = 1.0f + x;
     const float d = u - 1.0f;
-    const float l = logf(u);
-    if (d == 0.0f) return x;
-    return __builtin_isinf(u) ? l : l * ex_div(x, d);
+    const float l = ex_log(u);
+    const float r = __builtin_isinf(u) ? l : l * ex_div(x, d);
+    return d == 0.0f ? x : r;
 }
 
 // The distribution nodes' element formulas: elem_normal / elem_halfnormal /
@@ -897,8 +922,8 @@ MC_DEV ElemOut ex_exponential(float v, float r, float logr) {
 
 // Forward value of a non-leaf node (x, y, z: its argument values; c0: the
 // distribution nodes' f32 normaliser, as elem_normal / elem_halfnormal).
-// Divisions go through ex_div, log1p through ex_log1p; exp / log / sqrt /
-// pow / tanh are ocml's.
+// Divisions go through ex_div, exp / log / log1p through ex_exp / ex_log /
+// ex_log1p; sqrt / pow / tanh are ocml's.
 MC_DEV float ex_fwd(int op, float x, float y, float z, float c0) {
     switch (op) {
         case MC_EX_ADD: return x + y;
@@ -906,18 +931,18 @@ MC_DEV float ex_fwd(int op, float x, float y, float z, float c0) {
         case MC_EX_MUL: return x * y;
         case MC_EX_DIV: return ex_div(x, y);
         case MC_EX_NEG: return -x;
-        case MC_EX_EXP: return expf(x);
-        case MC_EX_LOG: return logf(x);
+        case MC_EX_EXP: return ex_exp(x);
+        case MC_EX_LOG: return ex_log(x);
         case MC_EX_SQRT: return sqrtf(x);
         case MC_EX_SQUARE: return x * x;
         case MC_EX_POW: return powf(x, y);
         case MC_EX_ABS: return fabsf(x);
         case MC_EX_LOG1P: return ex_log1p(x);
         case MC_EX_TANH: return tanhf(x);
-        case MC_EX_SIGMOID: return ex_div(1.0f, 1.0f + expf(-x));
-        case MC_EX_NORMAL_LP: return ex_normal(c0, x, y, z, logf(z)).lp;
-        case MC_EX_HALFNORMAL_LP: return ex_halfnormal(c0, x, z, logf(z)).lp;
-        case MC_EX_EXPONENTIAL_LP: return ex_exponential(x, z, logf(z)).lp;
+        case MC_EX_SIGMOID: return ex_div(1.0f, 1.0f + ex_exp(-x));
+        case MC_EX_NORMAL_LP: return ex_normal(c0, x, y, z, ex_log(z)).lp;
+        case MC_EX_HALFNORMAL_LP: return ex_halfnormal(c0, x, z, ex_log(z)).lp;
+        case MC_EX_EXPONENTIAL_LP: return ex_exponential(x, z, ex_log(z)).lp;
         case MC_EX_WHERE: return x != 0.0f ? y : z;
         default: return 0.0f;
     }
@@ -949,20 +974,20 @@ MC_DEV void ex_bwd(int op, float x, float y, float z, float v, float c, float c0
         case MC_EX_TANH: dx = c * (1.0f - v * v); break;
         case MC_EX_SIGMOID: dx = c * (v * (1.0f - v)); break;
         case MC_EX_NORMAL_LP: {
-            const ElemOut e = ex_normal(c0, x, y, z, logf(z));
+            const ElemOut e = ex_normal(c0, x, y, z, ex_log(z));
             dx = c * e.dv;
             dy = c * e.dm;
             dz = c * e.ds;
             break;
         }
         case MC_EX_HALFNORMAL_LP: {
-            const ElemOut e = ex_halfnormal(c0, x, z, logf(z));
+            const ElemOut e = ex_halfnormal(c0, x, z, ex_log(z));
             dx = c * e.dv;
             dz = c * e.ds;
             break;
         }
         case MC_EX_EXPONENTIAL_LP: {
-            const ElemOut e = ex_exponential(x, z, logf(z));
+            const ElemOut e = ex_exponential(x, z, ex_log(z));
             dx = c * e.dv;
             dz = c * e.ds;
             break;

@@ -95,7 +95,18 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
             o << "  const float c" << k << " = N[" << k << "].leaf.cval;\n";
         }
     }
-    o << "  const int npass = VALUE_ONLY ? 1 : T.npass;\n"
+    // the pass count is a function of the leaves' passes (api.hip
+    // build_expr_term), so it is a constant here: one pass (the usual case)
+    // leaves no pass tests in the element code
+    int npass_c = 1;
+    for (int k = 0; k < nn; ++k)
+        if (N[k].op == MC_EX_LEAF && (N[k].leaf.kind == MC_OP_PVEC || N[k].leaf.kind == MC_OP_GATHER))
+            npass_c = std::max(npass_c, (N[k].pass & 15) + 1);
+    if (npass_c == T.npass)
+        o << "  const int npass = VALUE_ONLY ? 1 : " << npass_c << ";\n";
+    else
+        o << "  const int npass = VALUE_ONLY ? 1 : T.npass;\n";
+    o
       << "  for (int pass = 0; pass < npass; ++pass) {\n";
     for (int k = 0; k < nn; ++k)
         if (is_part(k)) o << "    float p" << k << " = 0.0f;\n";
