@@ -826,16 +826,15 @@ enum : uint32_t {
 // an ulp of the IEEE quotient (the residual x - y q is exact in an FMA),
 // at 5 VALU beside the reciprocal instead of the ~10 of the scaled IEEE
 // sequence (v_div_scale / v_div_fmas / v_div_fixup).  An element loop's
-// uniform divisor keeps its reciprocal in a register.  Special operands
-// fall back to q = x * (1/y) (a NaN residual: infinities, 0/0), which is
-// the IEEE result for them.  Divisors beyond 2^126 in magnitude (their
-// reciprocal is subnormal) are outside its range.
+// uniform divisor keeps its reciprocal in a register.  v_div_fixup_f32
+// replaces the quotient by the IEEE result where an operand is special (a
+// zero or infinite divisor, infinite or NaN operands).  Divisors beyond 2^126
+// in magnitude (their reciprocal is subnormal) are outside its range.
 MC_DEV float ex_div(float x, float y) {
     const float r = __builtin_amdgcn_rcpf(y);
     const float q = x * r;
     const float e = __builtin_fmaf(-y, q, x);
-    const float q1 = __builtin_fmaf(e, r, q);
-    return q1 == q1 ? q1 : q;
+    return __builtin_amdgcn_div_fixupf(__builtin_fmaf(e, r, q), y, x);
 }
 
 // exp and log in expression nodes: the transcendental unit (v_exp_f32 /

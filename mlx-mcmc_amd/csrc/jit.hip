@@ -90,7 +90,9 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
                 o << "  const int64_t l" << k << " = N[" << k << "].leaf.pool;\n";
             if (!N[k].prim && kind == MC_OP_CONST)
                 o << "  const float c" << k << " = N[" << k << "].leaf.cval;\n";
-            if (kind == MC_OP_PSCALAR) o << "  const int s" << k << " = N[" << k << "].leaf.slot;\n";
+            if (kind == MC_OP_PSCALAR)
+                o << "  const int s" << k << " = N[" << k << "].leaf.slot;\n"
+                  << "  const float qv" << k << " = q[o" << k << "];  // (read once per term)\n";
         } else {
             o << "  const float c" << k << " = N[" << k << "].leaf.cval;\n";
         }
@@ -139,7 +141,7 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
             const int kind = d.leaf.kind;
             if (d.prim) o << "q[o" << k << " + kr]";
             else if (kind == MC_OP_CONST) o << "c" << k;
-            else if (kind == MC_OP_PSCALAR) o << "q[o" << k << "]";
+            else if (kind == MC_OP_PSCALAR) o << "qv" << k;
             else if (kind == MC_OP_DATA) o << "d" << k;
             else if (kind == MC_OP_PVEC) o << "q[o" << k << " + e]";
             else o << "q[o" << k << " + x" << k << "]";
@@ -179,7 +181,9 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
     o << "    };\n";
     if (!seg) {
         // four elements per trip, their loads first (the element order, and
-        // so every sum, is the strided loop's)
+        // so every sum, is the strided loop's).  (Prefetching the next trip's
+        // loads behind this trip's arithmetic measured slower: the loop is
+        // issue-bound, and pinning the loads costs the scheduler its freedom.)
         o << "    int64_t i = tid;\n"
           << "    const int64_t st = nthr;\n"
           << "    for (; i + 3 * st < T.n; i += 4 * st) {\n"
@@ -187,25 +191,25 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
         {
             std::string decl[4];
             for (int u = 0; u < 4; ++u) {
-                const std::string e = "e" + std::to_string(u);
-                const std::string a = args_at(e);
-                // a, ", x, y" -> named temporaries t<u>_<n>
+                const std::string a = args_at("e" + std::to_string(u));
+                // a = ", x, y": named temporaries t<u>_<n>
                 std::string names;
                 size_t pos = 0;
                 int n = 0;
                 while ((pos = a.find(", ", pos)) != std::string::npos) {
-                    size_t nxt = a.find(", ", pos + 2);
-                    const std::string ex = a.substr(pos + 2, nxt == std::string::npos ? std::string::npos : nxt - pos - 2);
+                    const size_t nxt = a.find(", ", pos + 2);
+                    const std::string ex =
+                        a.substr(pos + 2, nxt == std::string::npos ? std::string::npos : nxt - pos - 2);
                     const bool isint = ex.rfind("P.index", 0) == 0;
-                    o << "      const " << (isint ? "int" : "float") << " t" << u << "_" << n << " = " << ex << ";\n";
+                    o << "      const " << (isint ? "int" : "float") << " t" << u << "_" << n << " = "
+                      << ex << ";\n";
                     names += ", t" + std::to_string(u) + "_" + std::to_string(n);
                     ++n;
                     pos += 2;
                 }
                 decl[u] = names;
             }
-            for (int u = 0; u < 4; ++u)
-                o << "      element(e" << u << ", 0" << decl[u] << ");\n";
+            for (int u = 0; u < 4; ++u) o << "      element(e" << u << ", 0" << decl[u] << ");\n";
         }
         o << "    }\n"
           << "    for (; i < T.n; i += st) element(i, 0" << args_at("i") << ");\n";
