@@ -999,6 +999,93 @@ MC_DEV void ex_bwd(int op, float x, float y, float z, float v, float c, float c0
     }
 }
 
+// ---- two elements at once (the expression JIT's paired element code) -------
+// The same operations as ex_fwd / ex_bwd on a pair of elements: the plain
+// arithmetic packed (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 round every
+// lane exactly as the scalar instruction), the transcendental unit, the
+// fix-ups and the selects per component.  So each component is bit-identical
+// to the scalar path's result for its element.
+typedef float exf2 __attribute__((ext_vector_type(2)));
+
+MC_DEV exf2 ex2_fma(exf2 a, exf2 b, exf2 c) { return __builtin_elementwise_fma(a, b, c); }
+MC_DEV exf2 ex2_div(exf2 x, exf2 y) {
+    const exf2 r = {__builtin_amdgcn_rcpf(y.x), __builtin_amdgcn_rcpf(y.y)};
+    const exf2 q = x * r;
+    const exf2 e = ex2_fma(-y, q, x);
+    const exf2 q1 = ex2_fma(e, r, q);
+    return exf2{__builtin_amdgcn_div_fixupf(q1.x, y.x, x.x),
+                __builtin_amdgcn_div_fixupf(q1.y, y.y, x.y)};
+}
+MC_DEV exf2 ex2_exp(exf2 x) {
+    const float L = 1.44269502162933349609375f;
+    const float Llo = 1.925963033500011079e-8f;
+    const exf2 t = x * L;
+    const exf2 lo = ex2_fma(x, exf2{L, L}, -t) + x * Llo;
+    const exf2 r = {__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+    const exf2 c = lo * 0.693147180559945309f;
+    const exf2 f = ex2_fma(r, c, r);
+    return exf2{(r.x == 0.0f || __builtin_isinf(r.x)) ? r.x : f.x,
+                (r.y == 0.0f || __builtin_isinf(r.y)) ? r.y : f.y};
+}
+MC_DEV exf2 ex2_log(exf2 x) {
+    const bool sx = x.x < 1.17549435e-38f, sy = x.y < 1.17549435e-38f;
+    const exf2 xs = x * exf2{sx ? 4294967296.0f : 1.0f, sy ? 4294967296.0f : 1.0f};
+    const exf2 r = {__builtin_amdgcn_logf(xs.x), __builtin_amdgcn_logf(xs.y)};
+    return exf2{sx ? r.x - 32.0f : r.x, sy ? r.y - 32.0f : r.y} * 0.693147180559945309f;
+}
+MC_DEV exf2 ex2_log1p(exf2 x) {
+    const exf2 u = 1.0f + x;
+    const exf2 d = u - 1.0f;
+    const exf2 l = ex2_log(u);
+    const exf2 r = l * ex2_div(x, d);
+    return exf2{d.x == 0.0f ? x.x : (__builtin_isinf(u.x) ? l.x : r.x),
+                d.y == 0.0f ? x.y : (__builtin_isinf(u.y) ? l.y : r.y)};
+}
+MC_DEV exf2 ex2_each(float (*f)(float), exf2 x) { return exf2{f(x.x), f(x.y)}; }
+
+MC_DEV exf2 ex2_fwd(int op, exf2 x, exf2 y, exf2 z, float c0) {
+    switch (op) {
+        case MC_EX_ADD: return x + y;
+        case MC_EX_SUB: return x - y;
+        case MC_EX_MUL: return x * y;
+        case MC_EX_DIV: return ex2_div(x, y);
+        case MC_EX_NEG: return -x;
+        case MC_EX_EXP: return ex2_exp(x);
+        case MC_EX_LOG: return ex2_log(x);
+        case MC_EX_SQUARE: return x * x;
+        case MC_EX_LOG1P: return ex2_log1p(x);
+        case MC_EX_SIGMOID: return ex2_div(exf2{1.0f, 1.0f}, 1.0f + ex2_exp(-x));
+        default:  // the rest per component through the scalar path
+            return exf2{ex_fwd(op, x.x, y.x, z.x, c0), ex_fwd(op, x.y, y.y, z.y, c0)};
+    }
+}
+MC_DEV void ex2_bwd(int op, exf2 x, exf2 y, exf2 z, exf2 v, exf2 c, float c0, exf2& dx, exf2& dy,
+                    exf2& dz) {
+    dx = dy = dz = exf2{0.0f, 0.0f};
+    switch (op) {
+        case MC_EX_ADD: dx = c; dy = c; break;
+        case MC_EX_SUB: dx = c; dy = -c; break;
+        case MC_EX_MUL: dx = c * y; dy = c * x; break;
+        case MC_EX_DIV: dx = ex2_div(c, y); dy = -ex2_div(c * x, y * y); break;
+        case MC_EX_NEG: dx = -c; break;
+        case MC_EX_EXP: dx = c * v; break;
+        case MC_EX_LOG: dx = ex2_div(c, x); break;
+        case MC_EX_SQUARE: dx = c * (2.0f * x); break;
+        case MC_EX_LOG1P: dx = ex2_div(c, 1.0f + x); break;
+        case MC_EX_TANH: dx = c * (1.0f - v * v); break;
+        case MC_EX_SIGMOID: dx = c * (v * (1.0f - v)); break;
+        default: {
+            float ax, ay, az, bx, by, bz;
+            ex_bwd(op, x.x, y.x, z.x, v.x, c.x, c0, ax, ay, az);
+            ex_bwd(op, x.y, y.y, z.y, v.y, c.y, c0, bx, by, bz);
+            dx = exf2{ax, bx};
+            dy = exf2{ay, by};
+            dz = exf2{az, bz};
+            break;
+        }
+    }
+}
+
 // One expression term.  Strided (element i -> thread i mod nthr) or, with a
 // non-injective gather (T.primary >= 0), per (virtual) segment of the
 // segment-tiled layout (build_segments_ops), the gathered leaves read

@@ -179,6 +179,59 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
         o << " }\n";
     }
     o << "    };\n";
+    // terms over constants, broadcast parameters and data only (no vector
+    // parameter leaves, so no gradient writes whose order could change) also
+    // get a paired element: two elements' nodes in packed FP32 (eval.h
+    // ex2_fwd / ex2_bwd, bit-identical per component), sums taken in element
+    // order
+    bool pairs = !seg;
+    for (int k = 0; k < nn; ++k)
+        if (N[k].op == MC_EX_LEAF && (N[k].prim || N[k].leaf.kind == MC_OP_PVEC ||
+                                      N[k].leaf.kind == MC_OP_GATHER))
+            pairs = false;
+    if (pairs) {
+        std::string params2;
+        for (int k = 0; k < nn; ++k)
+            if (N[k].op == MC_EX_LEAF && N[k].leaf.kind == MC_OP_DATA)
+                params2 += ", exf2 d" + std::to_string(k);
+        o << "    auto element2 = [&](" << (params2.empty() ? std::string() : params2.substr(2))
+          << ") {\n";
+        auto arg2 = [&](int a) { return a >= 0 ? "v" + std::to_string(a) : std::string("z2"); };
+        o << "      const exf2 z2 = {0.0f, 0.0f};\n      (void)z2;\n";
+        for (int k = 0; k < nn; ++k) {
+            const DevExprNode& d = N[k];
+            o << "      const exf2 v" << k << " = ";
+            if (d.op == MC_EX_LEAF) {
+                const int kind = d.leaf.kind;
+                if (kind == MC_OP_CONST) o << "exf2{c" << k << ", c" << k << "}";
+                else if (kind == MC_OP_PSCALAR) o << "exf2{qv" << k << ", qv" << k << "}";
+                else o << "d" << k;
+            } else {
+                o << "ex2_fwd(" << d.op << ", " << arg2(d.a) << ", " << arg2(d.b) << ", " << arg2(d.c)
+                  << ", c" << k << ")";
+            }
+            o << ";\n";
+        }
+        o << "      if (pass == 0) { const exf2 wv = w * v" << nn - 1
+          << "; lp_acc += wv.x; lp_acc += wv.y; }\n"
+          << "      if constexpr (VALUE_ONLY) return;\n";
+        for (int k = 0; k < nn; ++k) o << "      exf2 a" << k << " = {-0.0f, -0.0f};\n";
+        o << "      a" << nn - 1 << " = exf2{w, w};\n";
+        for (int k = nn - 1; k >= 0; --k) {
+            const DevExprNode& d = N[k];
+            if (d.op == MC_EX_LEAF) {
+                if (is_part(k)) o << "      p" << k << " += a" << k << ".x; p" << k << " += a" << k << ".y;\n";
+                continue;
+            }
+            o << "      { exf2 dx, dy, dz; ex2_bwd(" << d.op << ", " << arg2(d.a) << ", " << arg2(d.b)
+              << ", " << arg2(d.c) << ", v" << k << ", a" << k << ", c" << k << ", dx, dy, dz);\n"
+              << "        a" << d.a << " += dx;";
+            if (d.b >= 0) o << " a" << d.b << " += dy;";
+            if (d.c >= 0) o << " a" << d.c << " += dz;";
+            o << " }\n";
+        }
+        o << "    };\n";
+    }
     if (!seg) {
         // four elements per trip, their loads first (the element order, and
         // so every sum, is the strided loop's).  (Prefetching the next trip's
@@ -209,7 +262,24 @@ void gen_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N) {
                 }
                 decl[u] = names;
             }
-            for (int u = 0; u < 4; ++u) o << "      element(e" << u << ", 0" << decl[u] << ");\n";
+            if (pairs) {
+                // decl[u] = ", t<u>_0, t<u>_1, ...": pair the loads of elements 2h, 2h + 1
+                for (int h = 0; h < 2; ++h) {
+                    std::string a = decl[2 * h], b = decl[2 * h + 1], call;
+                    size_t pa = 0, pb = 0;
+                    while ((pa = a.find(", ", pa)) != std::string::npos) {
+                        pb = b.find(", ", pb);
+                        const size_t na = a.find(", ", pa + 2), nb = b.find(", ", pb + 2);
+                        call += ", exf2{" + a.substr(pa + 2, na == std::string::npos ? std::string::npos : na - pa - 2) +
+                                ", " + b.substr(pb + 2, nb == std::string::npos ? std::string::npos : nb - pb - 2) + "}";
+                        pa += 2;
+                        pb += 2;
+                    }
+                    o << "      element2(" << (call.empty() ? std::string() : call.substr(2)) << ");\n";
+                }
+            } else {
+                for (int u = 0; u < 4; ++u) o << "      element(e" << u << ", 0" << decl[u] << ");\n";
+            }
         }
         o << "    }\n"
           << "    for (; i < T.n; i += st) element(i, 0" << args_at("i") << ");\n";
