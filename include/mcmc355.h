@@ -177,8 +177,12 @@ typedef enum {
     MC_EX_NORMAL_LP      = 15,  /* Normal(b, c).log_prob(a)  normal.py:49-56 */
     MC_EX_HALFNORMAL_LP  = 16,  /* HalfNormal(c).log_prob(a) halfnormal.py:43-63 */
     MC_EX_EXPONENTIAL_LP = 17,  /* Exponential(c).log_prob(a) exponential.py:48-71 */
-    MC_EX_WHERE   = 18   /* a != 0 ? b : c, a a CONST / DATA leaf (mx.where  */
+    MC_EX_WHERE   = 18,  /* a != 0 ? b : c, a a CONST / DATA leaf (mx.where  */
                          /* over a data mask; no cotangent through a)        */
+    MC_EX_GAMMA_LP = 19, /* Gamma(b, c).log_prob(a)  gamma.py:48-88: gammaln */
+                         /* (b) at the current value, no cotangent through it */
+    MC_EX_BETA_LP  = 20  /* Beta(b, c).log_prob(a)   beta.py:45-91: log B(b, */
+                         /* c) at the current values, no cotangent through it */
 } mc_expr_op;
 
 typedef struct mc_expr_node {

@@ -66,9 +66,19 @@ class TraceError(TypeError):
 
 
 _UNSUPPORTED = (
-    "the MI355X tape supports log densities built from Normal / HalfNormal "
-    "terms (summed with mx.sum, +, -, scalar *) whose arguments are parameters, "
-    "parameter slices / integer gathers, data arrays or constants")
+    "the MI355X tape supports log densities built from Normal / HalfNormal / "
+    "Exponential / Gamma / Beta terms and elementwise mx expressions (summed "
+    "with mx.sum / mx.mean, +, -, scalar *) whose arguments are parameters, "
+    "parameter slices / integer gathers, data arrays, constants or elementwise "
+    "expressions of them")
+
+
+def _compare_error(what):
+    def f(self, *a, **k):
+        raise TraceError(f"comparison of {what(self)} (x < y, x > 0: a Python branch or "
+                         "mask on a parameter value cannot be traced; masks must be data): "
+                         + _UNSUPPORTED)
+    return f
 
 
 # ---------------------------------------------------------------------------
@@ -214,7 +224,7 @@ class Param:
     def __abs__(self):
         return Expr.unary(_lib.MC_EX_ABS, self)
 
-    __lt__ = __le__ = __gt__ = __ge__ = _unsupported
+    __lt__ = __le__ = __gt__ = __ge__ = _compare_error(lambda p: f"traced parameter '{p.name}'")
 
     def __float__(self):
         raise TraceError(f"float() of traced parameter '{self.name}' (a Python branch on a "
@@ -356,10 +366,11 @@ class Affine:
     def __abs__(self):
         return Expr.unary(_lib.MC_EX_ABS, self)
 
-    def _unsupported(self, *a, **k):
-        raise TraceError("this operation on a traced parameter expression: " + _UNSUPPORTED)
+    def __getitem__(self, item):
+        raise TraceError("indexing a traced parameter expression ((a + b * x)[i]: index the "
+                         "parameter or the data before the arithmetic): " + _UNSUPPORTED)
 
-    __getitem__ = __lt__ = __le__ = __gt__ = __ge__ = _unsupported
+    __lt__ = __le__ = __gt__ = __ge__ = _compare_error(lambda e: "a traced parameter expression")
 
     def __float__(self):
         raise TraceError("float() of a traced parameter expression: " + _UNSUPPORTED)
@@ -414,8 +425,10 @@ class Expr:
         if isinstance(x, Expr):
             return x
         if isinstance(x, LogProbExpr):
-            raise TraceError("a log density inside a parameter expression (only + / - / scalar * "
-                             "combine log densities): " + _UNSUPPORTED)
+            raise TraceError("a log density inside a parameter expression or as a distribution "
+                             "argument (only + / - / scalar * / mx.sum / mx.mean combine log "
+                             "densities, and mx.sum / mx.mean of a parameter expression is read "
+                             "as a log density): " + _UNSUPPORTED)
         if isinstance(x, Param):
             if x.xf:
                 raw = Param(x.name, x.offset, x.base_shape, x.view, 0)
@@ -500,10 +513,11 @@ class Expr:
     def __abs__(self):
         return Expr.unary(_lib.MC_EX_ABS, self)
 
-    def _unsupported(self, *a, **k):
-        raise TraceError("this operation on a traced expression: " + _UNSUPPORTED)
+    def __getitem__(self, item):
+        raise TraceError("indexing a traced expression (expr[i]: index the parameter or the "
+                         "data before the arithmetic): " + _UNSUPPORTED)
 
-    __getitem__ = __lt__ = __le__ = __gt__ = __ge__ = _unsupported
+    __lt__ = __le__ = __gt__ = __ge__ = _compare_error(lambda e: "a traced expression")
 
     def __float__(self):
         raise TraceError("float() of a traced expression (a Python branch on a parameter value "
@@ -529,17 +543,19 @@ def expr_term(root: Expr) -> "LogProbExpr":
 
 
 _EXPR_DIST = {"Normal": _lib.MC_EX_NORMAL_LP, "HalfNormal": _lib.MC_EX_HALFNORMAL_LP,
-              "Exponential": _lib.MC_EX_EXPONENTIAL_LP}
+              "Exponential": _lib.MC_EX_EXPONENTIAL_LP, "Gamma": _lib.MC_EX_GAMMA_LP,
+              "Beta": _lib.MC_EX_BETA_LP}
 
 
 def dist_expr(dist_name: str, value, loc, scale) -> "LogProbExpr":
-    """Distribution.log_prob over expression arguments (MC_EX_*_LP node)."""
+    """Distribution.log_prob over expression arguments (MC_EX_*_LP node;
+    Gamma / Beta: loc and scale are the shapes alpha, beta)."""
     op = _EXPR_DIST.get(dist_name)
     if op is None:
-        raise TraceError(f"{dist_name} with parameter-expression arguments (only Normal, "
-                         "HalfNormal and Exponential take them): " + _UNSUPPORTED)
+        raise TraceError(f"{dist_name} with parameter-expression arguments (Normal, HalfNormal, "
+                         "Exponential, Gamma and Beta take them): " + _UNSUPPORTED)
     ev, es = Expr.of(value), Expr.of(scale)
-    if op == _lib.MC_EX_NORMAL_LP:
+    if op in (_lib.MC_EX_NORMAL_LP, _lib.MC_EX_GAMMA_LP, _lib.MC_EX_BETA_LP):
         el = Expr.of(loc)
         root = Expr(op, [ev, el, es], shape=_bshape(dist_name, [ev.shape, el.shape, es.shape]))
     else:
@@ -693,10 +709,48 @@ class LogProbExpr:
 
     __rmul__ = __mul__
 
-    def sum(self, axis=None):
-        if axis not in (None, 0) or (axis == 0 and len(self.shape) > 1):
-            raise TraceError("only full reductions of a log density are supported")
-        return LogProbExpr(list(self.terms), self.const, ())
+    def _reduced(self, axis, keepdims):
+        """The shape after summing `axis` (None, an int or a tuple; negative
+        axes count from the end), and the number of elements summed into each
+        entry."""
+        nd = len(self.shape)
+        if axis is None:
+            axes = tuple(range(nd))
+        else:
+            axes = tuple(axis) if isinstance(axis, (tuple, list)) else (axis,)
+            norm = []
+            for a in axes:
+                a = int(a)
+                if not -nd <= a < nd:
+                    raise TraceError(f"axis {a} out of range for a log density of shape "
+                                     f"{self.shape}")
+                norm.append(a % nd)
+            if len(set(norm)) != len(norm):
+                raise TraceError(f"repeated axis in {axes}")
+            axes = tuple(norm)
+        shape = tuple((1 if keepdims else None) if i in axes else d
+                      for i, d in enumerate(self.shape))
+        count = int(np.prod([self.shape[i] for i in axes])) if axes else 1
+        return tuple(d for d in shape if d is not None), count
+
+    def sum(self, axis=None, keepdims=False):
+        """mx.sum of a log density: over every axis the scalar the sampler
+        needs; over some axes a smaller log density whose later use must stay
+        linear (sums, + / -, scalar weights) — the terms are unchanged, only
+        the shape they are summed into (the total is the same)."""
+        shape, _ = self._reduced(axis, keepdims)
+        return LogProbExpr(list(self.terms), self.const, shape)
+
+    def mean(self, axis=None, keepdims=False):
+        """mx.mean of a log density: its sum over `axis` times the f32
+        reciprocal of the element count (MLX's mean, mx.sum(x) * (1 / n))."""
+        shape, count = self._reduced(axis, keepdims)
+        r = float(np.float32(1.0) / np.float32(count))
+        return LogProbExpr(list(self.terms), self.const, shape) * r
+
+    def __getitem__(self, item):
+        raise TraceError("indexing a log density (lp[i]: per-element log densities are summed "
+                         "whole, or over an axis with mx.sum(lp, axis=k)): " + _UNSUPPORTED)
 
     def __float__(self):
         raise TraceError("float() of a traced log density: " + _UNSUPPORTED)
@@ -747,10 +801,12 @@ def _scaled(t: Term, c: float) -> Term:
 
 def _scalar_const(x) -> float:
     if isinstance(x, (Param, LogProbExpr, Affine, Expr)):
-        raise TraceError(_UNSUPPORTED)
+        raise TraceError("a log density times a traced value (lp * theta, lp * lp: log "
+                         "densities combine linearly, with constant weights): " + _UNSUPPORTED)
     arr = np.asarray(x)
     if arr.dtype == object or arr.size != 1:
-        raise TraceError("only scalar constants can be combined with a log density")
+        raise TraceError("a log density times a non-scalar constant (per-element weights: "
+                         "only scalar constants combine with a log density)")
     return float(arr.reshape(()))
 
 

@@ -42,20 +42,32 @@ def array(x, dtype=None):
     return a.astype(np.float32)
 
 
-def sum(x, axis=None, keepdims=False):  # noqa: A001 - mirrors mx.sum
+def _as_log_density(x):
+    """A traced value summed into a log density: itself, or a parameter
+    expression (`mx.sum(log_x)`, the Jacobian of a vector reparameterisation)
+    as identity terms, or an expression term when it is more general."""
     if isinstance(x, _trace.LogProbExpr):
-        return x.sum(axis)
+        return x
     if isinstance(x, (_trace.Param, _trace.Affine)):
-        # a parameter expression summed into a log density (`mx.sum(log_x)`,
-        # the Jacobian of a vector reparameterisation): identity terms, or an
-        # expression term when the sum is of a more general expression
         try:
-            return _trace.identity_expr(x).sum(axis)
+            return _trace.identity_expr(x)
         except _trace.TraceError:
-            return _trace.expr_term(_trace.Expr.of(x)).sum(axis)
-    if isinstance(x, _trace.Expr):
-        return _trace.expr_term(x).sum(axis)
+            return _trace.expr_term(_trace.Expr.of(x))
+    return _trace.expr_term(x)
+
+
+def sum(x, axis=None, keepdims=False):  # noqa: A001 - mirrors mx.sum
+    if isinstance(x, (_trace.LogProbExpr, _trace.Param, _trace.Affine, _trace.Expr)):
+        return _as_log_density(x).sum(axis, keepdims)
     return np.sum(np.asarray(x), axis=axis, keepdims=keepdims)
+
+
+def mean(x, axis=None, keepdims=False):
+    """mx.mean: of a log density (or a parameter expression summed into one)
+    its sum times 1 / n; of concrete arrays the NumPy value."""
+    if isinstance(x, (_trace.LogProbExpr, _trace.Param, _trace.Affine, _trace.Expr)):
+        return _as_log_density(x).mean(axis, keepdims)
+    return np.mean(np.asarray(_trace._to_numpy(x)), axis=axis, keepdims=keepdims)
 
 
 def _concrete(name, fn):
@@ -132,7 +144,6 @@ add = _binary("add", _trace._lib.MC_EX_ADD, np.add)
 subtract = _binary("subtract", _trace._lib.MC_EX_SUB, np.subtract)
 multiply = _binary("multiply", _trace._lib.MC_EX_MUL, np.multiply)
 divide = _binary("divide", _trace._lib.MC_EX_DIV, np.divide)
-mean = _concrete("mean", np.mean)
 std = _concrete("std", np.std)
 var = _concrete("var", np.var)
 median = _concrete("median", np.median)

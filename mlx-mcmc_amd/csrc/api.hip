@@ -1341,7 +1341,7 @@ static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, 
         d.c = s.c;
         d.leaf.kind = MC_OP_NONE;
         d.leaf.slot = -1;
-        if (s.op < MC_EX_LEAF || s.op > MC_EX_WHERE)
+        if (s.op < MC_EX_LEAF || s.op > MC_EX_BETA_LP)
             return fail(MC_ERR_INVALID, "term %d node %d: unknown op %d", t, k, s.op);
         if (s.op == MC_EX_LEAF) {
             const mc_operand& o = s.leaf;
@@ -1398,7 +1398,7 @@ static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, 
             case MC_EX_ADD: case MC_EX_SUB: case MC_EX_MUL: case MC_EX_DIV: case MC_EX_POW:
                 ub = true;
                 break;
-            case MC_EX_NORMAL_LP: case MC_EX_WHERE:
+            case MC_EX_NORMAL_LP: case MC_EX_WHERE: case MC_EX_GAMMA_LP: case MC_EX_BETA_LP:
                 ub = uc = true;
                 break;
             case MC_EX_HALFNORMAL_LP: case MC_EX_EXPONENTIAL_LP:

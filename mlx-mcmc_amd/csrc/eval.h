@@ -919,6 +919,41 @@ MC_DEV ElemOut ex_exponential(float v, float r, float logr) {
     return o;
 }
 
+// Gamma(a, b).log_prob(v) and Beta(a, b).log_prob(v) nodes (elem_gamma /
+// elem_beta's operations, divisions and logs through ex_div / ex_log): the
+// gammaln normaliser is the reference's host scipy value of the current
+// float32 shapes — float64 lgamma rounded once — and carries no cotangent
+// (gamma.py:48-59, beta.py:45-57), so the shape cotangents are log b + log v
+// and log v / log(1 - v).  Outside the support: -inf, no cotangents (where).
+MC_DEV float ex_gamma_lp(float v, float a, float b) {
+    if (!(v > 0.0f)) return -__builtin_inff();
+    const float lga = (float)lgamma((double)a);
+    return ((a * ex_log(b) - lga) + (a - 1.0f) * ex_log(v)) - b * v;
+}
+MC_DEV void ex_gamma_grad(float v, float a, float b, float& dv, float& da, float& db) {
+    if (!(v > 0.0f)) {
+        dv = da = db = 0.0f;
+        return;
+    }
+    dv = ex_div(a - 1.0f, v) - b;
+    da = ex_log(b) + ex_log(v);
+    db = ex_div(a, b) - v;
+}
+MC_DEV float ex_beta_lp(float v, float a, float b) {
+    if (!(v > 0.0f && v < 1.0f)) return -__builtin_inff();
+    const float lbeta = (float)(lgamma((double)a) + lgamma((double)b) - lgamma((double)a + (double)b));
+    return ((a - 1.0f) * ex_log(v) + (b - 1.0f) * ex_log(1.0f - v)) - lbeta;
+}
+MC_DEV void ex_beta_grad(float v, float a, float b, float& dv, float& da, float& db) {
+    if (!(v > 0.0f && v < 1.0f)) {
+        dv = da = db = 0.0f;
+        return;
+    }
+    dv = ex_div(a - 1.0f, v) - ex_div(b - 1.0f, 1.0f - v);
+    da = ex_log(v);
+    db = ex_log(1.0f - v);
+}
+
 // Forward value of a non-leaf node (x, y, z: its argument values; c0: the
 // distribution nodes' f32 normaliser, as elem_normal / elem_halfnormal).
 // Divisions go through ex_div, exp / log / log1p through ex_exp / ex_log /
@@ -943,6 +978,8 @@ MC_DEV float ex_fwd(int op, float x, float y, float z, float c0) {
         case MC_EX_HALFNORMAL_LP: return ex_halfnormal(c0, x, z, ex_log(z)).lp;
         case MC_EX_EXPONENTIAL_LP: return ex_exponential(x, z, ex_log(z)).lp;
         case MC_EX_WHERE: return x != 0.0f ? y : z;
+        case MC_EX_GAMMA_LP: return ex_gamma_lp(x, y, z);
+        case MC_EX_BETA_LP: return ex_beta_lp(x, y, z);
         default: return 0.0f;
     }
 }
@@ -995,6 +1032,16 @@ MC_DEV void ex_bwd(int op, float x, float y, float z, float v, float c, float c0
             if (x != 0.0f) dy = c;
             else dz = c;
             break;
+        case MC_EX_GAMMA_LP:
+        case MC_EX_BETA_LP: {
+            float gv, ga, gb;
+            if (op == MC_EX_GAMMA_LP) ex_gamma_grad(x, y, z, gv, ga, gb);
+            else ex_beta_grad(x, y, z, gv, ga, gb);
+            dx = c * gv;
+            dy = c * ga;
+            dz = c * gb;
+            break;
+        }
         default: break;
     }
 }

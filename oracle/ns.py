@@ -41,9 +41,18 @@ def array(x, dtype=None):
     return _t(x)
 
 
-def sum(x, axis=None):  # noqa: A001
+def sum(x, axis=None, keepdims=False):  # noqa: A001
     x = _t(x)
-    return torch.sum(x) if axis is None else torch.sum(x, dim=axis)
+    return torch.sum(x) if axis is None else torch.sum(x, dim=axis, keepdim=keepdims)
+
+
+def mean(x, axis=None, keepdims=False):
+    """MLX's mean: the sum times the f32 reciprocal of the count."""
+    x = _t(x)
+    n = x.numel() if axis is None else int(np.prod([x.shape[a] for a in
+                                                     (axis if isinstance(axis, (tuple, list)) else (axis,))]))
+    r = float(np.float32(1.0) / np.float32(n))
+    return (torch.sum(x) if axis is None else torch.sum(x, dim=axis, keepdim=keepdims)) * r
 
 
 def log(x):

@@ -23,6 +23,8 @@ MODELS = {"two_predictor": W.two_predictor_regression,
           "logistic": W.logistic_regression,
           "varying_slopes": W.varying_slopes,
           "cauchy": W.cauchy_location,
+          "gamma_beta": W.gamma_beta_regression,
+          "axis_reductions": W.axis_reductions,
           "tiny_scalar": tiny_scalar}
 
 

@@ -5,7 +5,8 @@ Models beyond the fused terms — two predictors with a log-scale noise, a
 Bernoulli likelihood through mx.sigmoid / mx.log1p, varying slopes (two
 gathers through one non-injective index: the segmented expression path), a
 hand-written Cauchy likelihood using every other op (sqrt, square, log1p,
-tanh, abs, power, where) — run on the GPU tape and are checked against the CPU
+tanh, abs, power, where), Gamma and Beta likelihoods with expression shapes —
+run on the GPU tape and are checked against the CPU
 oracle, whose gradients are torch autograd over the same user model.
 
 Bars: tape log p within 2e-6 * 50 of max(1, |lp|) (f32 summation order and
@@ -38,6 +39,8 @@ MODELS = {"two_predictor": W.two_predictor_regression,
           "logistic": W.logistic_regression,
           "varying_slopes": W.varying_slopes,
           "cauchy": W.cauchy_location,
+          "gamma_beta": W.gamma_beta_regression,
+          "axis_reductions": W.axis_reductions,
           "tiny_scalar": tiny_scalar}
 POSITIVE = ("sigma", "v")
 
@@ -95,6 +98,11 @@ def test_expr_nan_and_support(gpu):
     ("two_predictor", {"a": 0.5, "b1": 1.2, "b2": -0.8, "log_sigma": -0.5}, 0.004, 0),
     ("logistic", {"a": -0.3, "b": 1.1}, 0.05, 1),
     ("cauchy", {"mu": 2.0, "v": 0.5, "w": 0.1}, 0.02, 2),
+    # (the shapes' gradients omit digamma, as the reference's host gammaln
+    # does: the trajectories follow a biased force, so only small steps accept)
+    ("gamma_beta", {"b0": 0.3, "b1": 0.2, "c0": 0.0, "c1": 0.5, "log_a": 1.0, "log_phi": 2.0},
+     1e-4, 4),
+    ("axis_reductions", {"a": 0.4, "b": 1.4, "log_sigma": -0.4}, 0.01, 5),
 ])
 def test_expr_hmc_trace_matches_oracle(gpu, model, start, eps, seed):
     import mlx_mcmc_amd as m

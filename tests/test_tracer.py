@@ -1,4 +1,6 @@
 """Host logic without a GPU: tracing user models into the term program."""
+import re
+
 import numpy as np
 import pytest
 
@@ -132,19 +134,35 @@ def test_affine_forms(expr, want):
 X3 = np.arange(3, dtype=np.float32)
 
 
-@pytest.mark.parametrize("bad", [
-    lambda p: m.Gamma(p["x"] * 2.0, 1.0).log_prob(p["x"]),      # Gamma over an expression
-    lambda p: m.Normal(0, 1).log_prob(p["x"]) if p["x"] > 0 else 0,  # Python branch
-    lambda p: m.Normal(0, 1).log_prob(p["v"]),                  # unsummed vector
-    lambda p: m.Normal(0, 1).log_prob(p["x"]) + p["v"],         # unsummed vector identity
-    lambda p: mx.sum(m.Normal(0, 1).log_prob((p["v"] * 2.0)[0])),  # indexing an expression
-    lambda p: mx.sum(mx.where(p["v"] > 0, p["v"], 0.0)),         # a traced where condition
-    lambda p: m.Normal(0, 1).log_prob(p["x"]) * p["x"],         # a density times a parameter
-    lambda p: mx.sum(m.Normal(p["v"] * X3, 1.0).log_prob(np.zeros(4, np.float32))),  # shapes
-    lambda p: mx.sum(_deep(p["v"], 40)),                        # more than 32 nodes
+# Constructs that still raise: each error names its construct
+@pytest.mark.parametrize("bad,names", [
+    (lambda p: m.Normal(0, 1).log_prob(p["x"]) if p["x"] > 0 else 0,     # Python branch
+     "comparison of traced parameter 'x'"),
+    (lambda p: m.Normal(0, 1).log_prob(p["v"]), "must return a scalar"),  # unsummed vector
+    (lambda p: m.Normal(0, 1).log_prob(p["x"]) + p["v"],                   # unsummed identity
+     "adding a scalar log density to an unsummed vector one"),
+    (lambda p: mx.sum(m.Normal(0, 1).log_prob((p["v"] * 2.0)[0])),         # indexing an expr
+     "indexing a traced"),
+    (lambda p: mx.sum(mx.where(p["v"] > 0, p["v"], 0.0)),                   # traced where mask
+     "comparison of traced parameter 'v'"),
+    (lambda p: m.Normal(0, 1).log_prob(p["x"]) * p["x"],                   # density x parameter
+     "a log density times a traced value"),
+    (lambda p: mx.sum(m.Normal(0, 1).log_prob(p["v"]) * X3),               # per-element weights
+     "a log density times a non-scalar constant"),
+    (lambda p: mx.sum(m.Normal(p["v"] * X3, 1.0).log_prob(np.zeros(4, np.float32))),
+     "cannot broadcast shapes"),
+    (lambda p: mx.sum(_deep(p["v"], 40)), "nodes (at most 32)"),           # too deep
+    (lambda p: mx.exp(mx.sum(m.Normal(0, 1).log_prob(p["v"]))),            # logsumexp-like
+     "a log density inside a parameter expression"),
+    (lambda p: mx.sum(m.Normal(0, 1).log_prob(p["v"])[1:]), "indexing a log density"),
+    (lambda p: mx.sum(m.Normal(0, 1).log_prob(p["v"]), axis=2), "axis 2 out of range"),
+    (lambda p: m.Normal(mx.mean(p["v"]), 1.0).log_prob(p["x"]),            # a reduction as a value
+     "as a distribution argument"),
+    (lambda p: float(m.Normal(0, 1).log_prob(p["x"])), "float() of a traced log density"),
+    (lambda p: mx.std(p["v"]), "mx.std of a traced value"),
 ])
-def test_unsupported_models_raise(bad):
-    with pytest.raises(_trace.TraceError):
+def test_unsupported_models_raise(bad, names):
+    with pytest.raises(_trace.TraceError, match=re.escape(names)):
         _trace.trace(bad, {"x": 1.0, "v": np.zeros(3, np.float32)})
 
 
@@ -174,6 +192,11 @@ def _deep(x, k):
     lambda p: mx.sum(mx.log1p(mx.sigmoid(p["v"]) ** 2.0)),
     lambda p: m.HalfNormal(mx.exp(p["x"]) + 1.0).log_prob(p["y"] * p["y"]),
     lambda p: m.Exponential(p["x"] * p["y"]).log_prob(mx.exp(p["y"])),
+    lambda p: m.Gamma(p["x"] * 2.0, 1.0).log_prob(p["y"]),      # Gamma over expressions
+    lambda p: mx.sum(m.Gamma(mx.exp(p["x"]), p["y"] * X3 + 1.0).log_prob(X3 + 1.0)),
+    lambda p: mx.sum(m.Beta(p["y"] * 4.0, (1.0 - p["y"]) * 4.0).log_prob(X3 * 0.2 + 0.1)),
+    lambda p: m.Beta(2.0, 3.0).log_prob(mx.sigmoid(p["x"])),     # Beta of an expression
+    lambda p: mx.mean(-0.5 * mx.square(p["v"] - X3)),             # mx.mean of an expression
 ])
 def test_general_expressions_trace(good):
     tm = _trace.trace(good, {"x": 1.0, "y": 0.5, "v": np.zeros(3, np.float32)})
@@ -305,3 +328,33 @@ def test_transformed_operands_and_identity_terms():
         return lp
     tm = _trace.trace(two_scales, {"mu": 0.0, "s": 0.0})
     assert [(t.n, t.scale.transform) for t in tm.terms] == [(3, 0), (3, _lib.MC_XF_EXP)]
+
+
+def test_axis_sums_and_means():
+    """mx.sum(lp, axis=k) keeps the terms and reduces the shape; mx.mean is
+    the sum times f32(1 / n); a row-summed log density summed again (or G
+    times its mean) is the whole; the traced model W.axis_reductions (run on
+    the GPU against autograd in tests/test_gpu_expr.py) carries those
+    weights."""
+    Y = np.ones((4, 5), np.float32)
+
+    def f(axis_ops):
+        def lp(p):
+            per = m.Normal(p["x"], 1.0).log_prob(Y)
+            return axis_ops(per)
+        return _trace.trace(lp, {"x": 1.0})
+
+    tm = f(lambda per: mx.sum(mx.sum(per, axis=1)))
+    assert [t.weight for t in tm.terms] == [1.0] and tm.terms[0].n == 20
+    tm = f(lambda per: mx.sum(mx.sum(per, axis=-1, keepdims=True)))
+    assert [t.weight for t in tm.terms] == [1.0]
+    tm = f(lambda per: mx.mean(per))
+    assert tm.terms[0].weight == pytest.approx(float(np.float32(1) / np.float32(20)))
+    tm = f(lambda per: mx.sum(mx.mean(per, axis=0)))
+    assert tm.terms[0].weight == pytest.approx(0.25)
+    tm = f(lambda per: mx.mean(per, axis=(0, 1)))
+    assert tm.terms[0].weight == pytest.approx(0.05)
+    tm = _trace.trace(*W.axis_reductions(W.ns_product()))
+    assert sorted(round(t.weight, 6) for t in tm.terms if t.n == 400) == [0.00125, 1.0]
+    with pytest.raises(_trace.TraceError, match="must return a scalar"):
+        f(lambda per: mx.sum(per, axis=1))

@@ -18,7 +18,7 @@ def ns_product():
     import mlx_mcmc_amd.core as mx
 
     return SimpleNamespace(Normal=m.Normal, HalfNormal=m.HalfNormal, Exponential=m.Exponential,
-                           Gamma=m.Gamma, Beta=m.Beta, sum=mx.sum, array=mx.array,
+                           Gamma=m.Gamma, Beta=m.Beta, sum=mx.sum, mean=mx.mean, array=mx.array,
                            exp=mx.exp, log=mx.log, sqrt=mx.sqrt, square=mx.square,
                            power=mx.power, abs=mx.abs, log1p=mx.log1p, tanh=mx.tanh,
                            sigmoid=mx.sigmoid, where=mx.where, pi=mx.pi, name="product")
@@ -28,7 +28,7 @@ def ns_oracle():
     from oracle import ns
 
     return SimpleNamespace(Normal=ns.Normal, HalfNormal=ns.HalfNormal, Exponential=ns.Exponential,
-                           Gamma=ns.Gamma, Beta=ns.Beta, sum=ns.sum, array=ns.array,
+                           Gamma=ns.Gamma, Beta=ns.Beta, sum=ns.sum, mean=ns.mean, array=ns.array,
                            exp=ns.exp, log=ns.log, sqrt=ns.sqrt, square=ns.square,
                            power=ns.power, abs=ns.abs, log1p=ns.log1p, tanh=ns.tanh,
                            sigmoid=ns.sigmoid, where=ns.where, pi=ns.pi, name="oracle")
@@ -385,6 +385,71 @@ def varying_slopes(ns, G=16, N=1600):
     return log_prob, {"mu_a": np.float32(1.0), "mu_b": np.float32(-0.5),
                       "sigma": np.float32(0.5), "alpha": np.ones(G, np.float32),
                       "beta": np.zeros(G, np.float32)}
+
+
+def gamma_beta_data(n=300, seed=9):
+    rng = np.random.default_rng(seed)
+    x = rng.normal(0.0, 1.0, n).astype(np.float32)
+    mu = np.exp(0.4 + 0.3 * x)
+    y = rng.gamma(3.0, mu / 3.0).astype(np.float32)             # shape 3, mean mu
+    p = 1.0 / (1.0 + np.exp(-(-0.2 + 0.8 * x)))
+    z = np.clip(rng.beta(8.0 * p, 8.0 * (1.0 - p)), 1e-4, 1 - 1e-4).astype(np.float32)
+    return x, y, z
+
+
+def gamma_beta_regression(ns, n=300):
+    """Gamma and Beta likelihoods with parameter-expression arguments
+    (gamma.py:48-88, beta.py:45-91): a Gamma GLM y ~ Gamma(a, a / mu),
+    mu = exp(b0 + b1 x), and a Beta regression z ~ Beta(phi p, phi (1 - p)),
+    p = sigmoid(c0 + c1 x) — the shapes are expressions, so their gammaln
+    normalisers are evaluated per element at the current values, and (as in
+    the reference, whose gammaln is a host scipy constant) the shape
+    gradients carry no digamma term."""
+    x, y, z = gamma_beta_data(n)
+
+    def log_prob(params):
+        b0, b1, c0, c1 = params["b0"], params["b1"], params["c0"], params["c1"]
+        la, lphi = params["log_a"], params["log_phi"]
+        lp = ns.Normal(0, 2).log_prob(b0) + ns.Normal(0, 2).log_prob(b1)
+        lp = lp + ns.Normal(0, 2).log_prob(c0) + ns.Normal(0, 2).log_prob(c1)
+        lp = lp + ns.Normal(1, 1).log_prob(la) + ns.Normal(2, 1).log_prob(lphi)
+        a = ns.exp(la)
+        mu = ns.exp(b0 + b1 * ns.array(x))
+        lp = lp + ns.sum(ns.Gamma(a, a / mu).log_prob(ns.array(y)))
+        phi = ns.exp(lphi)
+        p = ns.sigmoid(c0 + c1 * ns.array(x))
+        return lp + ns.sum(ns.Beta(phi * p, phi * (1.0 - p)).log_prob(ns.array(z)))
+
+    return log_prob, {"b0": np.float32(0.3), "b1": np.float32(0.2), "c0": np.float32(0.0),
+                      "c1": np.float32(0.5), "log_a": np.float32(1.0),
+                      "log_phi": np.float32(2.0)}
+
+
+def axis_reduction_data(G=8, K=50, seed=10):
+    rng = np.random.default_rng(seed)
+    x = rng.normal(0.0, 1.0, (G, K)).astype(np.float32)
+    y = (0.5 + 1.5 * x + rng.normal(0.0, 0.6, (G, K))).astype(np.float32)
+    return x, y
+
+
+def axis_reductions(ns, G=8, K=50):
+    """Log densities reduced over axes and averaged (mx.sum(lp, axis=1),
+    mx.mean): a 2-D regression likelihood written out (an expression term)
+    summed per row, then G times the mean of the rows (the total), and a
+    fused 2-D term averaged over both axes with a weight."""
+    x, y = axis_reduction_data(G, K)
+
+    def log_prob(params):
+        a, b, ls = params["a"], params["b"], params["log_sigma"]
+        lp = ns.Normal(0, 5).log_prob(a) + ns.Normal(0, 5).log_prob(b)
+        lp = lp + ns.Normal(0, 1).log_prob(ls)
+        z = (ns.array(y) - (a + b * ns.array(x))) / ns.exp(ls)
+        per = -0.5 * ns.square(z) - ls - 0.9189385                              # (G, K)
+        rows = ns.sum(per, axis=1)                                               # (G,)
+        lp = lp + float(G) * ns.mean(rows)
+        return lp + 0.5 * ns.mean(ns.Normal(a, 2.0).log_prob(ns.array(y)), axis=(0, 1))
+
+    return log_prob, {"a": np.float32(0.4), "b": np.float32(1.4), "log_sigma": np.float32(-0.4)}
 
 
 def cauchy_location(ns, n=200, seed=8):
