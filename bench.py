@@ -585,7 +585,8 @@ def main_nuts(args):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     sc = chains.scalars()
-    leaves = int(np.sum(sc["n_grad"].astype(np.int64) - g0))
+    per = sc["n_grad"].astype(np.int64) - g0
+    leaves = int(np.sum(per))
     full = [a.elapsed_time(b) for (a, b), (_, n) in zip(ev, timed) if n == B] or \
            [a.elapsed_time(b) for (a, b), _ in zip(ev, timed)]
     launch_ms = float(np.mean(full)) if K else float("nan")
@@ -624,6 +625,13 @@ def main_nuts(args):
                          + " (SURVEY 8d unit: one leaf)")},
             "leaves": leaves_all, "leaves_rank0": leaves, "mean_tree_depth": float(np.mean(sc["depth_sum"] / np.maximum(
                 sc["n_total"], 1))),
+            # a launch lasts as long as its longest chain: the per-chain
+            # leaves of the timed window (rank 0), and mean / max — the share
+            # of the chain slots that stay busy (scripts/probe_nuts_balance.py)
+            "chain_balance": {"min": int(per.min()), "median": float(np.median(per)),
+                              "max": int(per.max()), "mean_over_max": float(per.mean() / max(per.max(), 1)),
+                              "step_size_min": float(np.min(sc["step_size"])),
+                              "step_size_median": float(np.median(sc["step_size"]))},
             "accept_stat_mean": float(np.mean(sc["alpha_sum"]) / max(Wm + K, 1)),
             "step_size": float(np.mean(sc["step_size"])),
             "clock_warm_ms": args.clock_warm_ms,
