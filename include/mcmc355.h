@@ -416,6 +416,16 @@ int mc_debug_nuts_variant(int variant);
  * -1 restores the default (MC_NUTS_SLICED from the environment, else on).
  * Trees agree up to fp32 summation order.                                  */
 int mc_debug_nuts_sliced(int on);
+/* Diagnostic of the same-XCD exchange (csrc/sliced.h xcd_handshake): the
+ * exchange kernels' workgroups since `ws` was last cleared that found every
+ * slice of their exchange group on one XCD (their records then stay in that
+ * XCD's L2) and those that did not.                                         */
+int mc_debug_workspace_xcd(const void* ws, int32_t* local, int32_t* remote);
+/* The same-XCD exchange (L2-resident records, csrc/host.h xcd_round_robin):
+ * 0 off, 1 on where the device's workgroup placement allows it, -1 the
+ * default (MC_XCD_LOCAL from the environment, else on).  Results are the same
+ * bits either way.                                                          */
+int mc_debug_xcd_local(int on);
 /* The sliced Metropolis-Hastings kernel k_mh_sl (csrc/mh_sliced.h):
  * mc_program_mh_sliced is 1 when mc_mh_run runs it (a program sliced onto
  * the fast-form lane layout: one wave per chain and slice, one log-p record

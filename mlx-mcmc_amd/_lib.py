@@ -216,6 +216,9 @@ SIGNATURES = [
     ("mc_debug_lanes_fast", ctypes.c_int, [ctypes.c_int]),
     ("mc_debug_nuts_variant", ctypes.c_int, [ctypes.c_int]),
     ("mc_debug_nuts_sliced", ctypes.c_int, [ctypes.c_int]),
+    ("mc_debug_xcd_local", ctypes.c_int, [ctypes.c_int]),
+    ("mc_debug_workspace_xcd", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
+                                              ctypes.POINTER(ctypes.c_int32)]),
     ("mc_debug_mh_sliced", ctypes.c_int, [ctypes.c_int]),
     ("mc_program_mh_sliced", ctypes.c_int32, [_VP]),
     ("mc_debug_expr_jit", ctypes.c_int, [ctypes.c_int]),
@@ -271,7 +274,15 @@ def load():
             "(or __graft_entry__.build()) — there is no CPU fallback")
     lib = ctypes.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            # (a test / diagnostic hook an older build lacks — A/B runs of
+            # other builds, scripts/ab_lib.py; every product entry point is
+            # required)
+            if name.startswith("mc_debug_"):
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     if lib.mc_abi_version() != 2:

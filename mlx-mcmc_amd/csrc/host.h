@@ -351,6 +351,19 @@ inline int check_cfg(const mc_program* p, const mc_run_config* cfg, void* state)
     return MC_OK;
 }
 
+// ---- same-XCD exchange (sliced.h granule_store_xcd) ---------------------------
+// The exchange kernels place a block's S slices at workgroups w with equal
+// w % 8 when the grid allows (grid % 8 == 0 and (grid / 8) % S == 0); with
+// the device dealing workgroups round-robin over its 8 XCDs (observed on
+// MI355X, not an architectural guarantee) those share an XCD, and records
+// can stay in its L2.  xcd_round_robin(grid) checks that dealing once per
+// (device, grid size): a probe launch records each workgroup's XCC id and
+// every residue class mod 8 must name one XCD.  MC_XCD_LOCAL=0 in the
+// environment (or mc_debug_xcd_local(0)) turns the L2-resident exchange off.
+// The kernels check the placement again before their first publish.
+inline int g_xcd_local = -1;  // mc_debug_xcd_local; -1: MC_XCD_LOCAL from the environment
+bool xcd_round_robin(int64_t grid, int S);  // (run_hmc.hip)
+
 // ---- sliced launches ---------------------------------------------------------
 inline int device_cus() {
     static int cached[64] = {0};

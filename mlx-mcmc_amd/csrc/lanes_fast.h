@@ -251,7 +251,10 @@ MC_DEV LfTerms lf_terms(const MC_CONST LrTerm* tt, int nsweep, int ndirect) {
 }
 
 // NSH: shared slots of the record (FORM >= 0: lf_nroles(FORM)).
-template <int RS, int NSH, int NW, bool X1, int FORM>
+// XL: the host found every exchange group's workgroups on one XCD
+// (host.h xcd_round_robin): records are published with L2-resident stores
+// (sliced.h granule_store_xcd), after an in-kernel check of the placement.
+template <int RS, int NSH, int NW, bool X1, int FORM, bool XL = false>
 __global__ void __launch_bounds__(64 * NW)
 k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scalars* scal,
          float* st_q, float* st_g, float* samples, TraceDev tr, unsigned long long* xch,
@@ -499,6 +502,18 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         else if (pr < NV + 2) need_k0 |= 1u << ps;
         else need_k1 |= 1u << ps;
     }
+    // XL: check that the block's slices share an XCD (sliced.h xcd_announce /
+    // xcd_agree) before the first publish.  The check's granules: granule 15
+    // of each slice's parity-0 line of wave 0 (record pairs use 0 .. NPAIR - 1
+    // < 15); its tag ebase + 1 is never 0, the value of a freshly cleared
+    // line (the steps' tags start there too, on the record granules).  Its
+    // loads are issued here and completed after the first sweep.
+    constexpr bool xchk = XL && !X1;
+    unsigned long long* const xslots = xch + ((int64_t)grp * (NB / 2)) * S * 16 + 15;
+    XcdPoll xpoll = {0ull};
+    if (xchk && cfg.iter_count > 0)
+        xpoll = xcd_announce(xslots, S, slice, ebase + 1, wave == 0 && j == 0);
+    static_assert(NPAIR <= 15, "granule 15 of a record line is the XCD handshake's");
     const int64_t it_end = cfg.iter_begin + cfg.iter_count;
     for (int64_t it = cfg.iter_begin; it < it_end && ok; ++it) {
         MC_STAMP_DECL
@@ -629,6 +644,22 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         drift_private(false);
         drift_shared(false);
         sweep(M1, M2);
+        if (xchk && it == cfg.iter_begin) {  // (before the launch's first publish)
+            const bool same = xcd_agree(xpoll, xslots, S, ebase + 1, ok);
+            // (diagnostic: workgroups that found their block on one XCD / not,
+            // in the status area's words 8 / 9; mc_debug_workspace_xcd)
+            if (ok && wave == 0 && j == 0)
+                __hip_atomic_fetch_add(status + (same ? 8 : 9), 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (!ok || !same) {
+                // a timeout (1), or a placement the L2-resident stores would
+                // not reach (2): nothing published, the block's chains keep
+                // their state, the launch reports it (mc_workspace_status)
+                __hip_atomic_store(status, ok ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = false;
+                break;
+            }
+        }
         // one leapfrog step at the point q(l + 1), compiled per kind so that the
         // intermediate steps carry none of the first / last steps' work (K0 /
         // K1 items, log p) nor its uniform branches and their live masks:
@@ -811,7 +842,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 float pv = xr[0];
 #pragma unroll
                 for (int x = 1; x < 2 * NRS; ++x) pv = (x == pub_x) ? xr[x] : pv;
-                if (pub_mid) granule_store(gline[par] + pub_off, epoch, pv);
+                if (pub_mid) granule_put(gline[par] + pub_off, epoch, pv, XL);
             } else if (!X1) {
                 // one store instruction: the record pairs, and the K items on the
                 // first / last step (lanes 2, 3 of rows 0 / 1)
@@ -835,7 +866,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                         pv = c ? k1w[1] : k1w[0];
                     }
                 }
-                if (pp >= 0) granule_store(gline[par] + slice * 16 + pp, epoch, pv);
+                if (pp >= 0) granule_put(gline[par] + slice * 16 + pp, epoch, pv, XL);
             }
             MC_STAMP(2);
             // the sweep issues at a higher wave priority than the latency-bound

@@ -12,6 +12,60 @@ extern "C" int mc_debug_exchange_fault(int on) {
     return MC_OK;
 }
 
+// Workgroups of the exchange kernels since the workspace was last cleared
+// whose exchange group was found on one XCD (L2-resident publishes) / not
+// (sliced.h xcd_handshake): the status area's words 8 and 9.
+extern "C" int mc_debug_workspace_xcd(const void* ws, int32_t* local, int32_t* remote) {
+    if (!ws) return fail(MC_ERR_INVALID, "workspace is NULL");
+    int32_t w[2] = {0, 0};
+    MC_HIP_TRY(hipMemcpy(w, (const int32_t*)ws + 8, sizeof(w), hipMemcpyDeviceToHost));
+    if (local) *local = w[0];
+    if (remote) *remote = w[1];
+    return MC_OK;
+}
+
+// host.h: the device deals workgroups round-robin over its XCDs (probe)
+static __global__ void k_xcc_probe(uint32_t* out) {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    if (threadIdx.x == 0) out[blockIdx.x] = x;
+}
+bool xcd_round_robin(int64_t grid, int S) {
+    if (g_xcd_local < 0) {
+        const char* e = std::getenv("MC_XCD_LOCAL");
+        g_xcd_local = (e && e[0] == '0') ? 0 : 1;
+    }
+    if (g_xcd_local == 0 || S < 2 || grid % 8 != 0 || (grid / 8) % S != 0) return false;
+    static std::mutex mu;
+    static std::map<std::pair<int, int64_t>, bool> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto key = std::make_pair(dev, grid);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    bool ok = false;
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, grid * sizeof(uint32_t)) == hipSuccess) {
+        std::vector<uint32_t> h((size_t)grid, 0xFFFFFFFFu);
+        hipLaunchKernelGGL(k_xcc_probe, dim3((unsigned)grid), dim3(64), 0, 0, d);
+        if (hipGetLastError() == hipSuccess &&
+            hipMemcpy(h.data(), d, grid * sizeof(uint32_t), hipMemcpyDeviceToHost) == hipSuccess) {
+            ok = true;
+            for (int64_t b = 8; b < grid && ok; ++b) ok = h[b] == h[b % 8];
+        }
+        (void)hipFree(d);
+    }
+    (void)hipGetLastError();
+    cache[key] = ok;
+    return ok;
+}
+
+extern "C" int mc_debug_xcd_local(int on) {
+    g_xcd_local = on < 0 ? -1 : (on ? 1 : 0);
+    return MC_OK;
+}
+
 extern "C" int mc_debug_lanes_fast(int on) {
     g_lanes_fast = on ? 1 : 0;
     return MC_OK;
@@ -77,6 +131,11 @@ extern "C" int mc_workspace_status(const mc_program* p, const void* ws, int64_t 
     MC_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     if (v != 0) {
         ws_forget(ws);  // the next launch clears the status word and the granules
+        if (v == 2)
+            return fail(MC_ERR_UNSUPPORTED,
+                        "sliced launch: an exchange group's workgroups were not on one XCD, which "
+                        "its L2-resident records need (the device's workgroup placement differs "
+                        "from its probe); MC_XCD_LOCAL=0 turns that exchange off");
         return fail(MC_ERR_TIMEOUT, "sliced HMC: a cross-workgroup exchange timed out");
     }
     return MC_OK;

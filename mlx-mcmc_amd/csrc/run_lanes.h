@@ -9,11 +9,18 @@ inline int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
     const bool fast = p->lr.fast && lanes_fast_enabled();
     auto kern = fast ? k_hmc_lf<RS, NSH, NW, X1, -1> : k_hmc_lr<RS, NSH, NW, X1>;
+    auto kern_xl = kern;  // the same with L2-resident records (host.h xcd_round_robin)
     const bool forms = lanes_forms_enabled();
     if constexpr (NSH == 3) {  // the compile-time forms (one instantiation each)
         constexpr int HIER = LF_SW | LF_SWS | LF_DIR | LF_DM | LF_DS;
-        if (fast && forms && p->lr.form == HIER) kern = k_hmc_lf<RS, lf_nroles(HIER), NW, X1, HIER>;
-        if (fast && forms && p->lr.form == LF_DIR) kern = k_hmc_lf<RS, lf_nroles(LF_DIR), NW, X1, LF_DIR>;
+        if (fast && forms && p->lr.form == HIER) {
+            kern = k_hmc_lf<RS, lf_nroles(HIER), NW, X1, HIER>;
+            kern_xl = X1 ? kern : k_hmc_lf<RS, lf_nroles(HIER), NW, X1, HIER, true>;
+        }
+        if (fast && forms && p->lr.form == LF_DIR) {
+            kern = k_hmc_lf<RS, lf_nroles(LF_DIR), NW, X1, LF_DIR>;
+            kern_xl = X1 ? kern : k_hmc_lf<RS, lf_nroles(LF_DIR), NW, X1, LF_DIR, true>;
+        }
     }
     int64_t qo, go;
     mc_state_offsets(p, cfg->num_chains, &qo, &go);
@@ -24,6 +31,7 @@ inline int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
     const LrCtx ctx = lrctx_of(p);
     const size_t lds = (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm);
     MC_HIP_TRY(allow_lds(kern, lds));
+    if (kern_xl != kern) MC_HIP_TRY(allow_lds(kern_xl, lds));
     const int64_t C = cfg->num_chains;
     constexpr int NB = 2 * NW;
     const int64_t groups = (C + NB - 1) / NB;
@@ -55,8 +63,9 @@ inline int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
                                (float*)(b + go), samples, trace_of(tr), xch, status, base);
             MC_HIP_TRY(hipGetLastError());
         } else {
+            const bool xl = kern_xl != kern && xcd_round_robin(grid, p->lr.S);
             const hipError_t e = launch_exchange(
-                kern, grid, 64 * NW, lds, st, ctx, A, g0 * NB, ng,
+                xl ? kern_xl : kern, grid, 64 * NW, lds, st, ctx, A, g0 * NB, ng,
                 (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples, trace_of(tr),
                 xch, status, base);
             MC_HIP_TRY(e);
