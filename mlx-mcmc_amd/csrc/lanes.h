@@ -877,7 +877,10 @@ MC_DEV void wave_sum8(const float (&v)[8], float (&out)[8]) {
 // ---------------------------------------------------------------------------
 // X1: a program of one slice (an unsliced program): no exchange — a
 // compile-time flag so the sliced variants keep their code and registers.
-template <int RS, int NSH, int NW, bool X1>
+// XL: records published with L2-resident stores (sliced.h
+// granule_store_xcd: the block's slices share an XCD), the placement checked
+// at the launch's first iteration.
+template <int RS, int NSH, int NW, bool X1, bool XL = false>
 __global__ void __launch_bounds__(64 * NW)
 k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scalars* scal,
          float* st_q, float* st_g, float* samples, TraceDev tr, unsigned long long* xch,
@@ -1014,7 +1017,27 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     }
     const bool poll_lane = (j & 15) < S;
     const int64_t it_end = cfg.iter_begin + cfg.iter_count;
+    // XL: the block's slices share an XCD (sliced.h xcd_announce / xcd_agree;
+    // slots: granule 15 of each slice's parity-0 line of wave 0 — the record
+    // pairs are granules 0 .. NPAIR - 1 < 15)
+    static_assert(NPAIR <= 15, "granule 15 of a record line is the XCD check's");
+    constexpr bool xchk = XL && !X1;
+    unsigned long long* const xslots = xch + ((int64_t)grp * (NB / 2)) * S * 16 + 15;
+    XcdPoll xpoll = {0ull};
+    if (xchk && cfg.iter_count > 0)
+        xpoll = xcd_announce(xslots, S, slice, ebase + 1, wave == 0 && j == 0);
     for (int64_t it = cfg.iter_begin; it < it_end && ok; ++it) {
+        if (xchk && it == cfg.iter_begin) {  // (before the launch's first publish)
+            const bool same = xcd_agree(xpoll, xslots, S, ebase + 1, ok);
+            if (ok && wave == 0 && j == 0)
+                __hip_atomic_fetch_add(status + (same ? 8 : 9), 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (!ok || !same) {  // nothing published: the chains keep their state
+                __hip_atomic_store(status, ok ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = false;
+                break;
+            }
+        }
         MC_STAMP_DECL
         const bool warm = it < cfg.num_warmup;
         float h[2], e[2];
@@ -1168,7 +1191,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 float v = rec[0];
 #pragma unroll
                 for (int x = 1; x < NPAIR; ++x) v = (j == x) ? rec[x] : v;
-                granule_store(par ? gpub[1] : gpub[0], epoch, v);
+                granule_put(par ? gpub[1] : gpub[0], epoch, v, XL);
             }
             MC_STAMP(2);
             // the sweep at a higher wave priority than the latency-bound rest of

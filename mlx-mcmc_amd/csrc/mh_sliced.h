@@ -58,7 +58,9 @@ MC_DEV float msl_sumsq(const float* xv, int len, int lmin4, int lmax, float th) 
     return b[0] + b[1];
 }
 
-template <int RS, int NSH, int NW, int OCC, int FORM>
+// XL: records published with L2-resident stores (the same-XCD exchange of
+// k_hmc_lf, sliced.h granule_store_xcd), the placement checked first.
+template <int RS, int NSH, int NW, int OCC, int FORM, bool XL = false>
 __global__ void __launch_bounds__(64 * NW, OCC)
 k_mh_sl(LrCtx P, RunArgs A, float scale, int64_t chain_base, int64_t n_groups,
         mc_chain_scalars* scal, float* st_q, float* samples, TraceDev tr, unsigned long long* xch,
@@ -187,7 +189,25 @@ k_mh_sl(LrCtx P, RunArgs A, float scale, int64_t chain_base, int64_t n_groups,
     uint32_t epoch = ebase;
     bool ok = true;
     const int64_t it_end = cfg.iter_begin + cfg.iter_count;
+    // XL: the block's slices share an XCD (sliced.h xcd_announce / xcd_agree;
+    // slots: granule 15 of each slice's parity-0 line of wave 0 — the record
+    // is granule 0)
+    unsigned long long* const xslots = xch + ((int64_t)grp * NW) * S * kMslLine + 15;
+    XcdPoll xpoll = {0ull};
+    if (XL && cfg.iter_count > 0)
+        xpoll = xcd_announce(xslots, S, slice, ebase + 1, wave == 0 && j == 0);
     for (int64_t it = cfg.iter_begin; it < it_end; ++it) {
+        if (XL && it == cfg.iter_begin) {  // (before the launch's first publish)
+            const bool same = xcd_agree(xpoll, xslots, S, ebase + 1, ok);
+            if (ok && wave == 0 && j == 0)
+                __hip_atomic_fetch_add(status + (same ? 8 : 9), 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (!ok || !same) {  // nothing published: the chains keep their state
+                __hip_atomic_store(status, ok ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = false;
+                break;
+            }
+        }
         // Gaussian random walk (metropolis.py:66-74): parameter g takes normal
         // g % 4 of Philox block g / 4 (k_mh's mapping)
         auto normal_of = [&](int gi) {
@@ -243,7 +263,7 @@ k_mh_sl(LrCtx P, RunArgs A, float scale, int64_t chain_base, int64_t n_groups,
         const float wt = wave_sum(lpp);
         ++epoch;
         const int par = epoch & 1;
-        if (j == 0) granule_store(gline0 + par * pstride + slice * kMslLine, epoch, wt);
+        if (j == 0) granule_put(gline0 + par * pstride + slice * kMslLine, epoch, wt, XL);
         unsigned long long* const gpp = gp0 + par * pstride;
         unsigned long long y = poll_lane ? granule_load(gpp) : 0ull;
         // the accept draw while the records travel (metropolis.py:81-88)

@@ -140,7 +140,10 @@ MC_DEV float nsl_colsum(float t, int cw) {
 
 // NSH: shared slots of the record (FORM >= 0: lf_nroles(FORM)); NW chains
 // (waves) per workgroup; OCC the waves per SIMD the register budget allows.
-template <int RS, int NSH, int NW, int OCC, int FORM>
+// XL: records published with L2-resident stores (the same-XCD exchange of
+// k_hmc_lf, sliced.h granule_store_xcd), the placement checked at the
+// launch's first iteration.
+template <int RS, int NSH, int NW, int OCC, int FORM, bool XL = false>
 __global__ void __launch_bounds__(64 * NW, OCC)
 k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scalars* scal,
           float* st_q, float* st_g, float* samples, TraceDev tr, unsigned long long* xch,
@@ -316,9 +319,26 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
     uint32_t epoch = ebase;  // tags continue across launches (api.hip ws_reserve)
     bool ok = true;
     MC_STAMP_INIT
+    // XL: the block's slices share an XCD (sliced.h xcd_announce / xcd_agree;
+    // slots: the check area after both parities' lines, 16 granules apart)
+    unsigned long long* const xslots = xch + 2 * pstride + (int64_t)grp * S * 16;
+    XcdPoll xpoll = {0ull};
+    if (XL && cfg.iter_count > 0)
+        xpoll = xcd_announce(xslots, S, slice, ebase + 1, wave == 0 && j == 0);
 
     for (int64_t it = cfg.iter_begin; it < it_end && ok; ++it) {
         MC_STAMP_DECL
+        if (XL && it == cfg.iter_begin) {  // (before the launch's first publish)
+            const bool same = xcd_agree(xpoll, xslots, S, ebase + 1, ok);
+            if (ok && wave == 0 && j == 0)
+                __hip_atomic_fetch_add(status + (same ? 8 : 9), 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (!ok || !same) {  // nothing published: the chains keep their state
+                __hip_atomic_store(status, ok ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = false;
+                break;
+            }
+        }
         if (it == cfg.num_warmup) {  // nuts.py:318-319, 328-330
             if (cfg.adapt_step_size) eps = sc.step_size_bar;
             sc.warmup_accept = sc.n_accept;
@@ -601,7 +621,7 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                     float pv = xr[0];
 #pragma unroll
                     for (int x = 1; x < 8; ++x) pv = (x == col16) ? xr[x] : pv;
-                    granule_store(gline0 + par * pstride + slice * kNslLine + pub_pair, epoch, pv);
+                    granule_put(gline0 + par * pstride + slice * kNslLine + pub_pair, epoch, pv, XL);
                 }
                 // park the leaf's private part: candidate pool (q, g) and, when
                 // it opens a subtree, that subtree's first leaf (q, r)

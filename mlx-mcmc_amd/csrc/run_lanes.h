@@ -9,7 +9,9 @@ inline int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* st
                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
     const bool fast = p->lr.fast && lanes_fast_enabled();
     auto kern = fast ? k_hmc_lf<RS, NSH, NW, X1, -1> : k_hmc_lr<RS, NSH, NW, X1>;
-    auto kern_xl = kern;  // the same with L2-resident records (host.h xcd_round_robin)
+    // the same with L2-resident records (host.h xcd_round_robin): the generic
+    // kernel and the compile-time forms (the run-time form keeps sc1 records)
+    auto kern_xl = (fast || X1) ? kern : k_hmc_lr<RS, NSH, NW, X1, true>;
     const bool forms = lanes_forms_enabled();
     if constexpr (NSH == 3) {  // the compile-time forms (one instantiation each)
         constexpr int HIER = LF_SW | LF_SWS | LF_DIR | LF_DM | LF_DS;

@@ -6,6 +6,9 @@ template <int RS, int NSH, int OCC, int FORM>
 static int launch_mh_sl(const mc_program* p, const mc_run_config* cfg, float scale, void* state,
                         float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
     auto kern = k_mh_sl<RS, NSH, kNslWaves, OCC, FORM>;
+    // the compile-time form also with L2-resident records (host.h xcd_round_robin)
+    auto kern_xl = kern;
+    if constexpr (FORM >= 0) kern_xl = k_mh_sl<RS, NSH, kNslWaves, OCC, FORM, true>;
     int64_t qo, go;
     mc_state_offsets(p, cfg->num_chains, &qo, &go);
     char* b = (char*)state;
@@ -15,6 +18,7 @@ static int launch_mh_sl(const mc_program* p, const mc_run_config* cfg, float sca
     const LrCtx ctx = lrctx_of(p);
     const size_t lds = (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm);
     MC_HIP_TRY(allow_lds(kern, lds));
+    if (kern_xl != kern) MC_HIP_TRY(allow_lds(kern_xl, lds));
     const int64_t C = cfg->num_chains;
     const int64_t groups = (C + kNslWaves - 1) / kNslWaves;
     const int S = p->lr.S;
@@ -36,7 +40,9 @@ static int launch_mh_sl(const mc_program* p, const mc_run_config* cfg, float sca
     ws_mark_status(ws);
     for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
         const int64_t ng = std::min(gpl, groups - g0);
-        const hipError_t e = launch_exchange(kern, ng * S, 64 * kNslWaves, lds, st, ctx, A, scale,
+        const bool xl = kern_xl != kern && xcd_round_robin(ng * S, S);
+        const hipError_t e = launch_exchange(xl ? kern_xl : kern, ng * S, 64 * kNslWaves, lds, st,
+                                             ctx, A, scale,
                                              g0 * kNslWaves, ng, (mc_chain_scalars*)b,
                                              (float*)(b + qo), samples, trace_of(tr), xch, status,
                                              base);

@@ -31,16 +31,21 @@ inline int nuts_sl_occ(const mc_program* p) {
     return p->lr.S > 8 ? 4 : 2;
 }
 
-// exchange lines (both parities) for every chain block of C chains
+// exchange lines (both parities) for every chain block of C chains, then the
+// XCD check's slots (16 granules per slice of a block)
 inline int64_t nuts_sl_line_bytes(const mc_program* p, int64_t C) {
     const int64_t groups = (C + kNslWaves - 1) / kNslWaves;
-    return 2 * groups * kNslWaves * (int64_t)p->lr.S * kNslLine * 8;
+    return 2 * groups * kNslWaves * (int64_t)p->lr.S * kNslLine * 8 +
+           groups * (int64_t)p->lr.S * 16 * 8;
 }
 
 template <int RS, int NSH, int OCC, int FORM>
 inline int launch_nuts_sl(const mc_program* p, const mc_run_config* cfg, void* state,
                           float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
     auto kern = k_nuts_sl<RS, NSH, kNslWaves, OCC, FORM>;
+    // the compile-time form also with L2-resident records (host.h xcd_round_robin)
+    auto kern_xl = kern;
+    if constexpr (FORM >= 0) kern_xl = k_nuts_sl<RS, NSH, kNslWaves, OCC, FORM, true>;
     int64_t qo, go;
     mc_state_offsets(p, cfg->num_chains, &qo, &go);
     char* b = (char*)state;
@@ -51,6 +56,7 @@ inline int launch_nuts_sl(const mc_program* p, const mc_run_config* cfg, void* s
     const int maxj = cfg->max_tree_depth;
     const size_t lds = nuts_sl_lds_bytes(p, maxj);
     MC_HIP_TRY(allow_lds(kern, lds));
+    if (kern_xl != kern) MC_HIP_TRY(allow_lds(kern_xl, lds));
     const int64_t C = cfg->num_chains;
     const int64_t groups = (C + kNslWaves - 1) / kNslWaves;
     const int S = p->lr.S;
@@ -74,8 +80,9 @@ inline int launch_nuts_sl(const mc_program* p, const mc_run_config* cfg, void* s
     ws_mark_status(ws);
     for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
         const int64_t ng = std::min(gpl, groups - g0);
+        const bool xl = kern_xl != kern && xcd_round_robin(ng * S, S);
         const hipError_t e = launch_exchange(
-            kern, ng * S, 64 * kNslWaves, lds, st, ctx, A, g0 * kNslWaves, ng,
+            xl ? kern_xl : kern, ng * S, 64 * kNslWaves, lds, st, ctx, A, g0 * kNslWaves, ng,
             (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples, trace_of(tr), xch,
             pool, status, base);
         MC_HIP_TRY(e);
