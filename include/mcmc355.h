@@ -416,10 +416,10 @@ int mc_debug_nuts_variant(int variant);
  * -1 restores the default (MC_NUTS_SLICED from the environment, else on).
  * Trees agree up to fp32 summation order.                                  */
 int mc_debug_nuts_sliced(int on);
-/* Diagnostic of the same-XCD exchange (csrc/sliced.h xcd_handshake): the
- * exchange kernels' workgroups since `ws` was last cleared that found every
- * slice of their exchange group on one XCD (their records then stay in that
- * XCD's L2) and those that did not.                                         */
+/* Diagnostic of the same-XCD exchange (csrc/sliced.h xcd_announce /
+ * xcd_agree): the exchange groups (chain blocks, counted by their slice 0)
+ * launched on `ws` since it was last cleared whose slices all sat on one XCD
+ * (their records then stay in that XCD's L2), and those whose did not.      */
 int mc_debug_workspace_xcd(const void* ws, int32_t* local, int32_t* remote);
 /* The same-XCD exchange (L2-resident records, csrc/host.h xcd_round_robin):
  * 0 off, 1 on where the device's workgroup placement allows it, -1 the

@@ -1029,7 +1029,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     for (int64_t it = cfg.iter_begin; it < it_end && ok; ++it) {
         if (xchk && it == cfg.iter_begin) {  // (before the launch's first publish)
             const bool same = xcd_agree(xpoll, xslots, S, ebase + 1, ok);
-            if (ok && wave == 0 && j == 0)
+            if (ok && slice == 0 && wave == 0 && j == 0)  // (one per block)
                 __hip_atomic_fetch_add(status + (same ? 8 : 9), 1, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             if (!ok || !same) {  // nothing published: the chains keep their state

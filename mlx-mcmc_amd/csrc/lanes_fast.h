@@ -646,9 +646,9 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         sweep(M1, M2);
         if (xchk && it == cfg.iter_begin) {  // (before the launch's first publish)
             const bool same = xcd_agree(xpoll, xslots, S, ebase + 1, ok);
-            // (diagnostic: workgroups that found their block on one XCD / not,
+            // (diagnostic: blocks found on one XCD / not, counted by slice 0,
             // in the status area's words 8 / 9; mc_debug_workspace_xcd)
-            if (ok && wave == 0 && j == 0)
+            if (ok && slice == 0 && wave == 0 && j == 0)  // (one per block)
                 __hip_atomic_fetch_add(status + (same ? 8 : 9), 1, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             if (!ok || !same) {

@@ -330,7 +330,7 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
         MC_STAMP_DECL
         if (XL && it == cfg.iter_begin) {  // (before the launch's first publish)
             const bool same = xcd_agree(xpoll, xslots, S, ebase + 1, ok);
-            if (ok && wave == 0 && j == 0)
+            if (ok && slice == 0 && wave == 0 && j == 0)  // (one per block)
                 __hip_atomic_fetch_add(status + (same ? 8 : 9), 1, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             if (!ok || !same) {  // nothing published: the chains keep their state

@@ -12,9 +12,9 @@ extern "C" int mc_debug_exchange_fault(int on) {
     return MC_OK;
 }
 
-// Workgroups of the exchange kernels since the workspace was last cleared
-// whose exchange group was found on one XCD (L2-resident publishes) / not
-// (sliced.h xcd_handshake): the status area's words 8 and 9.
+// Exchange groups (blocks, counted by slice 0) launched on the workspace
+// since it was last cleared that were found on one XCD (L2-resident
+// publishes) / not (sliced.h xcd_agree): the status area's words 8 and 9.
 extern "C" int mc_debug_workspace_xcd(const void* ws, int32_t* local, int32_t* remote) {
     if (!ws) return fail(MC_ERR_INVALID, "workspace is NULL");
     int32_t w[2] = {0, 0};

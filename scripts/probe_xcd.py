@@ -1,6 +1,5 @@
-"""How many exchange workgroups found their block's slices on one XCD
-(sliced.h xcd_handshake; mc_debug_workspace_xcd) on the bench shapes, and the
-XCC id per workgroup of a plain grid of the same size (round-robin check)."""
+"""How many exchange groups (chain blocks) found their slices on one XCD
+(sliced.h xcd_agree; mc_debug_workspace_xcd) on the bench shapes."""
 import ctypes
 import os
 import sys
@@ -26,5 +25,5 @@ for shape in ("large", "medium", "small"):
     a, b = ctypes.c_int32(), ctypes.c_int32()
     _lib.check(lib.mc_debug_workspace_xcd(ctypes.c_void_p(cs._ws.data_ptr()), ctypes.byref(a),
                                           ctypes.byref(b)))
-    print(f"{shape}: {prog.num_slices} slices, kernel {prog.slice_kernel}: workgroups local "
+    print(f"{shape}: {prog.num_slices} slices, kernel {prog.slice_kernel}: blocks local "
           f"{a.value}, not local {b.value} (5 launches)", flush=True)
