@@ -214,6 +214,23 @@ def test_nuts_lanes_matches_tape_hierarchical(gpu):
         a, b = post["auto"][0][name], post["tape"][0][name]    # [C, S]
         sa = np.sqrt(a.mean(1).var() / a.shape[0] + b.mean(1).var() / b.shape[0])
         assert abs(a.mean() - b.mean()) < 5 * sa + 1e-3, (name, a.mean(), b.mean(), sa)
+    # the default mode (the reference's f32 slice) as well, on the chains that
+    # keep mixing in both runs: a step size that neither froze huge nor
+    # collapsed, and draws that move (the replicated layout's
+    # default-mode posterior was otherwise unchecked)
+    ea = runs["auto"][2].trace["step_size"][:, -1]
+    eb = runs["tape"][2].trace["step_size"][:, -1]
+    sa_, sb_ = runs["auto"][0], runs["tape"][0]
+    # (which chains freeze depends on the last bits, so each run's mixing
+    # chains are pooled on their own: two samples of the same posterior)
+    ma = [c for c in range(16) if 1e-4 < ea[c] < 1.0 and np.ptp(sa_["mu"][c]) > 0]
+    mb = [c for c in range(16) if 1e-4 < eb[c] < 1.0 and np.ptp(sb_["mu"][c]) > 0]
+    print(f"default mode: {len(ma)} / {len(mb)} of 16 chains mixing (lanes / tape)")
+    assert len(ma) >= 4 and len(mb) >= 4, (ea, eb)
+    for name in ("mu", "tau", "sigma"):
+        a, b = sa_[name][ma], sb_[name][mb]
+        sa = np.sqrt(a.mean(1).var() / a.shape[0] + b.mean(1).var() / b.shape[0])
+        assert abs(a.mean() - b.mean()) < 5 * sa + 1e-3, ("default", name, a.mean(), b.mean(), sa)
 
 
 @pytest.mark.parametrize("model", ["illcond", "eight_schools"])
