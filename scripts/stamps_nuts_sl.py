@@ -24,7 +24,7 @@ import workloads as W  # noqa: E402
 from mlx_mcmc_amd import _engine, _trace  # noqa: E402
 
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-C = 256
+C = int(os.environ.get("CHAINS", "256"))
 fn, init = W.hierarchical(W.ns_product(), *W.SHAPES["large"])
 prog = _trace.compile_model(fn, init, slices=S)
 assert prog.nuts_kernel(10) == "sliced"
