@@ -255,20 +255,23 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     // 2s^2 is the same -(theta - o) / s^2, the squares are equal
                     // bitwise, and the cotangent 0 + -(w (d iv)) never keeps the
                     // sign of a zero d — the same bits as the general form below
+                    // (selects, not a branch per slot: one basic block, so the
+                    // scheduler can interleave it with the leaf's other work)
                     const f2 w = f2s(dd_w), half = f2s(0.5f);
                     f2 lpd = {0.f, 0.f};
 #pragma unroll
                     for (int r = 0; r < RS; ++r) {
-                        if (!dd_on[r]) continue;
                         const f2 th = {R.q[r][0], R.q[r][1]};
                         const f2 other = dd_ko == SK_DATA ? f2s(dd_o[r]) : f2s(dd_cv);
                         const f2 d = th - other;
                         const f2 iv = f2s(dd_iv[r]);
                         const f2 lpt = f2s(dd_c0l[r]) - (half * (d * d)) * iv;
-                        lpd += w * lpt;
+                        const f2 lpn = lpd + w * lpt;
                         const f2 gp = (f2){0.f, 0.f} + -(w * (d * iv));
-                        R.g[r][0] = gp[0];
-                        R.g[r][1] = gp[1];
+                        lpd[0] = dd_on[r] ? lpn[0] : lpd[0];
+                        lpd[1] = dd_on[r] ? lpn[1] : lpd[1];
+                        R.g[r][0] = dd_on[r] ? gp[0] : 0.0f;
+                        R.g[r][1] = dd_on[r] ? gp[1] : 0.0f;
                     }
                     lpp[0] += lpd[0];
                     lpp[1] += lpd[1];
@@ -393,6 +396,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
     const uint32_t chain_id = (uint32_t)(cfg.chain_offset + c);
     const int64_t it_end = cfg.iter_begin + cfg.iter_count;
     int64_t n_grad = 0;
+    const float lp_const = P.lp_const;
 
     for (int64_t it = cfg.iter_begin; it < it_end; ++it) {
         MC_STAMP_DECL
@@ -521,6 +525,25 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
             int pend_idx = 0, pend_n = 0;  // lane l: the parked first half of level l
             const int nleaf = 1 << jd;
             for (int k = 0; k < nleaf; ++k) {
+                // an odd leaf closes the pair (k - 1, k): the level-0 merge's
+                // U-turn test reads leaf k - 1's (q, r), parked one leaf ago —
+                // read ahead here, its LDS latency hidden under the leaf
+                float aq0[RS + 1], ar0[RS + 1];
+                if (k & 1) {
+                    const int s0 = (k == 1) ? jd : ctz_u32((uint32_t)(k - 1));
+#pragma unroll
+                    for (int r = 0; r <= RS; ++r) {
+                        const bool in = r < RS || Dsh > 0;
+                        aq0[r] = in ? *at(0, s0, 0, r) : 0.0f;
+                        ar0[r] = in ? *at(0, s0, 1, r) : 0.0f;
+                    }
+                }
+                // and that merge's draw (scalar Philox: its instructions fill
+                // the leaf's dependency stalls; in the merge it was on the
+                // critical path)
+                uint32_t u0 = 0;
+                if (k & 1) u0 = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_MERGE,
+                                        (uint32_t)jd, (uint32_t)k).x;
                 // leaf: leapfrog_step(theta, r, v*eps) + hamiltonian (nuts.py:160-164)
                 // (both packed halves in one instruction each: the same IEEE
                 // operations as the per-half form)
@@ -560,7 +583,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     }
                     float ws[2] = {lane_lp, k};
                     wave_sum2(ws);
-                    lpl = (ws[0] + post) + P.lp_const;
+                    lpl = (ws[0] + post) + lp_const;
                     Kl = ws[1];
                 } else {
                     lpl = evaluate(nullptr);
@@ -628,14 +651,15 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     }
                     const int pidx = __builtin_amdgcn_readlane(pend_idx, l);
                     const int pn = __builtin_amdgcn_readlane(pend_n, l);
-                    const mc_u32x4 rm = mc_draw(cfg.seed, chain_id, (uint32_t)it,
-                                                MC_RNG_TAG_MERGE, (uint32_t)jd,
-                                                ((uint32_t)l << 20) | (uint32_t)k);
+                    const uint32_t ux =
+                        l == 0 ? u0
+                               : mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_MERGE,
+                                         (uint32_t)jd, ((uint32_t)l << 20) | (uint32_t)k).x;
                     const double den = (double)(pn + cn) > 1.0 ? (double)(pn + cn) : 1.0;
                     // U < cn / den (nuts.py:205) as U * den < cn: exact in f64 (U a
                     // multiple of 2^-24, den < 2^24), the same decision as the
                     // rounded quotient (no representable U lies between the two)
-                    const bool take_second = (double)mc_u01_f32(rm.x) * den < (double)cn;
+                    const bool take_second = (double)mc_u01_f32(ux) * den < (double)cn;
                     if (take_second) {
                         freemask |= (1u << pidx);
                     } else {
@@ -650,8 +674,13 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
 #pragma unroll
                     for (int r = 0; r <= RS; ++r) {
                         const bool in = r < RS || Dsh > 0;
-                        bq[r] = in ? *at(0, slot, 0, r) : 0.0f;
-                        br[r] = in ? *at(0, slot, 1, r) : 0.0f;
+                        if (l == 0) {  // (read ahead at the leaf's start)
+                            bq[r] = aq0[r];
+                            br[r] = ar0[r];
+                        } else {
+                            bq[r] = in ? *at(0, slot, 0, r) : 0.0f;
+                            br[r] = in ? *at(0, slot, 1, r) : 0.0f;
+                        }
                         eq[r] = r < RS ? R.q[r][0] : sh.q;
                         er[r] = r < RS ? R.p[r][0] : sh.p;
                     }
