@@ -434,7 +434,6 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
             const int nleaf = 1 << jd;
             for (int k = 0; k < nleaf; ++k) {
                 MC_STAMP_DECL
-#ifndef MC_AB_NO_RA
                 // an odd leaf's level-0 dots read leaf k - 1's (q, r), parked
                 // one leaf ago: read ahead here, the LDS latency off the path
                 // to the publish (k_nuts_lr's read-ahead)
@@ -447,7 +446,6 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                         ar0[r] = *first_at(s0, 1, r);
                     }
                 }
-#endif
                 // leaf: leapfrog_step(theta, r, v * eps) (nuts.py:160-161)
                 if (spec) {
 #pragma unroll
@@ -584,12 +582,8 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                     const int slot = (k0 == 0) ? jd : ctz_u32((uint32_t)k0);
 #pragma unroll
                     for (int r = 0; r < RS; ++r) {
-#ifndef MC_AB_NO_RA
                         const float bq = l == 0 ? aq0[r] : *first_at(slot, 0, r);
                         const float br = l == 0 ? ar0[r] : *first_at(slot, 1, r);
-#else
-                        const float bq = *first_at(slot, 0, r), br = *first_at(slot, 1, r);
-#endif
                         if (!lead) continue;
                         const float dd = v > 0 ? q[r] - bq : bq - q[r];
                         a += dd * (v > 0 ? br : p[r]);
