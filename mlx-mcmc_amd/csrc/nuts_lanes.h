@@ -335,7 +335,7 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         } else {
             lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp);
         }
-        if (rep > 1) {  // a replicated parameter's gradient: its lanes' partials
+        if (__builtin_expect(rep > 1, 0)) {  // a replicated parameter's gradient: its lanes' partials
 #pragma unroll
             for (int r = 0; r < RS; ++r) grp_sum2(R.g[r][0], R.g[r][1], rep);
         }
