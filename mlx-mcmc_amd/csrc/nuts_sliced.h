@@ -675,9 +675,12 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                             sp_[r] = bp + hh * bg;
                             sq_[r] = bq + ee * sp_[r];
                             M1[r] = M2[r] = 0.0f;
+                            // (4 float4 groups in flight at every occupancy: the
+                            // sweep-ahead is the lone chain's critical path at the
+                            // launch's tail, where its wave is alone on its SIMD)
                             if (len[r] > 0)
-                                nsl_moments<OCC >= 4 ? 2 : 4>(xv[r], len[r], lmin4[r], lmax[r], sq_[r],
-                                                              M1[r], M2[r]);
+                                nsl_moments<4>(xv[r], len[r], lmin4[r], lmax[r], sq_[r], M1[r],
+                                               M2[r]);
                         }
                         spec = true;
                     }
