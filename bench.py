@@ -9,7 +9,7 @@ One *step* = one HMC iteration of every chain (L leapfrog steps, fused
 gradient tape, accept, sample store) inside the persistent sampler kernel,
 which is launched in chunks of --iters-per-launch iterations (default 50).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]     (N > 1: spawns N rank processes)
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
 Warmup W = untimed warmup iterations of the sampler (the reference's step-size
@@ -204,8 +204,14 @@ def cpu_aggregate(G, N, L, step_size, budget_s, nproc):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-    with pool:
+    # close + join (workers exit on their own) rather than the context
+    # manager's terminate(): SIGTERMed workers print abort traces that would
+    # hide a real abort in a profiler log
+    try:
         vals = pool.map(_cpu_worker, [(G, N, L, step_size, budget_s, i) for i in range(nproc)])
+    finally:
+        pool.close()
+        pool.join()
     return float(sum(vals))
 
 
@@ -769,8 +775,90 @@ def main_mh(args):
         dist.destroy_process_group()
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_command(argv):
+    """The command line one spawned rank runs: this script, same arguments."""
+    return [sys.executable, os.path.abspath(__file__)] + list(argv)
+
+
+def spawn_ranks(n, argv, cmd=None, poll_s=0.2):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes
+    (rank r on GPU r, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set per child,
+    the same arguments) and wait for them.  The parent never imports torch or
+    opens the device — every rank initialises HIP itself — so this is the
+    torchrun layout (one process per GPU) by construction.  Rank 0's JSON line
+    reaches stdout directly (the children inherit it; other ranks print no
+    result line).  When a rank fails the others are stopped (they would wait
+    in a collective for it) and the first non-zero status is returned."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), MC_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen(cmd if cmd is not None else rank_command(argv), env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"bench.py: rank {procs.index(p)} exited with status {rc}; stopping the "
+                      f"other ranks", file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+                for q in live:
+                    try:
+                        q.wait(timeout=20)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                live = []
+        time.sleep(poll_s)
+    return status
+
+
+def resolve_world(args):
+    """None when this process runs the bench itself; otherwise the exit status
+    of the launch: `--gpus N > 1` with no WORLD_SIZE spawns N ranks
+    (spawn_ranks); a WORLD_SIZE that disagrees with --gpus is an error (the
+    line would report another GPU count than the one asked for)."""
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}: launch one process per "
+                  f"GPU with the same count (torchrun --nproc-per-node {args.gpus}), or run "
+                  f"without a launcher and let bench.py spawn the ranks", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus > 1:
+        return spawn_ranks(args.gpus, sys.argv[1:])
+    return None
+
+
 def main():
     args = parse()
+    status = resolve_world(args)
+    if status is not None:
+        sys.exit(status)
     if args.workload == "nuts":
         return main_nuts(args)
     if args.workload == "mh":

@@ -393,9 +393,15 @@ int mc_workspace_release(const void* workspace_dev);
 
 /* Test hook for the exchange kernels' timeout path (no reference counterpart):
  * while on != 0, the last workgroup of every sliced HMC launch exits without
- * publishing, so the other slices of its chain block time out; the launch's
- * chains of that block keep their state, mc_workspace_status then reports
- * MC_ERR_TIMEOUT and the next launch on the workspace starts clean.       */
+ * publishing, so the other slices of its chain block time out;
+ * mc_workspace_status then reports MC_ERR_TIMEOUT and the next launch on the
+ * workspace starts clean.  The state of a timed-out chain block is undefined
+ * in general and the caller re-initialises those chains: the HMC and MH
+ * kernels write a chain's state only at launch exit (a stranded block keeps
+ * the state the launch found), but sliced NUTS writes an accepted draw's
+ * private parameters when its tree level completes, and its shared
+ * parameters, log density and scalars at exit (csrc/nuts_sliced.h).  The
+ * hook faults before the first leaf, where every kernel keeps the state.  */
 int mc_debug_exchange_fault(int on);
 /* Test hook: 0 runs the fast-form kernel k_hmc_lf with the term form read at
  * run time (FORM = -1) instead of its compile-time instantiations; 1 restores

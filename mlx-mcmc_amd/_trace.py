@@ -44,10 +44,20 @@ HalfNormal / Exponential whose arguments are such expressions, and any such
 expression summed into the log density — traces to an *expression* term
 (``Expr``, MC_DIST_EXPR): a DAG of f32 elementwise ops evaluated and
 differentiated per element by the chain-per-workgroup kernels (eval.h
-eval_expr), as mx.grad differentiates the reference's MLX graph.  Gamma /
-Beta with expression arguments, indexing an expression, reductions other
-than a full ``mx.sum`` and Python branches on traced values raise
-``TraceError``.
+eval_expr), as mx.grad differentiates the reference's MLX graph.  Gamma and
+Beta take such expressions too (their log densities as expression nodes, with
+no gradient through gammaln, as the reference's distributions/gamma.py:61-88
+and beta.py:59-91).  What raises ``TraceError``, and why:
+
+* a Python branch on a parameter value (``float(theta)``, ``if theta > 0``):
+  the model is traced once, so a branch would freeze one side of it;
+* ``mx.where`` over a traced condition (the mask must be data, core.py);
+* indexing a parameter expression or a log density (``(a + b * x)[i]``,
+  ``lp[i]``): index the parameter or the data before combining them;
+* a log density multiplied by a traced value (``lp * theta``): a term's
+  weight is a constant;
+* reductions other than a full ``mx.sum`` of a log density, multi-dimensional
+  or strided parameter indexing, and expression terms over 32 nodes.
 """
 from __future__ import annotations
 

@@ -17,7 +17,8 @@
 // edges, leaf kinds, passes): leaf offsets, pools, slots and constants are
 // read from the program's node table at run time (scalar loads), so models of
 // the same structure share one code object whatever their data.  Code
-// objects are cached per (source, kernel, options) in the process and on disk
+// objects are cached per (source, kernel, options with the device arch,
+// hiprtc version) in the process and on disk
 // ($MC_JIT_CACHE, else ~/.cache/mcmc355; unwritable: in-process only).
 // MC_EXPR_JIT=0 in the environment (or mc_debug_expr_jit(0)) keeps the
 // interpreter; a failed compilation falls back to it with a kernel note.
@@ -25,7 +26,9 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <fstream>
+#include <thread>
 #include <sstream>
 
 #include "host.h"
@@ -402,16 +405,31 @@ std::string gen_source(const mc_program* p) {
     return o.str();
 }
 
-const char* const kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                             "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize",
-                             "-DMC_JIT=1"};
-constexpr int kNumOpts = (int)(sizeof(kOpts) / sizeof(kOpts[0]));
+// hiprtc options: the device's own architecture (gcnArchName's processor,
+// e.g. "gfx950"), so a library built for another ARCH still compiles for the
+// card it runs on; the arch and hiprtc's version are part of the cache key.
+std::vector<std::string> jit_opts(int dev) {
+    std::string arch = "gfx950";
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.gcnArchName[0]) {
+        arch = prop.gcnArchName;
+        const size_t colon = arch.find(':');
+        if (colon != std::string::npos) arch.resize(colon);
+    }
+    return {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off",
+            "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize", "-DMC_JIT=1"};
+}
 
-uint64_t cache_key(const std::string& src, const std::string& kernel) {
+uint64_t cache_key(const std::string& src, const std::string& kernel,
+                   const std::vector<std::string>& opts) {
     uint64_t h = 1469598103934665603ull;
     h = fnv1a(h, src);
     h = fnv1a(h, kernel);
-    for (int i = 0; i < kNumOpts; ++i) h = fnv1a(h, std::string(kOpts[i]));
+    for (const std::string& o : opts) h = fnv1a(h, o);
+    int major = 0, minor = 0;
+    (void)hiprtcVersion(&major, &minor);
+    const int ver[2] = {major, minor};
+    h = fnv1a(h, ver, sizeof ver);
     for (int i = 0; i < kJitNumHeaders; ++i) {
         h = fnv1a(h, std::string(kJitHeaderNames[i]));
         h = fnv1a(h, std::string(kJitHeaderTexts[i]));
@@ -419,12 +437,18 @@ uint64_t cache_key(const std::string& src, const std::string& kernel) {
     return h;
 }
 
-bool disk_load(uint64_t key, std::string& name, std::string& code) {
+std::string cache_path(uint64_t key) {
     const std::string dir = cache_dir();
-    if (dir.empty()) return false;
+    if (dir.empty()) return "";
     char fn[64];
     std::snprintf(fn, sizeof fn, "/%016llx.co", (unsigned long long)key);
-    std::ifstream f(dir + fn, std::ios::binary);
+    return dir + fn;
+}
+
+bool disk_load(uint64_t key, std::string& name, std::string& code) {
+    const std::string path = cache_path(key);
+    if (path.empty()) return false;
+    std::ifstream f(path, std::ios::binary);
     if (!f) return false;
     uint32_t n = 0;
     if (!f.read((char*)&n, 4) || n == 0 || n > 4096) return false;
@@ -443,10 +467,14 @@ void disk_store(uint64_t key, const std::string& name, const std::string& code) 
     const size_t cut = dir.find_last_of('/');
     if (cut != std::string::npos && cut > 0) (void)mkdir(dir.substr(0, cut).c_str(), 0755);
     (void)mkdir(dir.c_str(), 0755);
-    char fn[96];
-    std::snprintf(fn, sizeof fn, "/%016llx.co", (unsigned long long)key);
-    const std::string path = dir + fn;
-    const std::string tmp = path + ".tmp." + std::to_string((long long)getpid());
+    const std::string path = cache_path(key);
+    // a temp name unique to this write (pid, thread, sequence): two threads
+    // compiling programs of one structure must not interleave into one file
+    static std::atomic<uint64_t> seq{0};
+    const std::string tmp = path + ".tmp." + std::to_string((long long)getpid()) + "." +
+                            std::to_string((unsigned long long)std::hash<std::thread::id>()(
+                                std::this_thread::get_id())) +
+                            "." + std::to_string((unsigned long long)seq.fetch_add(1));
     {
         std::ofstream f(tmp, std::ios::binary);
         if (!f) return;
@@ -464,8 +492,9 @@ void disk_store(uint64_t key, const std::string& name, const std::string& code) 
 
 // Compile `kernel` (a name expression of a template instantiation) with the
 // program's source: (lowered name, code object), or an error message.
-bool compile(const std::string& src, const std::string& kernel, std::string& name,
-             std::string& code, std::string& err) {
+bool compile(const std::string& src, const std::string& kernel,
+             const std::vector<std::string>& opts, std::string& name, std::string& code,
+             std::string& err) {
     const std::string full = src;  // (the name expression instantiates the kernel)
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, full.c_str(), "mc_jit.hip", kJitNumHeaders, kJitHeaderTexts,
@@ -475,7 +504,9 @@ bool compile(const std::string& src, const std::string& kernel, std::string& nam
     }
     const std::string expr = "&" + kernel;
     hiprtcAddNameExpression(prog, expr.c_str());
-    const hiprtcResult r = hiprtcCompileProgram(prog, kNumOpts, kOpts);
+    std::vector<const char*> argv;
+    for (const std::string& o : opts) argv.push_back(o.c_str());
+    const hiprtcResult r = hiprtcCompileProgram(prog, (int)argv.size(), argv.data());
     if (r != HIPRTC_SUCCESS) {
         size_t n = 0;
         hiprtcGetProgramLogSize(prog, &n);
@@ -543,44 +574,66 @@ int jit_function(const mc_program* p, const std::string& kernel, hipFunction_t* 
         s->src = gen_source(p);
         s->have_src = true;
     }
-    const uint64_t key = cache_key(s->src, kernel);
+    const std::vector<std::string> opts = jit_opts(dev);
+    const uint64_t key = cache_key(s->src, kernel, opts);
     std::string name, code;
-    bool have = false;
+    int from = 0;  // where the code object came from: 1 process cache, 2 disk, 3 compiled
     {
         std::lock_guard<std::mutex> ck(g_cache_mu);
         auto c = g_code.find(key);
         if (c != g_code.end()) {
             name = c->second.first;
             code = c->second.second;
-            have = true;
+            from = 1;
         }
     }
-    if (!have && disk_load(key, name, code)) have = true;
-    if (!have) {
-        std::string err;
-        if (!compile(s->src, kernel, name, code, err)) {
-            s->error = err;
+    if (!from && disk_load(key, name, code)) from = 2;
+    // a cached object that does not load (truncated, corrupt, another
+    // toolchain's) is dropped and compiled afresh once; a fresh object that
+    // does not load is a compilation failure: the interpreter runs
+    for (;;) {
+        if (!from) {
+            std::string err;
+            if (!compile(s->src, kernel, opts, name, code, err)) {
+                s->error = err;
+                return MC_OK;
+            }
+            disk_store(key, name, code);
+            from = 3;
+        }
+        hipModule_t mod;
+        hipError_t e = hipModuleLoadData(&mod, code.data());
+        hipFunction_t f = nullptr;
+        if (e == hipSuccess) {
+            e = hipModuleGetFunction(&f, mod, name.c_str());
+            if (e != hipSuccess) (void)hipModuleUnload(mod);
+        }
+        if (e == hipSuccess) {
+            s->mods.push_back(mod);
+            {
+                std::lock_guard<std::mutex> ck(g_cache_mu);
+                g_code[key] = std::make_pair(name, code);
+            }
+            s->fns[fkey] = f;
+            *fn = f;
             return MC_OK;
         }
-        disk_store(key, name, code);
+        (void)hipGetLastError();
+        {
+            std::lock_guard<std::mutex> ck(g_cache_mu);
+            g_code.erase(key);
+        }
+        if (from == 3) {
+            s->error = std::string("expression JIT: the compiled code object does not load: ") +
+                       hipGetErrorString(e);
+            return MC_OK;
+        }
+        if (from == 2) {
+            const std::string path = cache_path(key);
+            if (!path.empty()) (void)unlink(path.c_str());
+        }
+        from = 0;
     }
-    {
-        std::lock_guard<std::mutex> ck(g_cache_mu);
-        g_code[key] = std::make_pair(name, code);
-    }
-    hipModule_t mod;
-    hipError_t e = hipModuleLoadData(&mod, code.data());
-    if (e != hipSuccess)
-        return fail(MC_ERR_HIP, "expression JIT: hipModuleLoadData failed: %s", hipGetErrorString(e));
-    s->mods.push_back(mod);
-    hipFunction_t f;
-    e = hipModuleGetFunction(&f, mod, name.c_str());
-    if (e != hipSuccess)
-        return fail(MC_ERR_HIP, "expression JIT: hipModuleGetFunction failed: %s",
-                    hipGetErrorString(e));
-    s->fns[fkey] = f;
-    *fn = f;
-    return MC_OK;
 }
 
 int jit_launch(const mc_program* p, const std::string& kernel, unsigned grid, unsigned block,
@@ -632,6 +685,8 @@ extern "C" int mc_debug_expr_jit_compile(const mc_program* p, const char* kernel
     if (!p || !kernel) return fail(MC_ERR_INVALID, "NULL argument");
     if (!p->ex) return fail(MC_ERR_INVALID, "the program has no expression terms");
     std::string name, code, err;
-    if (!compile(jit_source(p), kernel, name, code, err)) return fail(MC_ERR_UNSUPPORTED, "%s", err.c_str());
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (!compile(jit_source(p), kernel, jit_opts(dev), name, code, err)) return fail(MC_ERR_UNSUPPORTED, "%s", err.c_str());
     return MC_OK;
 }

@@ -995,8 +995,11 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
         MC_STAMP(15);
     }
     MC_STAMP_FLUSH
-    // a timed-out chain keeps its scalars and shared parameters (its private
-    // parameters hold the last accepted draw; mc_workspace_status reports it)
+    // a timed-out chain's state is undefined: its scalars, lp and shared
+    // parameters stay as the launch found them, while an accept at a completed
+    // level has already written its private parameters (st_q / st_g), so they
+    // may belong to a later draw.  mc_workspace_status reports the timeout and
+    // the caller re-initialises the chains (include/mcmc355.h).
     if (!ok) return;
 
     if (slice == 0 && xon) {

@@ -131,11 +131,17 @@ extern "C" int mc_workspace_status(const mc_program* p, const void* ws, int64_t 
     MC_HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     if (v != 0) {
         ws_forget(ws);  // the next launch clears the status word and the granules
-        if (v == 2)
+        if (v == 2) {
+            // the placement probe was wrong for this device: later launches in
+            // this process use the agent-scope exchange (as MC_XCD_LOCAL=0);
+            // the launch that failed skipped work and has to be redone
+            g_xcd_local = 0;
             return fail(MC_ERR_UNSUPPORTED,
                         "sliced launch: an exchange group's workgroups were not on one XCD, which "
                         "its L2-resident records need (the device's workgroup placement differs "
-                        "from its probe); MC_XCD_LOCAL=0 turns that exchange off");
+                        "from its probe); the L2-resident exchange is now off in this process: "
+                        "redo the launch from the chains' state before it");
+        }
         return fail(MC_ERR_TIMEOUT, "sliced HMC: a cross-workgroup exchange timed out");
     }
     return MC_OK;

@@ -171,6 +171,29 @@ def test_bench_ess_two_ranks_equal_one_rank(gpu):
     print("ESS converged (1 rank / 2 ranks):", a.get("ess_sum"), b.get("ess_sum"))
 
 
+def test_bench_spawns_ranks_itself(gpu):
+    """The driver's command shape without a launcher (VERDICT r5 "Next round"
+    1): `bench.py --gpus 2` spawns its two ranks itself (here sharing the one
+    GPU over gloo) and prints one line whose value sums both ranks' chains;
+    the large program at 64 chains per rank, as test_bench_large_two_ranks_gloo."""
+    env = dict(os.environ, MC_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20",
+           "--warmup", "5", "--chains", "64", "--no-cpu-baseline", "--clock-warm-ms", "0",
+           "--ess-draws", "200", "--ess-warmup", "50"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=170, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["total_chains"] == 128
+    assert out["value"] == pytest.approx(128 * 20 * 20 / (out["ms_per_step"] * 20 / 1e3),
+                                         rel=1e-6)
+    assert out["ess_converged"]["chains"] == 128
+    print("bench.py --gpus 2 (spawned ranks, one GPU):", out["value"] / 1e6, "M steps/s")
+
+
 def _run_large(C, offset):
     import mlx_mcmc_amd as m
 

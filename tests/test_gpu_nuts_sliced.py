@@ -142,7 +142,9 @@ def test_sliced_launch_split(gpu):
 def test_sliced_exchange_timeout_reported(gpu):
     """mc_debug_exchange_fault: the grid's last workgroup never publishes, so
     its chain block's slices time out; mc_workspace_status reports
-    MC_ERR_TIMEOUT, the stranded chains keep their state, the next launch on
+    MC_ERR_TIMEOUT, the stranded chains keep their state (the fault comes
+    before the first leaf; a timeout after an accept at a completed level
+    leaves the chain's state undefined, include/mcmc355.h), the next launch on
     the same workspace runs clean."""
     import torch
 

@@ -263,6 +263,15 @@ def test_mcmc_method_errors():
         mc.summary()
 
 
+def test_nuts_kernel_choice_is_checked():
+    """nuts(nuts_kernel=...) accepts only 'auto' and 'tape' (ADVICE r5): a
+    typo raises before anything is traced or launched."""
+    lp = lambda p: m.Normal(0, 1).log_prob(p["x"])  # noqa: E731
+    for bad in ("lanes", "sliced", "Auto", ""):
+        with pytest.raises(ValueError, match="nuts_kernel"):
+            m.nuts(lp, {"x": 0.0}, num_samples=1, num_warmup=0, nuts_kernel=bad)
+
+
 def test_transformed_operands_and_identity_terms():
     """Reparameterised models (include/mcmc355.h mc_transform_kind,
     MC_DIST_IDENTITY): mx.exp / mx.log of a parameter is a transformed
