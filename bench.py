@@ -258,9 +258,10 @@ def kernel_label(prog, C):
 def pmc_traffic(shape, iters_per_launch):
     """HBM bytes per launch of `iters_per_launch` iterations from
     profiles/pmc_traffic.json (scripts/pmc_traffic.py): records keyed
-    "<shape>@<iters per launch>", measured at that launch size (a launch has
-    fixed bytes — the slice blocks are loaded once per launch — so a record
-    of another size is not rescaled).  (None, reason) when absent."""
+    "<shape>@<iters per launch>" (HMC; "nuts-<model>[-<shape>]" and
+    "mh-<shape>" for the other lines), measured at that launch size (a launch
+    has fixed bytes — the slice blocks are loaded once per launch — so a
+    record of another size is not rescaled).  (None, reason) when absent."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         data = json.load(open(path))
@@ -605,6 +606,8 @@ def main_nuts(args):
         leaves_per_launch = leaves * (launch_ms / launch_ms_total) if launch_ms_total else 0.0
         achieved = leaves_per_launch * flops_per_leaf / (launch_ms * 1e-3) / 1e12
         hier = args.nuts_model == "hier"
+        traffic, traffic_src = pmc_traffic(
+            f"nuts-{args.nuts_model}" + (f"-{args.shape}" if hier else ""), min(B, K))
         out = {
             "metric": ("leapfrog-steps/sec (all chains), NUTS " +
                        (label if hier else "100-dim kappa=1000 Gaussian")),
@@ -621,7 +624,8 @@ def main_nuts(args):
                        "total_chains": C * world, "parallelism": f"chains sharded {C}/GPU"},
             "roofline": {
                 "bound": "valu_fp32", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
+                "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": nuts_kernel_name(prog),
                 "launch_ms": launch_ms,
                 "iters_per_launch": B, "flops_per_leaf": flops_per_leaf,
@@ -743,6 +747,7 @@ def main_mh(args):
         # parameter), the direct term (~8 per parameter)
         flops = 3 * N + 10 * D
         achieved = C * iters_per_launch * flops / (launch_ms * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic(f"mh-{args.shape}", iters_per_launch)
         kern = ("k_mh_sl (sliced lane-resident MH, one chain per wave, "
                 f"{prog.num_slices} slices)" if _lib.load().mc_program_mh_sliced(prog.handle) == 1
                 else f"k_mh<{prog.waves_per_chain}>")
@@ -758,7 +763,8 @@ def main_mh(args):
                        "num_params": D, "num_obs": N, "chains_per_gpu": C,
                        "total_chains": C * world, "parallelism": f"chains sharded {C}/GPU"},
             "roofline": {"bound": "valu_fp32", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
+                         "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": kern, "launch_ms": launch_ms,
                          "iters_per_launch": iters_per_launch, "flops_per_iteration": flops},
             "accept_rate": float(np.mean(sc["n_accept"] / np.maximum(sc["n_total"], 1))),

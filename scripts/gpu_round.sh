@@ -10,10 +10,19 @@
 #                                                          config 5 and Large
 #   bash scripts/gpu_round.sh kt TAG NAME [bench args]     rocprofv3 kernel trace + stats of a
 #                                                          bench run (filtered: prof_filter.py)
-#   bash scripts/gpu_round.sh pmc TAG NAME KERNEL [bench args]
+#   bash scripts/gpu_round.sh pmc TAG NAME KERNEL IPL L FLOOR KEY [bench args]
 #                                                          FETCH / WRITE passes and the two SQ
 #                                                          passes (separate runs), SQ summary
-#                                                          of KERNEL (pmc_sq.py)
+#                                                          of KERNEL (pmc_sq.py) per wave-step
+#                                                          of IPL-iteration launches of L steps
+#                                                          (every dispatch of KERNEL in the run
+#                                                          must be one: --clock-warm-kind gemm
+#                                                          --no-ess, warmup/steps multiples of
+#                                                          --iters-per-launch); FLOOR = the
+#                                                          sweep's VALU per wave-step (0: none);
+#                                                          the HBM bytes per launch go to
+#                                                          gpurun_out/TAG_traffic.json under
+#                                                          KEY@IPL (bench.py pmc_traffic)
 #   bash scripts/gpu_round.sh ab TAG LIB... [-- bench args] A/B of library builds on one box
 #                                                          ("-" = the in-tree build)
 #   bash scripts/gpu_round.sh final TAG                    tests + smoke + bench-lines
@@ -76,11 +85,13 @@ case $STEP in
   bench-lines) bench_lines ;;
   kt) n=$1; shift; prof kt_$n "$*" --kernel-trace --stats ;;
   pmc)
-    n=$1; k=$2; shift 2
+    n=$1; k=$2; ipl=$3; lf=$4; fl=$5; key=$6; shift 6
     prof fetch_$n "$*" --pmc FETCH_SIZE && prof write_$n "$*" --pmc WRITE_SIZE &&
     prof sq1_$n "$*" --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_SMEM &&
     prof sq2_$n "$*" --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU_TRANS_F32 SQ_INST_CYCLES_SALU &&
-    python scripts/pmc_sq.py gpurun_out/${TAG}_sq_$n.json "$k" 1 1 gpurun_out/${TAG}_sq1_$n gpurun_out/${TAG}_sq2_$n ;;
+    python scripts/pmc_sq.py gpurun_out/${TAG}_sq_$n.json "$k" "$ipl" "$lf" --floor "$fl" gpurun_out/${TAG}_sq1_$n gpurun_out/${TAG}_sq2_$n &&
+    python scripts/pmc_traffic.py gpurun_out/${TAG}_fetch_$n gpurun_out/${TAG}_write_$n "$key" "$ipl" \
+        "profiles/$TAG: fetch_$n|write_$n (bench.py $*)" --kernel "$k" --out gpurun_out/${TAG}_traffic.json ;;
   ab)
     libs=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do libs+=("$1"); shift; done
     [ "$1" = "--" ] && shift
