@@ -289,7 +289,9 @@ def test_nuts_large_dual_averaging_against_oracle(gpu, slices):
         # the committed trace separates from any other run of the same
         # restatement within a few iterations of eps ~ 4e-3 — the oracle's own
         # at 4 torch threads instead of 1 agrees with it for 3 iterations
-        # (chain 0: depths 10, 6, 7, then 4 vs 3): the first 3, which hold the
+        # (chain 0: depths 10, 6, 7, then 4 vs 3; committed as the CPU test
+        # test_oracle_pins.py::test_large_dual_averaging_fixture_vs_thread_count):
+        # the first 3, which hold the
         # depth-10 tree and the first dual-averaging jump, are pinned; the
         # strict replay above is the comparison beyond them
         assert same_fx >= min(3, sep), f"chain {chain}: trees diverge from the fixture at {same_fx}"
