@@ -461,6 +461,12 @@ int32_t mc_program_expr_jit(const mc_program* prog);
 int mc_debug_program_host_only(int on);
 int64_t mc_debug_expr_jit_source(const mc_program* prog, char* buf, int64_t cap);
 int mc_debug_expr_jit_compile(const mc_program* prog, const char* kernel);
+/* Test hook without a device: plan a host-only program's S slices onto the
+ * lane-resident layout (host tables only); with expression terms on it,
+ * mc_debug_expr_jit_source / _compile take a "mc::k_hmc_lr<...>" kernel name
+ * and give / compile the lane-resident source (jit.hip gen_lane_source).  */
+int mc_debug_lane_plan_host(mc_program* prog, int32_t num_slices);
+int64_t mc_debug_expr_jit_lane_source(const mc_program* prog, char* buf, int64_t cap);
 /* Test hooks (host code, no device): the samplers' Box-Muller pair from two
  * Philox words per pair (words [n][2] -> out [n][2] f32) and their f32 log
  * of a uniform in (0, 1] (philox.h mc_box_muller / mc_logf_unit).         */

@@ -226,6 +226,8 @@ SIGNATURES = [
     ("mc_debug_program_host_only", ctypes.c_int, [ctypes.c_int]),
     ("mc_debug_expr_jit_source", ctypes.c_int64, [_VP, ctypes.c_char_p, ctypes.c_int64]),
     ("mc_debug_expr_jit_compile", ctypes.c_int, [_VP, ctypes.c_char_p]),
+    ("mc_debug_lane_plan_host", ctypes.c_int, [_VP, ctypes.c_int32]),
+    ("mc_debug_expr_jit_lane_source", ctypes.c_int64, [_VP, ctypes.c_char_p, ctypes.c_int64]),
     ("mc_box_muller_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     ("mc_logf_unit_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
     ("mc_hmc_run", ctypes.c_int,

@@ -223,9 +223,11 @@ struct SlPartition {
 
 static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = nullptr) {
     const std::vector<DevTerm>& raw = p->raw;
-    if (has_expr(p))
-        return fail(MC_ERR_UNSUPPORTED, "expression terms run on the chain-per-workgroup "
-                    "kernels (not sliceable)");
+    if (has_expr(p) && !expr_lanes_ok(p))
+        return fail(MC_ERR_UNSUPPORTED, "expression terms other than data / broadcast "
+                    "parameter / constant leaves (a parameter vector, a gather, more than %d "
+                    "data leaves) run on the chain-per-workgroup kernels (not sliceable)",
+                    kLrExprData);
     if (has_affine(p) && !affine_lanes_ok(p))
         return fail(MC_ERR_UNSUPPORTED, "affine loc operands other than `loc + b * x` over "
                     "data x (x a parameter vector, a non-Normal term, a per-element scale) run "
@@ -255,6 +257,11 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = n
         for (int a = 0; a < 3; ++a)
             if (t.op[a].kind == MC_OP_PSCALAR) shared[t.op[a].poff] = 1;
         if (t.affine && t.ab.kind == MC_OP_PSCALAR) shared[t.ab.poff] = 1;  // the slope
+        if (t.dist == MC_DIST_EXPR)  // an expression's broadcast leaves
+            for (int k = 0; k < t.expr_n; ++k) {
+                const DevExprNode& d = p->nodes[t.expr_base + k];
+                if (d.op == MC_EX_LEAF && d.leaf.kind == MC_OP_PSCALAR) shared[d.leaf.poff] = 1;
+            }
     }
     std::vector<int64_t> cost(D, 1);
     for (int t = 0; t < nT; ++t)
@@ -300,7 +307,7 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = n
                 x = o.xf;
             }
         for (int t = 0; t < nT; ++t) {
-            bool sc = true;
+            bool sc = raw[t].dist != MC_DIST_EXPR;
             for (int a = 0; a < 3; ++a) {
                 const int k = raw[t].op[a].kind;
                 if (k != MC_OP_CONST && k != MC_OP_PSCALAR && k != MC_OP_NONE) sc = false;
@@ -311,6 +318,28 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = n
                 if (o.kind == MC_OP_PSCALAR && o.xf != shxf[jsh[o.poff]])
                     return fail(MC_ERR_UNSUPPORTED, "a broadcast parameter read both raw and "
                                 "through mx.exp / mx.log by per-element terms: not sliceable");
+            }
+            // an expression reads a transformed broadcast parameter only
+            // through the matching node (mx.exp(log_sigma) for an exp
+            // transform): the lane code reads the transformed value there and
+            // its cotangent is the value's (jit.hip gen_lane_term)
+            if (raw[t].dist == MC_DIST_EXPR) {
+                const DevExprNode* N = p->nodes.data() + raw[t].expr_base;
+                for (int k = 0; k < raw[t].expr_n; ++k) {
+                    if (N[k].op == MC_EX_LEAF) continue;
+                    const int args[3] = {N[k].a, N[k].b, N[k].c};
+                    for (int x = 0; x < 3; ++x) {
+                        const int a = args[x];
+                        if (a < 0 || N[a].op != MC_EX_LEAF || N[a].leaf.kind != MC_OP_PSCALAR) continue;
+                        const int xfk = shxf[jsh[N[a].leaf.poff]];
+                        if (xfk == MC_XF_NONE) continue;
+                        const int want = xfk == MC_XF_EXP ? MC_EX_EXP : MC_EX_LOG;
+                        if (N[k].op != want || x != 0)
+                            return fail(MC_ERR_UNSUPPORTED, "a broadcast parameter read raw by an "
+                                        "expression and through mx.exp / mx.log by a fused term: "
+                                        "not sliceable");
+                    }
+                }
             }
         }
     }
@@ -372,7 +401,7 @@ static int plan_slices(mc_program* p, int S, SlicePlan& P, SlPartition* part = n
     std::vector<int> sterm_raw;
     P.sterms.clear();
     for (int t = 0; t < nT; ++t) {
-        bool sc = true;
+        bool sc = raw[t].dist != MC_DIST_EXPR;  // (an expression term is sliced by element)
         for (int a = 0; a < 3; ++a) {
             const int k = raw[t].op[a].kind;
             if (k != MC_OP_CONST && k != MC_OP_PSCALAR && k != MC_OP_NONE) sc = false;
@@ -918,6 +947,13 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
                 lt.kind[lt.pp] == SK_PP && lt.kind[1 - lt.pp] != SK_PP &&
                 lt.kind[1 - lt.pp] != SK_NONE && !rt.affine)
                 lt.sig = LS_DSCALE;
+            // an expression term (a chunk term: its data leaves tiled below)
+            if (rt.dist == MC_DIST_EXPR) {
+                lt.sig = LS_EXPR;
+                lt.expr_base = rt.expr_base;
+                lt.expr_n = rt.expr_n;
+                L.has_expr = 1;
+            }
             // element lists per (slot, lane), in element order
             std::vector<std::vector<int64_t>> lists((size_t)kLrMaxSlots * 64);
             int nslot = 1;
@@ -985,6 +1021,26 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
                     }
                 if (a < 3) lt.doff[a] = (int32_t)(base - blk0);
                 else lt.xoff = (int32_t)(base - blk0);
+            }
+            if (lt.sig == LS_EXPR) {  // the data leaves, in node order
+                int e = 0;
+                for (int k = 0; k < rt.expr_n; ++k) {
+                    const DevExprNode& d = p->nodes[rt.expr_base + k];
+                    if (d.op != MC_EX_LEAF || d.leaf.kind != MC_OP_DATA) continue;
+                    if (e >= kLrExprData) return no("an expression with too many data leaves");
+                    while (L.data.size() % 4) L.data.push_back(0.0f);
+                    const int64_t base = (int64_t)L.data.size();
+                    L.data.resize(base + tot, 0.0f);
+                    const int64_t src = d.leaf.pool;
+                    for (int r = 0; r < nslot; ++r)
+                        for (int l = 0; l < 64; ++l) {
+                            const std::vector<int64_t>& li = lists[(size_t)r * 64 + l];
+                            for (size_t u = 0; u < li.size(); ++u)
+                                L.data[base + lt.toff[r] + (u >> 2) * 256 + 4 * l + (u & 3)] =
+                                    dp[src + li[u]];
+                        }
+                    lt.eoff[e++] = (int32_t)(base - blk0);
+                }
             }
             if (lt.sig == LS_DSCALE) {
                 // the scale tile becomes 1/s^2 and the private operand's (free)
@@ -1115,7 +1171,7 @@ static int64_t program_elements(const mc_program* p) {
 // slices, 79 M with 16, profiles/r4/slices).
 static constexpr int64_t kLrAutoMinElements = 2048;
 static int auto_slices(const mc_program* p) {
-    if (has_expr(p) || (has_affine(p) && !affine_lanes_ok(p)) ||
+    if ((has_expr(p) && !expr_lanes_ok(p)) || (has_affine(p) && !affine_lanes_ok(p)) ||
         (has_transform(p) && !transform_on_shared_only(p)))
         return 1;
     const int64_t n = program_elements(p);
@@ -1128,6 +1184,11 @@ static int auto_slices(const mc_program* p) {
 // Plan an unsliced program onto the lane-resident kernel (one slice).
 static int plan_lanes1(mc_program* p) {
     free_lanes(p->lr);
+    // expression programs below the slicing threshold stay on the tape (the
+    // one-slice lane kernel is not measured on them)
+    if (has_expr(p))
+        return fail(MC_ERR_UNSUPPORTED, "lane-resident kernel: an unsliced expression program "
+                    "runs on the tape");
     SlicePlan P;
     SlPartition part;
     const int rc = plan_slices(p, 1, P, &part);
@@ -1257,6 +1318,11 @@ extern "C" int mc_program_set_slice_kernel(mc_program* p, int32_t kernel) {
 
 extern "C" int32_t mc_program_slice_kernel(const mc_program* p) {
     if (!p) return -1;
+    // expression terms on the lane layout run there only with their JIT-compiled
+    // kernel: without it (off, or its compilation failed) the tape runs them
+    if (p->lr.ok && p->lr.has_expr && p->slice_kernel != 1 &&
+        (!jit_enabled() || !jit_error(p).empty()))
+        return 0;
     if (p->sl.S < 2) return (p->lr.ok && p->lr.S == 1) ? 2 : 0;
     if (p->slice_kernel == 1 || !p->lr.ok) return 1;
     return 2;
@@ -1970,6 +2036,25 @@ extern "C" int mc_program_create_expr(const mc_term* terms, int32_t n_terms,
         }
     }
     *out = p;
+    return MC_OK;
+}
+
+// Test hook without a device: the slice and lane plans of a host-only program
+// (mc_debug_program_host_only) with S slices, host tables only (no upload),
+// so the lane-resident expression source can be generated and compiled on a
+// machine without a GPU (mc_debug_expr_jit_source / _compile with a
+// "mc::k_hmc_lr<...>" kernel).  Returns the planner's status; MC_OK with
+// lr.has_expr set when the program's expression terms took the lane layout.
+extern "C" int mc_debug_lane_plan_host(mc_program* p, int32_t S) {
+    if (!p) return fail(MC_ERR_INVALID, "program is NULL");
+    if (S < 1 || S > kLrSlices) return fail(MC_ERR_INVALID, "S must be in [1, %d]", kLrSlices);
+    free_lanes(p->lr);
+    SlicePlan P;
+    SlPartition part;
+    int rc = plan_slices(p, S, P, &part);
+    if (rc != MC_OK) return rc;
+    rc = plan_lanes(p, P, part, p->lr);
+    if (rc != MC_OK) return fail(rc, "lane-resident kernel: %s", p->lr.why.c_str());
     return MC_OK;
 }
 

@@ -96,6 +96,8 @@ struct LanePlan {
     int32_t* d_rng = nullptr;
     int has_xf = 0;      // a shared parameter is transformed, or an identity term
                          // (no NUTS lanes, no term interpreter)
+    int has_expr = 0;    // LS_EXPR terms: only the JIT-compiled k_hmc_lr runs the plan
+                         // (jit.hip); without it the program runs on the tape
     std::string why;     // why it does not qualify
     std::vector<LrTerm> terms;
     std::vector<float> data;
@@ -231,9 +233,35 @@ inline bool affine_lanes_ok(const mc_program* p) {
     }
     return true;
 }
-// The term interpreter (k_hmc_sl) takes neither transformed operands nor
-// affine locs: such sliced programs run on the lane-resident kernels only.
-inline bool interp_ok(const mc_program* p) { return !has_transform(p) && !has_affine(p); }
+// Expression terms the lane-resident kernel takes (lanes.h LS_EXPR, code
+// generated per program by the expression JIT): leaves data, broadcast
+// parameters and constants only — no parameter vectors or gathers — with at
+// least one data leaf and at most kLrExprData of them, one pass.  Every term
+// of the program must qualify (else the program stays on the tape kernels).
+inline bool expr_lanes_ok(const mc_program* p) {
+    if (const char* e = std::getenv("MC_EXPR_LANES"))  // 0: the tape (A/B, tests)
+        if (e[0] == '0') return false;
+    for (const DevTerm& t : p->raw) {
+        if (t.dist != MC_DIST_EXPR) continue;
+        if (t.primary >= 0 || t.npass != 1 || t.expr_n < 1) return false;
+        int ndata = 0;
+        for (int k = 0; k < t.expr_n; ++k) {
+            const DevExprNode& d = p->nodes[t.expr_base + k];
+            if (d.op != MC_EX_LEAF) continue;
+            if (d.prim) return false;
+            if (d.leaf.kind == MC_OP_DATA) ++ndata;
+            else if (d.leaf.kind != MC_OP_CONST && d.leaf.kind != MC_OP_PSCALAR) return false;
+        }
+        if (ndata < 1 || ndata > kLrExprData) return false;
+    }
+    return true;
+}
+// The term interpreter (k_hmc_sl) takes neither transformed operands, affine
+// locs nor expression terms: such sliced programs run on the lane-resident
+// kernels only (or, expression terms without the JIT, on the tape).
+inline bool interp_ok(const mc_program* p) {
+    return !has_transform(p) && !has_affine(p) && !has_expr(p);
+}
 
 inline LrCtx lrctx_of(const mc_program* p) {
     LrCtx c;
@@ -456,6 +484,11 @@ inline int64_t sl_workspace_bytes(const mc_program* p, int64_t C) {
         x = std::max(x, 2 * lr_groups_per_launch(p, C) * lr_nw(p) * p->sl.S * 128);
     return kSlStatusBytes + x;
 }
+// A lane plan with expression terms (LanePlan::has_expr) runs only the
+// JIT-compiled k_hmc_lr (its LS_EXPR sweep is generated per program,
+// jit.hip gen_lane_term); when the JIT is off or its compilation failed the
+// launch returns kLanesNoJit and the caller runs the program on the tape.
+constexpr int kLanesNoJit = 1000;
 inline bool use_lanes(const mc_program* p, const mc_run_config* cfg) {
     return p->lr.ok && p->slice_kernel != 1 && cfg->num_leapfrog_steps > 0;
 }

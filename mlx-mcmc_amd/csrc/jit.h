@@ -13,6 +13,10 @@ bool jit_enabled();
 // compilation failed: the caller then launches the interpreter's kernel.
 int jit_launch(const mc_program* p, const std::string& kernel, unsigned grid, unsigned block,
                size_t lds, hipStream_t st, void** args, bool* used);
+// The compiled `kernel` of the program (loaded on the current device);
+// *fn = nullptr (and MC_OK) when the JIT is off, the program has no
+// expression terms, or the compilation failed.
+int jit_function(const mc_program* p, const std::string& kernel, hipFunction_t* fn);
 // The last compilation failure of the program ("" if none).
 std::string jit_error(const mc_program* p);
 void jit_free(mc_program* p);

@@ -43,6 +43,8 @@ struct JitState {
     std::mutex mu;
     bool have_src = false;
     std::string src;
+    bool have_lsrc = false;
+    std::string lsrc;  // the lane-resident kernels' source (gen_lane_source)
     std::map<std::pair<std::string, int>, hipFunction_t> fns;  // (kernel, device)
     std::vector<hipModule_t> mods;
     std::string error;  // the last compilation failure ("" if none)
@@ -405,6 +407,173 @@ std::string gen_source(const mc_program* p) {
     return o.str();
 }
 
+// ---- lane-resident expression terms (lanes.h LS_EXPR) -----------------------
+// A float constant as its bit pattern (exact in the generated source).
+std::string flit(float v) {
+    uint32_t b;
+    std::memcpy(&b, &v, 4);
+    char buf[48];
+    std::snprintf(buf, sizeof buf, "__uint_as_float(0x%08xu)", b);
+    return buf;
+}
+
+// One LS_EXPR term's lane sweep: lane j's run of the term's elements in its
+// slice (a chunk term: slot 0, lengths at len_off), both chains of the wave
+// packed per element (exf2 = chain 0, chain 1), every node's forward value
+// and reverse step through eval.h ex2_fwd / ex2_bwd (the tape's arithmetic,
+// component for component), the broadcast leaves' adjoints summed over the
+// run in element order.  Data leaf e is tile eoff[e] (node order); a
+// broadcast leaf reads the raw parameter of shared ordinal K (lane 2K + c of
+// sh.q, the planner keeps expression-read parameters untransformed).
+// Constants are literals.  LP = false leaves out what only log p needs (the
+// compiler drops the nodes no adjoint reads).
+void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N,
+                   const LanePlan& L) {
+    const int nn = T.expr_n;
+    auto ordinal = [&](int poff) {
+        for (int k = 0; k < L.Dsh; ++k)
+            if (L.shl[k] == poff) return k;
+        return 0;
+    };
+    o << "template <bool LP>\n"
+      << "MC_DEV void jit_lt" << T.expr_base
+      << "(const MC_CONST LrTerm* T, const float* sd, int j, const LrShared& sh,\n"
+      << "    float (&lpp)[2], float (&gshp)[kLrMaxShared][2]) {\n"
+      << "  const int len = ((const int32_t*)sd)[T->len_off + j];\n"
+      << "  const exf2 wv = {T->weight, T->weight};\n"
+      << "  exf2 lpa = {0.0f, 0.0f};\n  (void)lpa;\n";
+    // a transformed broadcast parameter (LanePlan::shxf) is read through its
+    // transform node only (the planner checks it): that node reads the lane's
+    // transformed value sh.v and its adjoint is the value's cotangent
+    auto xf_node = [&](int k) {
+        const DevExprNode& d = N[k];
+        if ((d.op != MC_EX_EXP && d.op != MC_EX_LOG) || d.a < 0) return -1;
+        const DevExprNode& x = N[d.a];
+        if (x.op != MC_EX_LEAF || x.leaf.kind != MC_OP_PSCALAR) return -1;
+        const int K = ordinal(x.leaf.poff);
+        const int xf = L.shxf[K];
+        if (xf == MC_XF_NONE || d.op != (xf == MC_XF_EXP ? MC_EX_EXP : MC_EX_LOG)) return -1;
+        return K;
+    };
+    auto raw_leaf = [&](int k) {  // a broadcast leaf read raw (its own cotangent)
+        return N[k].op == MC_EX_LEAF && N[k].leaf.kind == MC_OP_PSCALAR &&
+               L.shxf[ordinal(N[k].leaf.poff)] == MC_XF_NONE;
+    };
+    std::vector<int> dleaves;
+    for (int k = 0; k < nn; ++k) {
+        const DevExprNode& d = N[k];
+        if (xf_node(k) >= 0) {
+            const int K = xf_node(k);
+            o << "  const exf2 v" << k << " = {rl(sh.v, " << 2 * K << "), rl(sh.v, " << 2 * K + 1
+              << ")};\n  exf2 p" << k << " = {0.0f, 0.0f};\n";
+            continue;
+        }
+        if (d.op == MC_EX_LEAF) {
+            if (d.leaf.kind == MC_OP_PSCALAR && !raw_leaf(k)) {
+                o << "  const exf2 v" << k << " = {0.0f, 0.0f};  // (read through node transforms)\n";
+            } else if (d.leaf.kind == MC_OP_CONST) {
+                o << "  const exf2 v" << k << " = {" << flit(d.leaf.cval) << ", " << flit(d.leaf.cval)
+                  << "};\n";
+            } else if (d.leaf.kind == MC_OP_PSCALAR) {
+                const int K = ordinal(d.leaf.poff);
+                o << "  const exf2 v" << k << " = {rl(sh.q, " << 2 * K << "), rl(sh.q, " << 2 * K + 1
+                  << ")};\n  exf2 p" << k << " = {0.0f, 0.0f};\n";
+            } else {  // data
+                o << "  const float* d" << k << " = sd + T->eoff[" << dleaves.size() << "] + 4 * j;\n";
+                dleaves.push_back(k);
+            }
+        } else {
+            o << "  const float c" << k << " = " << flit(d.leaf.cval) << ";\n";
+        }
+    }
+    auto arg = [&](int a) { return a >= 0 ? "v" + std::to_string(a) : std::string("z2"); };
+    o << "  const exf2 z2 = {0.0f, 0.0f};\n  (void)z2;\n";
+    o << "  auto element = [&](";
+    for (size_t e = 0; e < dleaves.size(); ++e) o << (e ? ", " : "") << "float x" << dleaves[e];
+    o << ") {\n";
+    for (int k = 0; k < nn; ++k) {
+        const DevExprNode& d = N[k];
+        if (d.op == MC_EX_LEAF) {
+            if (d.leaf.kind == MC_OP_DATA) o << "    const exf2 v" << k << " = {x" << k << ", x" << k << "};\n";
+            continue;
+        }
+        if (xf_node(k) >= 0) continue;
+        o << "    const exf2 v" << k << " = ex2_fwd(" << d.op << ", " << arg(d.a) << ", " << arg(d.b)
+          << ", " << arg(d.c) << ", c" << k << ");\n";
+    }
+    o << "    if constexpr (LP) lpa += wv * v" << nn - 1 << ";\n";
+    // (adjoints start at -0, as the tape's: -0 + x == x)
+    for (int k = 0; k < nn; ++k) o << "    exf2 a" << k << " = {-0.0f, -0.0f};\n";
+    o << "    a" << nn - 1 << " = wv;\n";
+    for (int k = nn - 1; k >= 0; --k) {
+        const DevExprNode& d = N[k];
+        if (d.op == MC_EX_LEAF) {
+            if (raw_leaf(k)) o << "    p" << k << " += a" << k << ";\n";
+            continue;
+        }
+        if (xf_node(k) >= 0) {
+            o << "    p" << k << " += a" << k << ";\n";
+            continue;
+        }
+        o << "    { exf2 dx, dy, dz; ex2_bwd(" << d.op << ", " << arg(d.a) << ", " << arg(d.b) << ", "
+          << arg(d.c) << ", v" << k << ", a" << k << ", c" << k << ", dx, dy, dz);\n"
+          << "      a" << d.a << " += dx;";
+        if (d.b >= 0) o << " a" << d.b << " += dy;";
+        if (d.c >= 0) o << " a" << d.c << " += dz;";
+        o << " (void)dx; (void)dy; (void)dz; }\n";
+    }
+    o << "  };\n";
+    // four elements per trip: a 16-byte LDS load per data leaf, then the
+    // elements in order; the ragged tail one at a time
+    o << "  int u = 0;\n  for (; u + 4 <= len; u += 4) {\n";
+    for (int k : dleaves)
+        o << "    const float4 X" << k << " = *(const float4*)(d" << k << " + (u >> 2) * 256);\n";
+    const char* comp[4] = {"x", "y", "z", "w"};
+    for (int c = 0; c < 4; ++c) {
+        o << "    element(";
+        for (size_t e = 0; e < dleaves.size(); ++e)
+            o << (e ? ", " : "") << "X" << dleaves[e] << "." << comp[c];
+        o << ");\n";
+    }
+    o << "  }\n  for (; u < len; ++u) {\n    const int ou = (u >> 2) * 256 + (u & 3);\n    element(";
+    for (size_t e = 0; e < dleaves.size(); ++e) o << (e ? ", " : "") << "d" << dleaves[e] << "[ou]";
+    o << ");\n  }\n"
+      << "  if constexpr (LP) {\n    lpp[0] += lpa.x;\n    lpp[1] += lpa.y;\n  }\n";
+    for (int k = 0; k < nn; ++k) {
+        int K = xf_node(k);
+        if (K < 0 && raw_leaf(k)) K = ordinal(N[k].leaf.poff);
+        if (K < 0) continue;
+        o << "  gshp[" << K << "][0] += p" << k << ".x;\n  gshp[" << K << "][1] += p" << k << ".y;\n";
+    }
+    o << "}\n\n";
+}
+
+// The lane-resident kernels' source for a program with LS_EXPR terms:
+// lanes.h with its expression hook defined.
+std::string gen_lane_source(const mc_program* p) {
+    std::ostringstream o;
+    o << "// generated by jit.hip (lane-resident expression terms) for one program: do not edit\n"
+      << "#define MC_JIT_LANES 1\n#include \"lanes.h\"\nnamespace mc {\n";
+    std::vector<int32_t> bases;
+    for (const DevTerm& T : p->raw) {
+        if (T.dist != MC_DIST_EXPR) continue;
+        if (std::find(bases.begin(), bases.end(), T.expr_base) != bases.end()) continue;
+        bases.push_back(T.expr_base);
+        gen_lane_term(o, T, p->nodes.data() + T.expr_base, p->lr);
+    }
+    o << "MC_DEV void mc_jit_lane_expr(const MC_CONST LrTerm* T, const float* sd, int j,\n"
+      << "    const LrShared& sh, float (&lpp)[2], float (&gshp)[kLrMaxShared][2], bool need_lp) {\n"
+      << "  switch (T->expr_base) {\n";
+    for (int32_t b : bases)
+        o << "    case " << b << ":\n      if (need_lp) jit_lt" << b
+          << "<true>(T, sd, j, sh, lpp, gshp);\n      else jit_lt" << b
+          << "<false>(T, sd, j, sh, lpp, gshp);\n      break;\n";
+    o << "    default: break;\n  }\n}\n}  // namespace mc\n";
+    return o.str();
+}
+
+bool is_lane_kernel(const std::string& kernel) { return kernel.rfind("mc::k_hmc_lr<", 0) == 0; }
+
 // hiprtc options: the device's own architecture (gcnArchName's processor,
 // e.g. "gfx950"), so a library built for another ARCH still compiles for the
 // card it runs on; the arch and hiprtc's version are part of the cache key.
@@ -570,12 +739,18 @@ int jit_function(const mc_program* p, const std::string& kernel, hipFunction_t* 
         return MC_OK;
     }
     if (!s->error.empty()) return MC_OK;  // a failed compilation: the interpreter runs
-    if (!s->have_src) {
+    const bool lane = is_lane_kernel(kernel);
+    if (lane && !s->have_lsrc) {
+        s->lsrc = gen_lane_source(p);
+        s->have_lsrc = true;
+    }
+    if (!lane && !s->have_src) {
         s->src = gen_source(p);
         s->have_src = true;
     }
+    const std::string& src = lane ? s->lsrc : s->src;
     const std::vector<std::string> opts = jit_opts(dev);
-    const uint64_t key = cache_key(s->src, kernel, opts);
+    const uint64_t key = cache_key(src, kernel, opts);
     std::string name, code;
     int from = 0;  // where the code object came from: 1 process cache, 2 disk, 3 compiled
     {
@@ -594,7 +769,7 @@ int jit_function(const mc_program* p, const std::string& kernel, hipFunction_t* 
     for (;;) {
         if (!from) {
             std::string err;
-            if (!compile(s->src, kernel, opts, name, code, err)) {
+            if (!compile(src, kernel, opts, name, code, err)) {
                 s->error = err;
                 return MC_OK;
             }
@@ -655,6 +830,9 @@ std::string jit_error(const mc_program* p) {
 }
 
 std::string jit_source(const mc_program* p) { return p->ex ? gen_source(p) : std::string(); }
+std::string jit_lane_source(const mc_program* p) {
+    return p->lr.has_expr ? gen_lane_source(p) : std::string();
+}
 
 extern "C" int mc_debug_expr_jit(int on) {
     g_expr_jit = on < 0 ? -1 : (on ? 1 : 0);
@@ -681,12 +859,25 @@ extern "C" int64_t mc_debug_expr_jit_source(const mc_program* p, char* buf, int6
     return (int64_t)s.size();
 }
 
+extern "C" int64_t mc_debug_expr_jit_lane_source(const mc_program* p, char* buf, int64_t cap) {
+    if (!p) return -1;
+    const std::string s = jit_lane_source(p);
+    if (buf && cap > 0) {
+        const size_t n = std::min<size_t>((size_t)cap - 1, s.size());
+        std::memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    return (int64_t)s.size();
+}
+
 extern "C" int mc_debug_expr_jit_compile(const mc_program* p, const char* kernel) {
     if (!p || !kernel) return fail(MC_ERR_INVALID, "NULL argument");
     if (!p->ex) return fail(MC_ERR_INVALID, "the program has no expression terms");
     std::string name, code, err;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (!compile(jit_source(p), kernel, jit_opts(dev), name, code, err)) return fail(MC_ERR_UNSUPPORTED, "%s", err.c_str());
+    const std::string src = is_lane_kernel(kernel) ? jit_lane_source(p) : jit_source(p);
+    if (src.empty()) return fail(MC_ERR_INVALID, "the program has no lane-resident expression terms");
+    if (!compile(src, kernel, jit_opts(dev), name, code, err)) return fail(MC_ERR_UNSUPPORTED, "%s", err.c_str());
     return MC_OK;
 }

@@ -38,6 +38,7 @@ constexpr int kLrMaxSlots = 4;   // private parameters per lane
 constexpr int kLrMaxShared = 4;  // broadcast parameters
 constexpr int kLrMaxNB = 16;     // chains per block: up to 8 waves x 2 chains
 constexpr int kLrSlices = 16;    // max slices (one 16-lane DPP row per item)
+constexpr int kLrExprData = 6;   // data leaves of a lane-resident expression term
 
 // One term restricted to one slice.
 struct LrTerm {
@@ -62,6 +63,12 @@ struct LrTerm {
     int32_t kb, jb;
     float cb;
     int32_t xoff;
+    // LS_EXPR (an expression term, MC_DIST_EXPR, over data, broadcast
+    // parameters and constants): its node range in the program's node table
+    // and the float offsets of its data leaves' tiles, in node order (tiled as
+    // a chunk term's value)
+    int32_t expr_base, expr_n;
+    int32_t eoff[kLrExprData];
 };
 
 // Specialised term forms (Normal, broadcast scale, moment sums) with their
@@ -79,6 +86,10 @@ enum : int32_t {
     LS_AFF = 8,          // y ~ Normal(loc + b * x, sigma): an affine loc (mc_affine) over
                          // data x; loc private (alpha[g]), shared or constant, b shared or
                          // constant, a broadcast scale (lr_affine_term)
+    LS_EXPR = 9,         // an expression term over data, broadcast parameters and
+                         // constants (a GLM likelihood: logistic, two-predictor ...): its
+                         // element code is generated and compiled per program by the
+                         // expression JIT (jit.hip gen_lane_term, mc_jit_lane_expr)
 };
 
 // A scalar term (constants and shared parameters only), compact for LDS.
@@ -591,12 +602,27 @@ MC_DEV void lr_affine(const MC_CONST LrTerm* T, const float* sd, int j, LrPriv<R
     else lr_affine_term<RS, SK_CONST>(T, sd, j, R, sh, lpp, gshp);
 }
 
+#ifdef MC_JIT_LANES
+// An LS_EXPR term's lane sweep, generated per program (jit.hip
+// gen_lane_term): both chains packed per element, the expression's forward
+// values and reverse-mode adjoints as the tape's (eval.h ex2_fwd / ex2_bwd),
+// its broadcast leaves' cotangents summed over the lane's run into gshp.
+// need_lp: the step's log p is read (the trajectory's last step); otherwise
+// the nodes only the log density needs are left out.
+MC_DEV void mc_jit_lane_expr(const MC_CONST LrTerm* T, const float* sd, int j,
+                             const LrShared& sh, float (&lpp)[2],
+                             float (&gshp)[kLrMaxShared][2], bool need_lp);
+#endif
+
 // Log p partial of this slice at the current point; private gradients
 // (complete) into R.g, this lane's shared-cotangent partials into gshp.
+// need_lp = false: the caller reads no log p of this point (an intermediate
+// leapfrog step); terms that can skip work for it may, the others add theirs.
 template <int RS>
 MC_DEV void lr_eval(const MC_CONST LrTerm* tt, int t0, int nact, const float* sd, int j,
                     LrPriv<RS>& R, const LrShared& sh, float (&lpp)[2],
-                    float (&gshp)[kLrMaxShared][2]) {
+                    float (&gshp)[kLrMaxShared][2], bool need_lp = true) {
+    (void)need_lp;
     for (int t = t0; t < nact; ++t) {
         const MC_CONST LrTerm* T = tt + t;
         switch (T->sig) {
@@ -623,6 +649,13 @@ MC_DEV void lr_eval(const MC_CONST LrTerm* tt, int t0, int nact, const float* sd
                 continue;
             case LS_AFF:
                 lr_affine<RS>(T, sd, j, R, sh, lpp, gshp);
+                continue;
+            case LS_EXPR:
+#ifdef MC_JIT_LANES
+                mc_jit_lane_expr(T, sd, j, sh, lpp, gshp, need_lp);
+#endif
+                // (the library's own instantiations never see one: a program
+                // with LS_EXPR terms launches the JIT-compiled kernel or the tape)
                 continue;
             default:
                 break;
@@ -1137,7 +1170,7 @@ k_hmc_lr(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             f2 lpp2 = {0.f, 0.f};
             lr_finish<RS>(tt, nsweep, ndirect, R, sh, M, KC, lpp2, gshp);
             float lpp[2] = {lpp2[0], lpp2[1]};
-            lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp);
+            lr_eval<RS>(tt, nfast, nact, sd, j, R, sh, lpp, gshp, l == L - 1);
             if (rep > 1) {  // a replicated parameter's gradient: its lanes' partials
 #pragma unroll
                 for (int r = 0; r < RS; ++r) grp_sum2(R.g[r][0], R.g[r][1], rep);

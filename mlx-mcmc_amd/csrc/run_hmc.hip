@@ -207,17 +207,22 @@ extern "C" int mc_hmc_run(const mc_program* p, const mc_run_config* cfg, void* s
         if (ws == nullptr || ws_bytes < need)
             return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
         if (device_cus() <= 0) return fail(MC_ERR_HIP, "no HIP device");
+        int rc = kLanesNoJit;
         if (use_lanes(p, cfg)) {
             hipStream_t st = (hipStream_t)stream;
             switch (p->lr.rs) {  // (one translation unit per slot count: run_lanes_rs*.hip)
-                case 1: return hmc_lanes_rs1(p, cfg, state, samples, tr, ws, st);
-                case 2: return hmc_lanes_rs2(p, cfg, state, samples, tr, ws, st);
-                default: return hmc_lanes_rs4(p, cfg, state, samples, tr, ws, st);
+                case 1: rc = hmc_lanes_rs1(p, cfg, state, samples, tr, ws, st); break;
+                case 2: rc = hmc_lanes_rs2(p, cfg, state, samples, tr, ws, st); break;
+                default: rc = hmc_lanes_rs4(p, cfg, state, samples, tr, ws, st); break;
             }
+            // an expression program without its JIT-compiled lane kernel (the
+            // JIT off or failed): the tape below
+            if (rc != kLanesNoJit) return rc;
+        } else {
+            return sl_nb_for(p, cfg->num_chains) == 16
+                       ? launch_hmc_sl<16>(p, cfg, state, samples, tr, ws, (hipStream_t)stream)
+                       : launch_hmc_sl<8>(p, cfg, state, samples, tr, ws, (hipStream_t)stream);
         }
-        return sl_nb_for(p, cfg->num_chains) == 16
-                   ? launch_hmc_sl<16>(p, cfg, state, samples, tr, ws, (hipStream_t)stream)
-                   : launch_hmc_sl<8>(p, cfg, state, samples, tr, ws, (hipStream_t)stream);
     }
     ws_forget(ws);
     const bool lds = hmc_use_lds(p);

@@ -3,10 +3,83 @@
 // the instantiations compile in parallel.
 #pragma once
 #include "host.h"
+#include "jit.h"
+
+
+// workgroups of a JIT-compiled kernel the device holds at once
+inline int64_t resident_capacity_fn(hipFunction_t f, int block, size_t lds) {
+    int n = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, block, lds) != hipSuccess)
+        return -1;
+    return (int64_t)n * device_cus();
+}
+
+template <int RS, int NSH, int NW, bool X1>
+inline int launch_hmc_lr_jit(const mc_program* p, const mc_run_config* cfg, void* state,
+                             float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
+    const std::string name = "mc::k_hmc_lr<" + std::to_string(RS) + ", " + std::to_string(NSH) +
+                             ", " + std::to_string(NW) + ", " + (X1 ? "true" : "false");
+    hipFunction_t f = nullptr, fxl = nullptr;
+    int rc = jit_function(p, name + ", false>", &f);
+    if (rc != MC_OK) return rc;
+    if (f == nullptr) return kLanesNoJit;
+    int64_t qo, go;
+    mc_state_offsets(p, cfg->num_chains, &qo, &go);
+    char* b = (char*)state;
+    RunArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.cfg = *cfg;
+    LrCtx ctx = lrctx_of(p);
+    const size_t lds = (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm);
+    const int64_t C = cfg->num_chains;
+    constexpr int NB = 2 * NW;
+    const int64_t groups = (C + NB - 1) / NB;
+    const int64_t gpl = lr_groups_per_launch(p, C);
+    const int64_t used = sl_workspace_bytes(p, C);
+    int* status = (int*)ws;
+    unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
+    const uint64_t per_launch = (uint64_t)cfg->iter_count * cfg->num_leapfrog_steps + 1;
+    const int64_t nlaunch = (groups + gpl - 1) / gpl;
+    if (!X1) {
+        const int64_t cap = resident_capacity_fn(f, 64 * NW, lds);
+        if (cap < std::min(gpl, groups) * p->lr.S)
+            return fail(MC_ERR_UNSUPPORTED,
+                        "lane-resident HMC (expression JIT): %lld workgroups must be co-resident, "
+                        "the device holds %lld of this kernel",
+                        (long long)(std::min(gpl, groups) * p->lr.S), (long long)cap);
+        A.fault = g_exchange_fault;
+    }
+    uint32_t base = 0;
+    if (ws_reserve(ws, per_launch * (uint64_t)nlaunch, (uint64_t)used, &base))
+        MC_HIP_TRY(hipMemsetAsync(ws, 0, used, st));
+    ws_mark_status(ws);
+    mc_chain_scalars* scal = (mc_chain_scalars*)b;
+    float *sq = (float*)(b + qo), *sg = (float*)(b + go);
+    TraceDev td = trace_of(tr);
+    for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
+        int64_t ng = std::min(gpl, groups - g0);
+        const int64_t grid = ng * p->lr.S;
+        int64_t cb = g0 * NB;
+        hipFunction_t k = f;
+        if (!X1 && xcd_round_robin(grid, p->lr.S)) {
+            if (fxl == nullptr) {
+                rc = jit_function(p, name + ", true>", &fxl);
+                if (rc != MC_OK) return rc;
+            }
+            if (fxl != nullptr) k = fxl;
+        }
+        void* args[] = {&ctx, &A, &cb, &ng, &scal, &sq, &sg, &samples, &td, &xch, &status, &base};
+        MC_HIP_TRY(hipModuleLaunchKernel(k, (unsigned)grid, 1, 1, 64 * NW, 1, 1, (unsigned)lds, st,
+                                         args, nullptr));
+        base += (uint32_t)per_launch;
+    }
+    return MC_OK;
+}
 
 template <int RS, int NSH, int NW, bool X1>
 inline int launch_hmc_lr(const mc_program* p, const mc_run_config* cfg, void* state,
                          float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
+    if (p->lr.has_expr) return launch_hmc_lr_jit<RS, NSH, NW, X1>(p, cfg, state, samples, tr, ws, st);
     const bool fast = p->lr.fast && lanes_fast_enabled();
     auto kern = fast ? k_hmc_lf<RS, NSH, NW, X1, -1> : k_hmc_lr<RS, NSH, NW, X1>;
     // the same with L2-resident records (host.h xcd_round_robin): the generic

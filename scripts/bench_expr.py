@@ -18,11 +18,13 @@ from mlx_mcmc_amd import _engine, _lib, _trace
 LIB = _lib.load()
 
 
-def rate(lp, init, chains=256, L=10, eps=1e-3, iters=20, jit=-1):
-    """jit: -1 the default (expression terms compiled), 0 the interpreter."""
+def rate(lp, init, chains=256, L=10, eps=1e-3, iters=20, jit=-1, slices=0):
+    """jit: -1 the default (expression terms compiled), 0 the interpreter;
+    slices: 0 automatic (N = 100 K: the lane-resident kernel with the
+    JIT-compiled LS_EXPR sweep), 1 the chain-per-workgroup tape."""
     LIB.mc_debug_expr_jit(jit)
     t0 = time.perf_counter()
-    prog = _trace.compile_model(lp, init)
+    prog = _trace.compile_model(lp, init, slices=slices)
     t_build = time.perf_counter() - t0
     cs = _engine.ChainSet(prog, chains, prog.layout.flatten(init), eps, device=torch.device("cuda"))
     samples = torch.empty((chains, 1, prog.D), dtype=torch.float32, device="cuda")
@@ -39,7 +41,11 @@ def rate(lp, init, chains=256, L=10, eps=1e-3, iters=20, jit=-1):
     ms = e0.elapsed_time(e1)
     cs.check_status()
     LIB.mc_debug_expr_jit(-1)
-    return chains * iters * L / (ms * 1e-3), t_build, prog.slice_kernel
+    kern = prog.slice_kernel
+    if kern == "lanes" and LIB.mc_program_expr_jit(prog.handle) == 1 and any(
+            t.dist == _lib.MC_DIST_EXPR for t in prog.model.terms):
+        kern = f"lanes + JIT LS_EXPR, {prog.num_slices} slices"
+    return chains * iters * L / (ms * 1e-3), t_build, kern
 
 
 N = 100000
@@ -98,12 +104,13 @@ for sl, name in ((0, "lane-resident (auto)"), (1, "tape (num_slices=1)")):
 lp, _ = W.two_predictor_regression(W.ns_product(), N)
 i2 = {"a": np.float32(0.5), "b1": np.float32(1.2), "b2": np.float32(-0.8),
       "log_sigma": np.float32(-0.5)}
-for jit, nm in ((0, "interpreter"), (-1, "JIT")):
-    r, tb, k = rate(lp, i2, jit=jit)
+VARIANTS = ((0, 1, "tape, interpreter"), (-1, 1, "tape, JIT"), (-1, 0, "auto"))
+for jit, sl, nm in VARIANTS:
+    r, tb, k = rate(lp, i2, jit=jit, slices=sl)
     print(f"two-predictor N={N} expression ({nm}): {r / 1e6:.3f} M chain-steps/s "
-          f"(build {tb:.2f} s)")
+          f"(kernel {k}; build {tb:.2f} s)")
 lp, _ = W.logistic_regression(W.ns_product(), N)
-for jit, nm in ((0, "interpreter"), (-1, "JIT")):
-    r, tb, k = rate(lp, {"a": np.float32(-0.3), "b": np.float32(1.1)}, jit=jit)
+for jit, sl, nm in VARIANTS:
+    r, tb, k = rate(lp, {"a": np.float32(-0.3), "b": np.float32(1.1)}, jit=jit, slices=sl)
     print(f"logistic N={N} expression ({nm}): {r / 1e6:.3f} M chain-steps/s "
-          f"(build {tb:.2f} s)")
+          f"(kernel {k}; build {tb:.2f} s)")
