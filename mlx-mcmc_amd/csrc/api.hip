@@ -1022,11 +1022,14 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
                 if (a < 3) lt.doff[a] = (int32_t)(base - blk0);
                 else lt.xoff = (int32_t)(base - blk0);
             }
-            if (lt.sig == LS_EXPR) {  // the data leaves, in node order
+            if (lt.sig == LS_EXPR) {  // the data leaves' arrays, in node order (one tile each)
                 int e = 0;
+                std::vector<int64_t> seen;
                 for (int k = 0; k < rt.expr_n; ++k) {
                     const DevExprNode& d = p->nodes[rt.expr_base + k];
                     if (d.op != MC_EX_LEAF || d.leaf.kind != MC_OP_DATA) continue;
+                    if (std::find(seen.begin(), seen.end(), d.leaf.pool) != seen.end()) continue;
+                    seen.push_back(d.leaf.pool);
                     if (e >= kLrExprData) return no("an expression with too many data leaves");
                     while (L.data.size() % 4) L.data.push_back(0.0f);
                     const int64_t base = (int64_t)L.data.size();

@@ -1089,6 +1089,23 @@ MC_DEV exf2 ex2_log1p(exf2 x) {
                 d.y == 0.0f ? x.y : (__builtin_isinf(u.y) ? l.y : r.y)};
 }
 MC_DEV exf2 ex2_each(float (*f)(float), exf2 x) { return exf2{f(x.x), f(x.y)}; }
+// ex_normal's operations on a pair (every component rounds as the scalar
+// path): log density, and the value / loc / scale cotangent factors.
+MC_DEV exf2 ex2_normal_lp(float c0, exf2 v, exf2 m, exf2 s) {
+    const exf2 var = s * s;
+    const exf2 d = v - m;
+    const exf2 d2 = d * d;
+    return (c0 - ex2_log(s)) - ex2_div(0.5f * d2, var);
+}
+MC_DEV void ex2_normal_grad(exf2 v, exf2 m, exf2 s, exf2& dv, exf2& dm, exf2& ds) {
+    const exf2 var = s * s;
+    const exf2 d = v - m;
+    const exf2 d2 = d * d;
+    const exf2 t = ex2_div(d, var);
+    dv = -t;
+    dm = t;
+    ds = ex2_div(d2, var * s) - ex2_div(exf2{1.0f, 1.0f}, s);
+}
 
 MC_DEV exf2 ex2_fwd(int op, exf2 x, exf2 y, exf2 z, float c0) {
     switch (op) {
@@ -1102,6 +1119,7 @@ MC_DEV exf2 ex2_fwd(int op, exf2 x, exf2 y, exf2 z, float c0) {
         case MC_EX_SQUARE: return x * x;
         case MC_EX_LOG1P: return ex2_log1p(x);
         case MC_EX_SIGMOID: return ex2_div(exf2{1.0f, 1.0f}, 1.0f + ex2_exp(-x));
+        case MC_EX_NORMAL_LP: return ex2_normal_lp(c0, x, y, z);
         default:  // the rest per component through the scalar path
             return exf2{ex_fwd(op, x.x, y.x, z.x, c0), ex_fwd(op, x.y, y.y, z.y, c0)};
     }
@@ -1121,6 +1139,14 @@ MC_DEV void ex2_bwd(int op, exf2 x, exf2 y, exf2 z, exf2 v, exf2 c, float c0, ex
         case MC_EX_LOG1P: dx = ex2_div(c, 1.0f + x); break;
         case MC_EX_TANH: dx = c * (1.0f - v * v); break;
         case MC_EX_SIGMOID: dx = c * (v * (1.0f - v)); break;
+        case MC_EX_NORMAL_LP: {
+            exf2 gv, gm, gs;
+            ex2_normal_grad(x, y, z, gv, gm, gs);
+            dx = c * gv;
+            dy = c * gm;
+            dz = c * gs;
+            break;
+        }
         default: {
             float ax, ay, az, bx, by, bz;
             ex_bwd(op, x.x, y.x, z.x, v.x, c.x, c0, ax, ay, az);

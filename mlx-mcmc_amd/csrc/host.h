@@ -236,7 +236,7 @@ inline bool affine_lanes_ok(const mc_program* p) {
 // Expression terms the lane-resident kernel takes (lanes.h LS_EXPR, code
 // generated per program by the expression JIT): leaves data, broadcast
 // parameters and constants only — no parameter vectors or gathers — with at
-// least one data leaf and at most kLrExprData of them, one pass.  Every term
+// least one data array and at most kLrExprData of them, one pass.  Every term
 // of the program must qualify (else the program stays on the tape kernels).
 inline bool expr_lanes_ok(const mc_program* p) {
     if (const char* e = std::getenv("MC_EXPR_LANES"))  // 0: the tape (A/B, tests)
@@ -244,15 +244,19 @@ inline bool expr_lanes_ok(const mc_program* p) {
     for (const DevTerm& t : p->raw) {
         if (t.dist != MC_DIST_EXPR) continue;
         if (t.primary >= 0 || t.npass != 1 || t.expr_n < 1) return false;
-        int ndata = 0;
+        std::vector<int64_t> arrays;  // distinct data arrays (one LDS tile each)
         for (int k = 0; k < t.expr_n; ++k) {
             const DevExprNode& d = p->nodes[t.expr_base + k];
             if (d.op != MC_EX_LEAF) continue;
             if (d.prim) return false;
-            if (d.leaf.kind == MC_OP_DATA) ++ndata;
-            else if (d.leaf.kind != MC_OP_CONST && d.leaf.kind != MC_OP_PSCALAR) return false;
+            if (d.leaf.kind == MC_OP_DATA) {
+                if (std::find(arrays.begin(), arrays.end(), d.leaf.pool) == arrays.end())
+                    arrays.push_back(d.leaf.pool);
+            } else if (d.leaf.kind != MC_OP_CONST && d.leaf.kind != MC_OP_PSCALAR) {
+                return false;
+            }
         }
-        if (ndata < 1 || ndata > kLrExprData) return false;
+        if (arrays.empty() || (int)arrays.size() > kLrExprData) return false;
     }
     return true;
 }

@@ -478,66 +478,97 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
                 const int K = ordinal(d.leaf.poff);
                 o << "  const exf2 v" << k << " = {rl(sh.q, " << 2 * K << "), rl(sh.q, " << 2 * K + 1
                   << ")};\n  exf2 p" << k << " = {0.0f, 0.0f};\n";
-            } else {  // data
-                o << "  const float* d" << k << " = sd + T->eoff[" << dleaves.size() << "] + 4 * j;\n";
-                dleaves.push_back(k);
+            } else {  // data: one tile per array (leaves of one array share it)
+                bool dup = false;
+                for (int r : dleaves) dup |= N[r].leaf.pool == d.leaf.pool;
+                if (!dup) {
+                    o << "  const float* d" << k << " = sd + T->eoff[" << dleaves.size()
+                      << "] + 4 * j;\n";
+                    dleaves.push_back(k);
+                }
             }
         } else {
             o << "  const float c" << k << " = " << flit(d.leaf.cval) << ";\n";
         }
     }
-    auto arg = [&](int a) { return a >= 0 ? "v" + std::to_string(a) : std::string("z2"); };
     o << "  const exf2 z2 = {0.0f, 0.0f};\n  (void)z2;\n";
-    o << "  auto element = [&](";
-    for (size_t e = 0; e < dleaves.size(); ++e) o << (e ? ", " : "") << "float x" << dleaves[e];
-    o << ") {\n";
-    for (int k = 0; k < nn; ++k) {
-        const DevExprNode& d = N[k];
-        if (d.op == MC_EX_LEAF) {
-            if (d.leaf.kind == MC_OP_DATA) o << "    const exf2 v" << k << " = {x" << k << ", x" << k << "};\n";
-            continue;
+    // E elements at once, their statements interleaved node by node (the
+    // elements' dependency chains are independent, so the hazards of one —
+    // transcendental results, packed read-after-write — are covered by the
+    // others' instructions); sums in element order.  x[e][i]: element e's
+    // value of data leaf i.
+    auto emit = [&](int E, const std::vector<std::vector<std::string>>& x, const char* ind) {
+        auto nm = [&](char c, int k, int e) {
+            // leaves outside the element (constants, parameters) keep one name
+            const DevExprNode& d = N[k];
+            const bool shared = xf_node(k) >= 0 ||
+                                (d.op == MC_EX_LEAF && d.leaf.kind != MC_OP_DATA);
+            if (c == 'v' && shared) return "v" + std::to_string(k);
+            return std::string(1, c) + std::to_string(k) + "_" + std::to_string(e);
+        };
+        auto argn = [&](int a, int e) { return a >= 0 ? nm('v', a, e) : std::string("z2"); };
+        for (int k = 0; k < nn; ++k) {
+            const DevExprNode& d = N[k];
+            for (int e = 0; e < E; ++e) {
+                if (d.op == MC_EX_LEAF) {
+                    if (d.leaf.kind == MC_OP_DATA) {
+                        size_t i = 0;
+                        while (N[dleaves[i]].leaf.pool != d.leaf.pool) ++i;
+                        o << ind << "const exf2 " << nm('v', k, e) << " = {" << x[e][i] << ", "
+                          << x[e][i] << "};\n";
+                    }
+                    continue;
+                }
+                if (xf_node(k) >= 0) continue;
+                o << ind << "const exf2 " << nm('v', k, e) << " = ex2_fwd(" << d.op << ", "
+                  << argn(d.a, e) << ", " << argn(d.b, e) << ", " << argn(d.c, e) << ", c" << k
+                  << ");\n";
+            }
         }
-        if (xf_node(k) >= 0) continue;
-        o << "    const exf2 v" << k << " = ex2_fwd(" << d.op << ", " << arg(d.a) << ", " << arg(d.b)
-          << ", " << arg(d.c) << ", c" << k << ");\n";
-    }
-    o << "    if constexpr (LP) lpa += wv * v" << nn - 1 << ";\n";
-    // (adjoints start at -0, as the tape's: -0 + x == x)
-    for (int k = 0; k < nn; ++k) o << "    exf2 a" << k << " = {-0.0f, -0.0f};\n";
-    o << "    a" << nn - 1 << " = wv;\n";
-    for (int k = nn - 1; k >= 0; --k) {
-        const DevExprNode& d = N[k];
-        if (d.op == MC_EX_LEAF) {
-            if (raw_leaf(k)) o << "    p" << k << " += a" << k << ";\n";
-            continue;
+        for (int e = 0; e < E; ++e)
+            o << ind << "if constexpr (LP) lpa += wv * " << nm('v', nn - 1, e) << ";\n";
+        // (adjoints start at -0, as the tape's: -0 + x == x)
+        for (int k = 0; k < nn; ++k)
+            for (int e = 0; e < E; ++e)
+                o << ind << "exf2 " << nm('a', k, e) << " = {-0.0f, -0.0f};\n";
+        for (int e = 0; e < E; ++e) o << ind << nm('a', nn - 1, e) << " = wv;\n";
+        for (int k = nn - 1; k >= 0; --k) {
+            const DevExprNode& d = N[k];
+            if (d.op == MC_EX_LEAF && !raw_leaf(k)) continue;
+            for (int e = 0; e < E; ++e) {
+                if (d.op == MC_EX_LEAF || xf_node(k) >= 0) {
+                    o << ind << "p" << k << " += " << nm('a', k, e) << ";\n";
+                    continue;
+                }
+                o << ind << "{ exf2 dx, dy, dz; ex2_bwd(" << d.op << ", " << argn(d.a, e) << ", "
+                  << argn(d.b, e) << ", " << argn(d.c, e) << ", " << nm('v', k, e) << ", "
+                  << nm('a', k, e) << ", c" << k << ", dx, dy, dz);\n"
+                  << ind << "  " << nm('a', d.a, e) << " += dx;";
+                if (d.b >= 0) o << " " << nm('a', d.b, e) << " += dy;";
+                if (d.c >= 0) o << " " << nm('a', d.c, e) << " += dz;";
+                o << " (void)dx; (void)dy; (void)dz; }\n";
+            }
         }
-        if (xf_node(k) >= 0) {
-            o << "    p" << k << " += a" << k << ";\n";
-            continue;
-        }
-        o << "    { exf2 dx, dy, dz; ex2_bwd(" << d.op << ", " << arg(d.a) << ", " << arg(d.b) << ", "
-          << arg(d.c) << ", v" << k << ", a" << k << ", c" << k << ", dx, dy, dz);\n"
-          << "      a" << d.a << " += dx;";
-        if (d.b >= 0) o << " a" << d.b << " += dy;";
-        if (d.c >= 0) o << " a" << d.c << " += dz;";
-        o << " (void)dx; (void)dy; (void)dz; }\n";
-    }
-    o << "  };\n";
-    // four elements per trip: a 16-byte LDS load per data leaf, then the
-    // elements in order; the ragged tail one at a time
+    };
+    // four elements per trip: a 16-byte LDS load per data leaf, the four
+    // elements interleaved; the ragged tail one at a time
     o << "  int u = 0;\n  for (; u + 4 <= len; u += 4) {\n";
     for (int k : dleaves)
         o << "    const float4 X" << k << " = *(const float4*)(d" << k << " + (u >> 2) * 256);\n";
-    const char* comp[4] = {"x", "y", "z", "w"};
-    for (int c = 0; c < 4; ++c) {
-        o << "    element(";
-        for (size_t e = 0; e < dleaves.size(); ++e)
-            o << (e ? ", " : "") << "X" << dleaves[e] << "." << comp[c];
-        o << ");\n";
+    {
+        const char* comp[4] = {"x", "y", "z", "w"};
+        std::vector<std::vector<std::string>> x(4);
+        for (int e = 0; e < 4; ++e)
+            for (int k : dleaves) x[e].push_back("X" + std::to_string(k) + "." + comp[e]);
+        emit(4, x, "    ");
     }
-    o << "  }\n  for (; u < len; ++u) {\n    const int ou = (u >> 2) * 256 + (u & 3);\n    element(";
-    for (size_t e = 0; e < dleaves.size(); ++e) o << (e ? ", " : "") << "d" << dleaves[e] << "[ou]";
-    o << ");\n  }\n"
+    o << "  }\n  for (; u < len; ++u) {\n    const int ou = (u >> 2) * 256 + (u & 3);\n";
+    {
+        std::vector<std::vector<std::string>> x(1);
+        for (int k : dleaves) x[0].push_back("d" + std::to_string(k) + "[ou]");
+        emit(1, x, "    ");
+    }
+    o << "  }\n"
       << "  if constexpr (LP) {\n    lpp[0] += lpa.x;\n    lpp[1] += lpa.y;\n  }\n";
     for (int k = 0; k < nn; ++k) {
         int K = xf_node(k);
