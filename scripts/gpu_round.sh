@@ -23,6 +23,9 @@
 #                                                          the HBM bytes per launch go to
 #                                                          gpurun_out/TAG_traffic.json under
 #                                                          KEY@IPL (bench.py pmc_traffic)
+#   bash scripts/gpu_round.sh traffic TAG NAME KERNEL IPL KEY [bench args]
+#                                                          the FETCH / WRITE passes only: the
+#                                                          traffic record KEY@IPL
 #   bash scripts/gpu_round.sh ab TAG LIB... [-- bench args] A/B of library builds on one box
 #                                                          ("-" = the in-tree build)
 #   bash scripts/gpu_round.sh final TAG                    tests + smoke + bench-lines
@@ -90,6 +93,11 @@ case $STEP in
     prof sq1_$n "$*" --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_SMEM &&
     prof sq2_$n "$*" --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU_TRANS_F32 SQ_INST_CYCLES_SALU &&
     python scripts/pmc_sq.py gpurun_out/${TAG}_sq_$n.json "$k" "$ipl" "$lf" --floor "$fl" gpurun_out/${TAG}_sq1_$n gpurun_out/${TAG}_sq2_$n &&
+    python scripts/pmc_traffic.py gpurun_out/${TAG}_fetch_$n gpurun_out/${TAG}_write_$n "$key" "$ipl" \
+        "profiles/$TAG: fetch_$n|write_$n (bench.py $*)" --kernel "$k" --out gpurun_out/${TAG}_traffic.json ;;
+  traffic)  # NAME KERNEL IPL KEY [bench args]: the FETCH / WRITE passes and the traffic record
+    n=$1; k=$2; ipl=$3; key=$4; shift 4
+    prof fetch_$n "$*" --pmc FETCH_SIZE && prof write_$n "$*" --pmc WRITE_SIZE &&
     python scripts/pmc_traffic.py gpurun_out/${TAG}_fetch_$n gpurun_out/${TAG}_write_$n "$key" "$ipl" \
         "profiles/$TAG: fetch_$n|write_$n (bench.py $*)" --kernel "$k" --out gpurun_out/${TAG}_traffic.json ;;
   ab)
