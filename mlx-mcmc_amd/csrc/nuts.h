@@ -68,32 +68,6 @@ MC_DEV bool no_u_turn(const float* qm, const float* qp, const float* rm, const f
 
 MC_DEV int ctz_u32(uint32_t x) { return __builtin_ctz(x); }
 
-// The merge draws of one subtree build, 64 at a time in vector form (the
-// lane-resident NUTS kernels; nuts.py:205's U of each merge).  The iterative
-// walk of a depth-jd subtree merges in post-order: leaf k closes levels
-// 0 .. ctz(k + 1) - 1, and the merges before leaf k number f(k) = k -
-// popcount(k) (sum over k' < k of ctz(k' + 1)), so merge m of the walk is
-// level m - f(k) of the leaf k with f(k) <= m < f(k + 1).  Lane i of batch b
-// finds the (k, l) of merge 64 b + i by a binary search over f and draws its
-// Philox block (the key of nuts.h: depth jd, (l << 20) | k) — one vector
-// Philox per 64 merges instead of a scalar one (~100 SALU) per merge.  The
-// draws are the same blocks, so the trees are unchanged.
-MC_DEV uint32_t nuts_merge_batch(uint64_t seed, uint32_t chain, uint32_t it, int jd, int m) {
-    const int nleaf = 1 << jd;
-    if (m >= nleaf - 1) return 0u;  // (past the subtree's last merge: unused)
-    // the smallest x in [1, nleaf] with f(x) > m; then k = x - 1
-    int lo = 1, hi = nleaf;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (mid - __builtin_popcount((uint32_t)mid) > m) hi = mid;
-        else lo = mid + 1;
-    }
-    const int k = lo - 1;
-    const int l = m - (k - __builtin_popcount((uint32_t)k));
-    return mc_draw(seed, chain, it, MC_RNG_TAG_MERGE, (uint32_t)jd,
-                   ((uint32_t)l << 20) | (uint32_t)k).x;
-}
-
 // LDS_ARENA: the arena lives in the workgroup's LDS after the group scratch
 // and the pending words (every trajectory vector one LDS round trip away
 // instead of an L2 one); else in the global workspace.

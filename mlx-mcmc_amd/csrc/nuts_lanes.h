@@ -518,22 +518,6 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
             }
 
             // ---- build_tree(jd) iteratively ---------------------------------
-            // the merge draws, 64 at a time (nuts.h nuts_merge_batch): lane i
-            // holds merge 64 ub + i's Philox word
-            int ub = -1;
-            uint32_t ubx = 0u;
-            auto merge_draw = [&](int m) -> uint32_t {
-                const int b = m >> 6;
-                if (b != ub) {
-                    ub = b;
-                    ubx = nuts_merge_batch(cfg.seed, chain_id, (uint32_t)it, jd, 64 * b + j);
-                }
-                return (uint32_t)__builtin_amdgcn_readlane((int)ubx, m & 63);
-            };
-            if (jd >= 1) {  // the first batch now: its latency hides under the first leaf
-                ub = 0;
-                ubx = nuts_merge_batch(cfg.seed, chain_id, (uint32_t)it, jd, j);
-            }
             uint32_t freemask = (1u << (MAXJ + 2)) - 1u;
             bool s_sub = true;
             int cand = -1, cn = 0;
@@ -554,6 +538,12 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                         ar0[r] = in ? *at(0, s0, 1, r) : 0.0f;
                     }
                 }
+                // and that merge's draw (scalar Philox: its instructions fill
+                // the leaf's dependency stalls; in the merge it was on the
+                // critical path)
+                uint32_t u0 = 0;
+                if (k & 1) u0 = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_MERGE,
+                                        (uint32_t)jd, (uint32_t)k).x;
                 // leaf: leapfrog_step(theta, r, v*eps) + hamiltonian (nuts.py:160-164)
                 // (both packed halves in one instruction each: the same IEEE
                 // operations as the per-half form)
@@ -661,8 +651,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     }
                     const int pidx = __builtin_amdgcn_readlane(pend_idx, l);
                     const int pn = __builtin_amdgcn_readlane(pend_n, l);
-                    // merge (k, l) is merge k - popcount(k) + l of the walk
-                    const uint32_t ux = merge_draw(k - __builtin_popcount((uint32_t)k) + l);
+                    const uint32_t ux =
+                        l == 0 ? u0
+                               : mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_MERGE,
+                                         (uint32_t)jd, ((uint32_t)l << 20) | (uint32_t)k).x;
                     const double den = (double)(pn + cn) > 1.0 ? (double)(pn + cn) : 1.0;
                     // U < cn / den (nuts.py:205) as U * den < cn: exact in f64 (U a
                     // multiple of 2^-24, den < 2^24), the same decision as the
