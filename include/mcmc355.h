@@ -177,12 +177,17 @@ typedef enum {
     MC_EX_NORMAL_LP      = 15,  /* Normal(b, c).log_prob(a)  normal.py:49-56 */
     MC_EX_HALFNORMAL_LP  = 16,  /* HalfNormal(c).log_prob(a) halfnormal.py:43-63 */
     MC_EX_EXPONENTIAL_LP = 17,  /* Exponential(c).log_prob(a) exponential.py:48-71 */
-    MC_EX_WHERE   = 18,  /* a != 0 ? b : c, a a CONST / DATA leaf (mx.where  */
-                         /* over a data mask; no cotangent through a)        */
+    MC_EX_WHERE   = 18,  /* a != 0 ? b : c, a a CONST / DATA leaf or a       */
+                         /* comparison node (mx.where over a data mask or a  */
+                         /* traced condition; no cotangent through a)        */
     MC_EX_GAMMA_LP = 19, /* Gamma(b, c).log_prob(a)  gamma.py:48-88: gammaln */
                          /* (b) at the current value, no cotangent through it */
-    MC_EX_BETA_LP  = 20  /* Beta(b, c).log_prob(a)   beta.py:45-91: log B(b, */
+    MC_EX_BETA_LP  = 20, /* Beta(b, c).log_prob(a)   beta.py:45-91: log B(b, */
                          /* c) at the current values, no cotangent through it */
+    MC_EX_GT       = 21, /* a > b  as 1 / 0 (mx.greater: a mask, no cotangent) */
+    MC_EX_GE       = 22, /* a >= b                                           */
+    MC_EX_LT       = 23, /* a < b                                            */
+    MC_EX_LE       = 24  /* a <= b                                           */
 } mc_expr_op;
 
 typedef struct mc_expr_node {

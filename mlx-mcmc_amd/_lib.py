@@ -45,7 +45,7 @@ MC_DIST_EXPR = 6
 (MC_EX_LEAF, MC_EX_ADD, MC_EX_SUB, MC_EX_MUL, MC_EX_DIV, MC_EX_NEG, MC_EX_EXP, MC_EX_LOG,
  MC_EX_SQRT, MC_EX_SQUARE, MC_EX_POW, MC_EX_ABS, MC_EX_LOG1P, MC_EX_TANH, MC_EX_SIGMOID,
  MC_EX_NORMAL_LP, MC_EX_HALFNORMAL_LP, MC_EX_EXPONENTIAL_LP, MC_EX_WHERE,
- MC_EX_GAMMA_LP, MC_EX_BETA_LP) = range(21)
+ MC_EX_GAMMA_LP, MC_EX_BETA_LP, MC_EX_GT, MC_EX_GE, MC_EX_LT, MC_EX_LE) = range(25)
 MC_EXPR_MAX_NODES = 32
 
 # mc_series_stats fields (include/mcmc355.h)

@@ -51,7 +51,8 @@ and beta.py:59-91).  What raises ``TraceError``, and why:
 
 * a Python branch on a parameter value (``float(theta)``, ``if theta > 0``):
   the model is traced once, so a branch would freeze one side of it;
-* ``mx.where`` over a traced condition (the mask must be data, core.py);
+* ``mx.where`` over a traced condition other than one comparison of traced
+  values (x > y, mx.less(x, y) ...: a comparison node, no cotangent);
 * indexing a parameter expression or a log density (``(a + b * x)[i]``,
   ``lp[i]``): index the parameter or the data before combining them;
 * a log density multiplied by a traced value (``lp * theta``): a term's
@@ -83,17 +84,27 @@ _UNSUPPORTED = (
     "expressions of them")
 
 
-def _compare_error(what):
-    def f(self, *a, **k):
-        raise TraceError(f"comparison of {what(self)} (x < y, x > 0: a Python branch or "
-                         "mask on a parameter value cannot be traced; masks must be data): "
-                         + _UNSUPPORTED)
-    return f
+_COMPARE_OPS = (_lib.MC_EX_GT, _lib.MC_EX_GE, _lib.MC_EX_LT, _lib.MC_EX_LE)
+
+
+def _comparisons(cls):
+    """x < y, x <= y, x > y, x >= y of traced values: a comparison expression
+    node (a 1 / 0 mask, no cotangent, as mx.greater / mx.less), usable as the
+    condition of mx.where; a Python branch on it (bool()) raises TraceError."""
+    ops = {"__lt__": "MC_EX_LT", "__le__": "MC_EX_LE", "__gt__": "MC_EX_GT",
+           "__ge__": "MC_EX_GE"}
+    for name, op in ops.items():
+        def f(self, other, _op=op):
+            return Expr.binary(getattr(_lib, _op), self, other)
+        f.__name__ = name
+        setattr(cls, name, f)
+    return cls
 
 
 # ---------------------------------------------------------------------------
 # symbolic values
 # ---------------------------------------------------------------------------
+@_comparisons
 class Param:
     """A parameter (or a view of one) during tracing."""
 
@@ -234,8 +245,6 @@ class Param:
     def __abs__(self):
         return Expr.unary(_lib.MC_EX_ABS, self)
 
-    __lt__ = __le__ = __gt__ = __ge__ = _compare_error(lambda p: f"traced parameter '{p.name}'")
-
     def __float__(self):
         raise TraceError(f"float() of traced parameter '{self.name}' (a Python branch on a "
                          "parameter value cannot be traced): " + _UNSUPPORTED)
@@ -264,6 +273,7 @@ def _is_term_operand(x) -> bool:
     return not isinstance(x, (Affine, LogProbExpr, Expr))
 
 
+@_comparisons
 class Affine:
     """A traced affine location ``loc + slope * x`` (mc_affine): one product
     and one sum per element, rounded in f32 as the reference's MLX ops."""
@@ -380,8 +390,6 @@ class Affine:
         raise TraceError("indexing a traced parameter expression ((a + b * x)[i]: index the "
                          "parameter or the data before the arithmetic): " + _UNSUPPORTED)
 
-    __lt__ = __le__ = __gt__ = __ge__ = _compare_error(lambda e: "a traced parameter expression")
-
     def __float__(self):
         raise TraceError("float() of a traced parameter expression: " + _UNSUPPORTED)
 
@@ -416,6 +424,7 @@ def _bshape(name: str, shapes) -> Tuple[int, ...]:
     return vec[0] if vec else ()
 
 
+@_comparisons
 class Expr:
     """A traced elementwise expression (MC_DIST_EXPR nodes, include/mcmc355.h
     mc_expr_node): op an MC_EX_* code, args its argument Exprs; a leaf holds
@@ -470,11 +479,19 @@ class Expr:
 
     @staticmethod
     def where(mask, a, b) -> "Expr":
-        m = np.asarray(_to_numpy(mask))
-        if m.dtype == object:
-            raise TraceError("mx.where over a traced condition (the mask must be data): "
-                             + _UNSUPPORTED)
-        em = Expr.of(m.astype(np.float32))
+        if is_symbolic(mask):
+            # a traced condition: a comparison of traced values (no cotangent
+            # through it, as mx.where's VJP)
+            if not (isinstance(mask, Expr) and mask.op in _COMPARE_OPS):
+                raise TraceError("mx.where over a traced condition other than one comparison "
+                                 "(x > y, x < y, x >= y, x <= y of traced values): "
+                                 + _UNSUPPORTED)
+            em = mask
+        else:
+            m = np.asarray(_to_numpy(mask))
+            if m.dtype == object:
+                raise TraceError("mx.where over an unsupported condition: " + _UNSUPPORTED)
+            em = Expr.of(m.astype(np.float32))
         ea, eb = Expr.of(a), Expr.of(b)
         e = Expr(_lib.MC_EX_WHERE, [em, ea, eb],
                  shape=_bshape("mx.where", [em.shape, ea.shape, eb.shape]))
@@ -526,8 +543,6 @@ class Expr:
     def __getitem__(self, item):
         raise TraceError("indexing a traced expression (expr[i]: index the parameter or the "
                          "data before the arithmetic): " + _UNSUPPORTED)
-
-    __lt__ = __le__ = __gt__ = __ge__ = _compare_error(lambda e: "a traced expression")
 
     def __float__(self):
         raise TraceError("float() of a traced expression (a Python branch on a parameter value "

@@ -153,11 +153,16 @@ isnan = _concrete("isnan", np.isnan)
 isinf = _concrete("isinf", np.isinf)
 
 
+greater = _binary("greater", _trace._lib.MC_EX_GT, np.greater)
+greater_equal = _binary("greater_equal", _trace._lib.MC_EX_GE, np.greater_equal)
+less = _binary("less", _trace._lib.MC_EX_LT, np.less)
+less_equal = _binary("less_equal", _trace._lib.MC_EX_LE, np.less_equal)
+
+
 def where(cond, a, b):
-    if _trace.is_symbolic(cond):
-        raise _trace.TraceError("mx.where over a traced condition (a Python-free branch on a "
-                                "parameter value; the mask must be data): " + _trace._UNSUPPORTED)
-    if _trace.is_symbolic(a, b):
+    """mx.where: over a data mask, or over a traced condition (a comparison of
+    traced values; no cotangent through the condition, as mx.where's VJP)."""
+    if _trace.is_symbolic(cond, a, b):
         return _trace.Expr.where(cond, a, b)
     return np.where(cond, a, b)
 

@@ -1410,7 +1410,7 @@ static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, 
         d.c = s.c;
         d.leaf.kind = MC_OP_NONE;
         d.leaf.slot = -1;
-        if (s.op < MC_EX_LEAF || s.op > MC_EX_BETA_LP)
+        if (s.op < MC_EX_LEAF || s.op > MC_EX_LE)
             return fail(MC_ERR_INVALID, "term %d node %d: unknown op %d", t, k, s.op);
         if (s.op == MC_EX_LEAF) {
             const mc_operand& o = s.leaf;
@@ -1465,6 +1465,7 @@ static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, 
         bool ua = true, ub = false, uc = false;
         switch (s.op) {
             case MC_EX_ADD: case MC_EX_SUB: case MC_EX_MUL: case MC_EX_DIV: case MC_EX_POW:
+            case MC_EX_GT: case MC_EX_GE: case MC_EX_LT: case MC_EX_LE:
                 ub = true;
                 break;
             case MC_EX_NORMAL_LP: case MC_EX_WHERE: case MC_EX_GAMMA_LP: case MC_EX_BETA_LP:
@@ -1480,11 +1481,12 @@ static int build_expr_term(int32_t t, const mc_term& src, const mc_expr* exprs, 
         if (!arg_ok(s.a, ua) || !arg_ok(s.b, ub) || !arg_ok(s.c, uc))
             return fail(MC_ERR_INVALID, "term %d node %d: bad arguments (%d, %d, %d) for op %d", t,
                         k, s.a, s.b, s.c, s.op);
-        if (s.op == MC_EX_WHERE && !(en[s.a].op == MC_EX_LEAF &&
-                                     (en[s.a].leaf.kind == MC_OP_CONST ||
-                                      en[s.a].leaf.kind == MC_OP_DATA)))
-            return fail(MC_ERR_UNSUPPORTED, "term %d node %d: a where mask must be data or a "
-                        "constant", t, k);
+        if (s.op == MC_EX_WHERE &&
+            !(en[s.a].op == MC_EX_LEAF &&
+              (en[s.a].leaf.kind == MC_OP_CONST || en[s.a].leaf.kind == MC_OP_DATA)) &&
+            !(en[s.a].op >= MC_EX_GT && en[s.a].op <= MC_EX_LE))
+            return fail(MC_ERR_UNSUPPORTED, "term %d node %d: a where mask must be data, a "
+                        "constant or a comparison", t, k);
         // the distribution nodes' f32 normalisers (elem_normal / elem_halfnormal)
         if (s.op == MC_EX_NORMAL_LP) d.leaf.cval = dist_c0(MC_DIST_NORMAL);
         if (s.op == MC_EX_HALFNORMAL_LP) d.leaf.cval = dist_c0(MC_DIST_HALFNORMAL);

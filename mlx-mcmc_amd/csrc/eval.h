@@ -980,6 +980,12 @@ MC_DEV float ex_fwd(int op, float x, float y, float z, float c0) {
         case MC_EX_WHERE: return x != 0.0f ? y : z;
         case MC_EX_GAMMA_LP: return ex_gamma_lp(x, y, z);
         case MC_EX_BETA_LP: return ex_beta_lp(x, y, z);
+        // comparisons: 1 / 0 masks (false for a NaN operand, as mx.greater's);
+        // their reverse step is zero (ex_bwd's default)
+        case MC_EX_GT: return x > y ? 1.0f : 0.0f;
+        case MC_EX_GE: return x >= y ? 1.0f : 0.0f;
+        case MC_EX_LT: return x < y ? 1.0f : 0.0f;
+        case MC_EX_LE: return x <= y ? 1.0f : 0.0f;
         default: return 0.0f;
     }
 }

@@ -91,6 +91,22 @@ def sigmoid(x):
     return torch.sigmoid(_t(x))
 
 
+def greater(a, b):
+    return torch.gt(_t(a), _t(b))
+
+
+def greater_equal(a, b):
+    return torch.ge(_t(a), _t(b))
+
+
+def less(a, b):
+    return torch.lt(_t(a), _t(b))
+
+
+def less_equal(a, b):
+    return torch.le(_t(a), _t(b))
+
+
 def where(c, a, b):
     c = _t(c)
     return torch.where(c if c.dtype == torch.bool else c != 0, _t(a), _t(b))

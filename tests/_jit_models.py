@@ -25,6 +25,7 @@ MODELS = {"two_predictor": W.two_predictor_regression,
           "cauchy": W.cauchy_location,
           "gamma_beta": W.gamma_beta_regression,
           "axis_reductions": W.axis_reductions,
+          "huber": W.huber_regression,
           "tiny_scalar": tiny_scalar}
 
 

@@ -53,3 +53,52 @@ def test_jit_source_is_data_independent():
         srcs.append(_source(h))
         lib.mc_program_destroy(h)
     assert srcs[0] == srcs[1]
+
+
+def _lane_source(h):
+    from mlx_mcmc_amd import _lib
+
+    lib = _lib.load()
+    n = lib.mc_debug_expr_jit_lane_source(h, None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    lib.mc_debug_expr_jit_lane_source(h, buf, n + 1)
+    return buf.value.decode()
+
+
+@pytest.mark.parametrize("model,nsh", [("logistic", 3), ("two_predictor", 4), ("huber", 3)])
+def test_lane_expression_source_compiles(model, nsh):
+    """GLM expression programs sliced onto the lane-resident layout (lanes.h
+    LS_EXPR): the host planner takes them, and the generated lane code
+    (jit.hip gen_lane_term) compiles into k_hmc_lr with the sliced exchange
+    (8 slices, 4 waves) and its L2-resident variant."""
+    from mlx_mcmc_amd import _lib
+
+    lib = _lib.load()
+    lp, init = MODELS[model](W.ns_product(), 20_000)
+    h = host_program(lp, init)
+    try:
+        assert lib.mc_debug_lane_plan_host(h, 8) == 0, (lib.mc_last_error() or b"").decode()
+        src = _lane_source(h)
+        assert "mc_jit_lane_expr" in src and "ex2_fwd(" in src and "#include \"lanes.h\"" in src
+        for xl in ("false", "true"):
+            k = f"mc::k_hmc_lr<1, {nsh}, 4, false, {xl}>"
+            rc = lib.mc_debug_expr_jit_compile(h, k.encode())
+            assert rc == 0, (lib.mc_last_error() or b"").decode()[:3000]
+    finally:
+        lib.mc_program_destroy(h)
+
+
+def test_lane_plan_declines_vector_leaves():
+    """An expression with a gathered parameter vector (varying slopes) is not
+    a lane-resident expression program: the planner declines it (the tape
+    runs it)."""
+    from mlx_mcmc_amd import _lib
+
+    lib = _lib.load()
+    lp, init = W.varying_slopes(W.ns_product())
+    h = host_program(lp, init)
+    try:
+        assert lib.mc_debug_lane_plan_host(h, 4) != 0
+        assert _lane_source(h) == ""
+    finally:
+        lib.mc_program_destroy(h)

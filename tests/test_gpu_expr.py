@@ -41,6 +41,7 @@ MODELS = {"two_predictor": W.two_predictor_regression,
           "cauchy": W.cauchy_location,
           "gamma_beta": W.gamma_beta_regression,
           "axis_reductions": W.axis_reductions,
+          "huber": W.huber_regression,
           "tiny_scalar": tiny_scalar}
 POSITIVE = ("sigma", "v")
 
@@ -103,6 +104,8 @@ def test_expr_nan_and_support(gpu):
     ("gamma_beta", {"b0": 0.3, "b1": 0.2, "c0": 0.0, "c1": 0.5, "log_a": 1.0, "log_phi": 2.0},
      1e-4, 4),
     ("axis_reductions", {"a": 0.4, "b": 1.4, "log_sigma": -0.4}, 0.01, 5),
+    # mx.where over a traced condition (|residual| < c: comparison nodes)
+    ("huber", {"a": 0.4, "b": 1.3}, 0.01, 6),
 ])
 def test_expr_hmc_trace_matches_oracle(gpu, model, start, eps, seed):
     import mlx_mcmc_amd as m

@@ -32,6 +32,8 @@ N = 100_000
 def _start(model):
     if model == "logistic":
         return W.logistic_regression, {"a": np.float32(-0.3), "b": np.float32(1.1)}
+    if model == "huber":
+        return W.huber_regression, {"a": np.float32(0.4), "b": np.float32(1.3)}
     x1, x2, y = W.two_predictor_data(N)
     X = np.stack([np.ones(N), x1, x2], 1).astype(np.float64)
     beta, *_ = np.linalg.lstsq(X, y.astype(np.float64), rcond=None)
@@ -41,7 +43,8 @@ def _start(model):
         "log_sigma": np.float32(np.log(np.std(res)))}
 
 
-@pytest.mark.parametrize("model,eps,seed", [("logistic", 2e-3, 11), ("two_predictor", 1e-3, 12)])
+@pytest.mark.parametrize("model,eps,seed", [("logistic", 2e-3, 11), ("two_predictor", 1e-3, 12),
+                                            ("huber", 1e-3, 13)])
 def test_expr_lanes_hmc_matches_oracle(gpu, model, eps, seed):
     import mlx_mcmc_amd as m
     from mlx_mcmc_amd import _lib, _trace

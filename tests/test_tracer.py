@@ -137,14 +137,14 @@ X3 = np.arange(3, dtype=np.float32)
 # Constructs that still raise: each error names its construct
 @pytest.mark.parametrize("bad,names", [
     (lambda p: m.Normal(0, 1).log_prob(p["x"]) if p["x"] > 0 else 0,     # Python branch
-     "comparison of traced parameter 'x'"),
+     "a Python branch on a parameter value"),
     (lambda p: m.Normal(0, 1).log_prob(p["v"]), "must return a scalar"),  # unsummed vector
     (lambda p: m.Normal(0, 1).log_prob(p["x"]) + p["v"],                   # unsummed identity
      "adding a scalar log density to an unsummed vector one"),
     (lambda p: mx.sum(m.Normal(0, 1).log_prob((p["v"] * 2.0)[0])),         # indexing an expr
      "indexing a traced"),
-    (lambda p: mx.sum(mx.where(p["v"] > 0, p["v"], 0.0)),                   # traced where mask
-     "comparison of traced parameter 'v'"),
+    (lambda p: mx.sum(mx.where((p["v"] > 0) * 1.0, p["v"], 0.0)),           # arithmetic mask
+     "mx.where over a traced condition other than one comparison"),
     (lambda p: m.Normal(0, 1).log_prob(p["x"]) * p["x"],                   # density x parameter
      "a log density times a traced value"),
     (lambda p: mx.sum(m.Normal(0, 1).log_prob(p["v"]) * X3),               # per-element weights
@@ -197,6 +197,9 @@ def _deep(x, k):
     lambda p: mx.sum(m.Beta(p["y"] * 4.0, (1.0 - p["y"]) * 4.0).log_prob(X3 * 0.2 + 0.1)),
     lambda p: m.Beta(2.0, 3.0).log_prob(mx.sigmoid(p["x"])),     # Beta of an expression
     lambda p: mx.mean(-0.5 * mx.square(p["v"] - X3)),             # mx.mean of an expression
+    lambda p: mx.sum(mx.where(p["v"] > 0, p["v"], 0.0)),          # a traced condition
+    lambda p: mx.sum(mx.where(mx.abs(p["v"] - X3) < p["x"], mx.square(p["v"]), p["v"])),
+    lambda p: mx.sum(mx.where(mx.less_equal(X3, p["v"]), 1.0, -mx.square(p["v"]))),
 ])
 def test_general_expressions_trace(good):
     tm = _trace.trace(good, {"x": 1.0, "y": 0.5, "v": np.zeros(3, np.float32)})

@@ -334,6 +334,31 @@ def two_predictor_regression(ns, n=1000):
                       "log_sigma": np.float32(0.0)}
 
 
+def huber_data(n=1000, seed=8):
+    rng = np.random.default_rng(seed)
+    x = rng.normal(0.0, 1.0, n).astype(np.float32)
+    noise = np.where(rng.random(n) < 0.1, rng.normal(0.0, 6.0, n), rng.normal(0.0, 0.5, n))
+    y = (0.4 + 1.3 * x + noise).astype(np.float32)
+    return x, y
+
+
+def huber_regression(ns, n=1000, c=1.0):
+    """A robust regression: the Huber loss of the residuals as the negative
+    log density, its two branches chosen by mx.where over a traced condition
+    (|r| < c, a comparison of a parameter expression)."""
+    x, y = huber_data(n)
+
+    def log_prob(params):
+        a, b = params["a"], params["b"]
+        lp = ns.Normal(0, 10).log_prob(a) + ns.Normal(0, 10).log_prob(b)
+        r = ns.array(y) - (a + b * ns.array(x))
+        ar = ns.abs(r)
+        loss = ns.where(ar < c, 0.5 * (r * r), c * ar - 0.5 * c * c)
+        return lp - ns.sum(loss)
+
+    return log_prob, {"a": np.float32(0.4), "b": np.float32(1.3)}
+
+
 def logistic_data(n=500, seed=6):
     rng = np.random.default_rng(seed)
     x = rng.normal(0.0, 1.0, n).astype(np.float32)
