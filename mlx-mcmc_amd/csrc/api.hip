@@ -858,7 +858,7 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
     L.gidx.assign((size_t)S * kLrMaxSlots * 64, -1);
     L.sdata_floats = 0;
     std::vector<int> lane_of(p->D, -1), slot_of_p(p->D, -1);
-    bool any_rest = false;
+    bool any_rest = false, any_rest_nonexpr = false;
     for (int s = 0; s < S; ++s) {
         // ---- parameters -> (lane, slot) ----
         const std::vector<int>& pv = part.priv[s];
@@ -1080,9 +1080,13 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
         }
         // fast form (lanes_fast.h): one swept term with data value and private
         // loc at most, one direct term at most, nothing else
-        if (!rest.empty() || swept.size() > 1 || direct.size() > 1 ||
-            (!swept.empty() && swept[0].sig != LS_DATA_PP_SH && swept[0].sig != LS_DATA_PP_C))
-            any_rest = true;
+        const bool core = !(swept.size() > 1 || direct.size() > 1 ||
+                            (!swept.empty() && swept[0].sig != LS_DATA_PP_SH &&
+                             swept[0].sig != LS_DATA_PP_C));
+        if (!rest.empty() || !core) any_rest = true;
+        bool rest_expr = true;  // every other term an expression term (LanePlan::nuts_expr)
+        for (const LrTerm& lt : rest) rest_expr &= lt.sig == LS_EXPR;
+        if (!rest_expr || !core) any_rest_nonexpr = true;
         for (const LrTerm& lt : swept) L.terms[(size_t)s * nT + nact++] = lt;
         for (const LrTerm& lt : direct) L.terms[(size_t)s * nT + nact++] = lt;
         for (const LrTerm& lt : rest) L.terms[(size_t)s * nT + nact++] = lt;
@@ -1137,6 +1141,7 @@ static int plan_lanes(const mc_program* p, const SlicePlan& SP, const SlPartitio
     if (L.data.empty()) L.data.assign(4, 0.0f);
     plan_lane_rng(L, S);
     L.fast = (!any_rest && lf_generic == 0) ? 1 : 0;
+    L.nuts_expr = (L.has_expr && !any_rest_nonexpr && lf_generic == 0) ? 1 : 0;
     L.form = L.fast ? lanes_form(L, nT) : -1;
     L.ok = 1;
     return MC_OK;

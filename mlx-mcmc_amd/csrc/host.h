@@ -98,6 +98,9 @@ struct LanePlan {
                          // (no NUTS lanes, no term interpreter)
     int has_expr = 0;    // LS_EXPR terms: only the JIT-compiled k_hmc_lr runs the plan
                          // (jit.hip); without it the program runs on the tape
+    int nuts_expr = 0;   // LS_EXPR terms beside a fast form (every other term swept /
+                         // direct, every scalar term an own prior): the JIT-compiled
+                         // run-time form of k_nuts_sl takes the program
     std::string why;     // why it does not qualify
     std::vector<LrTerm> terms;
     std::vector<float> data;

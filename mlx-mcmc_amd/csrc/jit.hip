@@ -418,33 +418,43 @@ std::string flit(float v) {
 }
 
 // One LS_EXPR term's lane sweep: lane j's run of the term's elements in its
-// slice (a chunk term: slot 0, lengths at len_off), both chains of the wave
-// packed per element (exf2 = chain 0, chain 1), every node's forward value
-// and reverse step through eval.h ex2_fwd / ex2_bwd (the tape's arithmetic,
-// component for component), the broadcast leaves' adjoints summed over the
-// run in element order.  Data leaf e is tile eoff[e] (node order); a
-// broadcast leaf reads the raw parameter of shared ordinal K (lane 2K + c of
-// sh.q, the planner keeps expression-read parameters untransformed).
-// Constants are literals.  LP = false leaves out what only log p needs (the
-// compiler drops the nodes no adjoint reads).
+// slice (a chunk term: slot 0, lengths at len_off), every node's forward
+// value and reverse step through eval.h ex2_fwd / ex2_bwd (the tape's
+// arithmetic, component for component), the broadcast leaves' adjoints
+// summed over the run.  Data leaf e is tile eoff[e] (one tile per data
+// array, in node order).  Constants are literals.  LP = false leaves out
+// what only log p needs (the compiler drops the nodes no adjoint reads).
+//   two chains (k_hmc_lr, ONE = false): the wave's two chains packed per
+//     element (exf2 = chain 0, chain 1); a broadcast leaf reads the raw
+//     parameter of shared ordinal K from lane 2K + c of sh.q;
+//   one chain (k_nuts_sl, ONE = true): two elements packed (exf2 = elements
+//     e, e + 1 of the chain); lane K of sh.q holds shared ordinal K; the
+//     pairs' two sums are added at the end.
+// A transformed broadcast parameter (LanePlan::shxf) is read through its
+// transform node only (the planner checks it): that node reads the lane's
+// transformed value sh.v and its adjoint is the value's cotangent.
 void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N,
-                   const LanePlan& L) {
+                   const LanePlan& L, bool one) {
     const int nn = T.expr_n;
     auto ordinal = [&](int poff) {
         for (int k = 0; k < L.Dsh; ++k)
             if (L.shl[k] == poff) return k;
         return 0;
     };
+    auto sh_read = [&](const char* f, int K) {  // both components of shared ordinal K
+        std::ostringstream x;
+        if (one) x << "exf2{rl(sh." << f << ", " << K << "), rl(sh." << f << ", " << K << ")}";
+        else x << "exf2{rl(sh." << f << ", " << 2 * K << "), rl(sh." << f << ", " << 2 * K + 1 << ")}";
+        return x.str();
+    };
     o << "template <bool LP>\n"
-      << "MC_DEV void jit_lt" << T.expr_base
+      << "MC_DEV void jit_l" << (one ? "o" : "t") << T.expr_base
       << "(const MC_CONST LrTerm* T, const float* sd, int j, const LrShared& sh,\n"
-      << "    float (&lpp)[2], float (&gshp)[kLrMaxShared][2]) {\n"
+      << (one ? "    float& lpp, float (&gsh)[kLrMaxShared]) {\n"
+              : "    float (&lpp)[2], float (&gshp)[kLrMaxShared][2]) {\n")
       << "  const int len = ((const int32_t*)sd)[T->len_off + j];\n"
       << "  const exf2 wv = {T->weight, T->weight};\n"
-      << "  exf2 lpa = {0.0f, 0.0f};\n  (void)lpa;\n";
-    // a transformed broadcast parameter (LanePlan::shxf) is read through its
-    // transform node only (the planner checks it): that node reads the lane's
-    // transformed value sh.v and its adjoint is the value's cotangent
+      << "  exf2 lpa = {0.0f, 0.0f}, lpt = {0.0f, 0.0f};\n  (void)lpa; (void)lpt;\n";
     auto xf_node = [&](int k) {
         const DevExprNode& d = N[k];
         if ((d.op != MC_EX_EXP && d.op != MC_EX_LOG) || d.a < 0) return -1;
@@ -459,25 +469,20 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
         return N[k].op == MC_EX_LEAF && N[k].leaf.kind == MC_OP_PSCALAR &&
                L.shxf[ordinal(N[k].leaf.poff)] == MC_XF_NONE;
     };
+    auto part = [&](int k) { return xf_node(k) >= 0 || raw_leaf(k); };  // a cotangent sum
     std::vector<int> dleaves;
     for (int k = 0; k < nn; ++k) {
         const DevExprNode& d = N[k];
         if (xf_node(k) >= 0) {
-            const int K = xf_node(k);
-            o << "  const exf2 v" << k << " = {rl(sh.v, " << 2 * K << "), rl(sh.v, " << 2 * K + 1
-              << ")};\n  exf2 p" << k << " = {0.0f, 0.0f};\n";
-            continue;
-        }
-        if (d.op == MC_EX_LEAF) {
+            o << "  const exf2 v" << k << " = " << sh_read("v", xf_node(k)) << ";\n";
+        } else if (d.op == MC_EX_LEAF) {
             if (d.leaf.kind == MC_OP_PSCALAR && !raw_leaf(k)) {
                 o << "  const exf2 v" << k << " = {0.0f, 0.0f};  // (read through node transforms)\n";
             } else if (d.leaf.kind == MC_OP_CONST) {
                 o << "  const exf2 v" << k << " = {" << flit(d.leaf.cval) << ", " << flit(d.leaf.cval)
                   << "};\n";
             } else if (d.leaf.kind == MC_OP_PSCALAR) {
-                const int K = ordinal(d.leaf.poff);
-                o << "  const exf2 v" << k << " = {rl(sh.q, " << 2 * K << "), rl(sh.q, " << 2 * K + 1
-                  << ")};\n  exf2 p" << k << " = {0.0f, 0.0f};\n";
+                o << "  const exf2 v" << k << " = " << sh_read("q", ordinal(d.leaf.poff)) << ";\n";
             } else {  // data: one tile per array (leaves of one array share it)
                 bool dup = false;
                 for (int r : dleaves) dup |= N[r].leaf.pool == d.leaf.pool;
@@ -490,14 +495,17 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
         } else {
             o << "  const float c" << k << " = " << flit(d.leaf.cval) << ";\n";
         }
+        if (part(k)) o << "  exf2 p" << k << " = {0.0f, 0.0f}, t" << k << " = {0.0f, 0.0f};\n";
     }
     o << "  const exf2 z2 = {0.0f, 0.0f};\n  (void)z2;\n";
     // E elements at once, their statements interleaved node by node (the
     // elements' dependency chains are independent, so the hazards of one —
     // transcendental results, packed read-after-write — are covered by the
     // others' instructions); sums in element order.  x[e][i]: element e's
-    // value of data leaf i.
-    auto emit = [&](int E, const std::vector<std::vector<std::string>>& x, const char* ind) {
+    // value of data array i (an exf2 expression); acc: the accumulators' prefix
+    // ("p" / "lpa" for the runs, "t" / "lpt" for a one-chain tail)
+    auto emit = [&](int E, const std::vector<std::vector<std::string>>& x, const char* ind,
+                    bool tail) {
         auto nm = [&](char c, int k, int e) {
             // leaves outside the element (constants, parameters) keep one name
             const DevExprNode& d = N[k];
@@ -507,6 +515,7 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
             return std::string(1, c) + std::to_string(k) + "_" + std::to_string(e);
         };
         auto argn = [&](int a, int e) { return a >= 0 ? nm('v', a, e) : std::string("z2"); };
+        const char* pa = tail ? "t" : "p";
         for (int k = 0; k < nn; ++k) {
             const DevExprNode& d = N[k];
             for (int e = 0; e < E; ++e) {
@@ -514,8 +523,7 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
                     if (d.leaf.kind == MC_OP_DATA) {
                         size_t i = 0;
                         while (N[dleaves[i]].leaf.pool != d.leaf.pool) ++i;
-                        o << ind << "const exf2 " << nm('v', k, e) << " = {" << x[e][i] << ", "
-                          << x[e][i] << "};\n";
+                        o << ind << "const exf2 " << nm('v', k, e) << " = " << x[e][i] << ";\n";
                     }
                     continue;
                 }
@@ -526,7 +534,8 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
             }
         }
         for (int e = 0; e < E; ++e)
-            o << ind << "if constexpr (LP) lpa += wv * " << nm('v', nn - 1, e) << ";\n";
+            o << ind << "if constexpr (LP) " << (tail ? "lpt" : "lpa") << " += wv * "
+              << nm('v', nn - 1, e) << ";\n";
         // (adjoints start at -0, as the tape's: -0 + x == x)
         for (int k = 0; k < nn; ++k)
             for (int e = 0; e < E; ++e)
@@ -536,8 +545,8 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
             const DevExprNode& d = N[k];
             if (d.op == MC_EX_LEAF && !raw_leaf(k)) continue;
             for (int e = 0; e < E; ++e) {
-                if (d.op == MC_EX_LEAF || xf_node(k) >= 0) {
-                    o << ind << "p" << k << " += " << nm('a', k, e) << ";\n";
+                if (part(k)) {
+                    o << ind << pa << k << " += " << nm('a', k, e) << ";\n";
                     continue;
                 }
                 o << ind << "{ exf2 dx, dy, dz; ex2_bwd(" << d.op << ", " << argn(d.a, e) << ", "
@@ -550,47 +559,68 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
             }
         }
     };
-    // four elements per trip: a 16-byte LDS load per data leaf, the four
-    // elements interleaved; the ragged tail one at a time
+    // four elements per trip (a 16-byte LDS load per data array): two chains,
+    // four elements interleaved; one chain, two element pairs interleaved
+    const char* comp[4] = {"x", "y", "z", "w"};
     o << "  int u = 0;\n  for (; u + 4 <= len; u += 4) {\n";
     for (int k : dleaves)
         o << "    const float4 X" << k << " = *(const float4*)(d" << k << " + (u >> 2) * 256);\n";
     {
-        const char* comp[4] = {"x", "y", "z", "w"};
-        std::vector<std::vector<std::string>> x(4);
-        for (int e = 0; e < 4; ++e)
-            for (int k : dleaves) x[e].push_back("X" + std::to_string(k) + "." + comp[e]);
-        emit(4, x, "    ");
+        const int E = one ? 2 : 4;
+        std::vector<std::vector<std::string>> x(E);
+        for (int e = 0; e < E; ++e)
+            for (int k : dleaves) {
+                const std::string X = "X" + std::to_string(k) + ".";
+                x[e].push_back(one ? "exf2{" + X + comp[2 * e] + ", " + X + comp[2 * e + 1] + "}"
+                                   : "exf2{" + X + comp[e] + ", " + X + comp[e] + "}");
+            }
+        emit(E, x, "    ", false);
     }
+    // the ragged tail, one element at a time (one chain: the element in both
+    // components, its sums taken from component x only)
     o << "  }\n  for (; u < len; ++u) {\n    const int ou = (u >> 2) * 256 + (u & 3);\n";
     {
         std::vector<std::vector<std::string>> x(1);
-        for (int k : dleaves) x[0].push_back("d" + std::to_string(k) + "[ou]");
-        emit(1, x, "    ");
+        for (int k : dleaves) {
+            const std::string d = "d" + std::to_string(k) + "[ou]";
+            x[0].push_back("exf2{" + d + ", " + d + "}");
+        }
+        emit(1, x, "    ", one);
     }
-    o << "  }\n"
-      << "  if constexpr (LP) {\n    lpp[0] += lpa.x;\n    lpp[1] += lpa.y;\n  }\n";
-    for (int k = 0; k < nn; ++k) {
-        int K = xf_node(k);
-        if (K < 0 && raw_leaf(k)) K = ordinal(N[k].leaf.poff);
-        if (K < 0) continue;
-        o << "  gshp[" << K << "][0] += p" << k << ".x;\n  gshp[" << K << "][1] += p" << k << ".y;\n";
+    o << "  }\n";
+    if (one) {
+        o << "  if constexpr (LP) lpp += (lpa.x + lpa.y) + lpt.x;\n";
+        for (int k = 0; k < nn; ++k) {
+            if (!part(k)) continue;
+            const int K = xf_node(k) >= 0 ? xf_node(k) : ordinal(N[k].leaf.poff);
+            o << "  gsh[" << K << "] += (p" << k << ".x + p" << k << ".y) + t" << k << ".x;\n";
+        }
+    } else {
+        o << "  if constexpr (LP) {\n    lpp[0] += lpa.x;\n    lpp[1] += lpa.y;\n  }\n";
+        for (int k = 0; k < nn; ++k) {
+            if (!part(k)) continue;
+            const int K = xf_node(k) >= 0 ? xf_node(k) : ordinal(N[k].leaf.poff);
+            o << "  gshp[" << K << "][0] += p" << k << ".x;\n  gshp[" << K << "][1] += p" << k
+              << ".y;\n";
+        }
     }
     o << "}\n\n";
 }
 
 // The lane-resident kernels' source for a program with LS_EXPR terms:
-// lanes.h with its expression hook defined.
+// lanes.h and nuts_sliced.h with their expression hooks defined (two chains
+// per wave: k_hmc_lr; one: k_nuts_sl).
 std::string gen_lane_source(const mc_program* p) {
     std::ostringstream o;
     o << "// generated by jit.hip (lane-resident expression terms) for one program: do not edit\n"
-      << "#define MC_JIT_LANES 1\n#include \"lanes.h\"\nnamespace mc {\n";
+      << "#define MC_JIT_LANES 1\n#include \"nuts_sliced.h\"\nnamespace mc {\n";
     std::vector<int32_t> bases;
     for (const DevTerm& T : p->raw) {
         if (T.dist != MC_DIST_EXPR) continue;
         if (std::find(bases.begin(), bases.end(), T.expr_base) != bases.end()) continue;
         bases.push_back(T.expr_base);
-        gen_lane_term(o, T, p->nodes.data() + T.expr_base, p->lr);
+        gen_lane_term(o, T, p->nodes.data() + T.expr_base, p->lr, false);
+        gen_lane_term(o, T, p->nodes.data() + T.expr_base, p->lr, true);
     }
     o << "MC_DEV void mc_jit_lane_expr(const MC_CONST LrTerm* T, const float* sd, int j,\n"
       << "    const LrShared& sh, float (&lpp)[2], float (&gshp)[kLrMaxShared][2], bool need_lp) {\n"
@@ -599,11 +629,19 @@ std::string gen_lane_source(const mc_program* p) {
         o << "    case " << b << ":\n      if (need_lp) jit_lt" << b
           << "<true>(T, sd, j, sh, lpp, gshp);\n      else jit_lt" << b
           << "<false>(T, sd, j, sh, lpp, gshp);\n      break;\n";
+    o << "    default: break;\n  }\n}\n"
+      << "MC_DEV void mc_jit_lane_expr1(const MC_CONST LrTerm* T, const float* sd, int j,\n"
+      << "    const LrShared& sh, float& lpp, float (&gsh)[kLrMaxShared]) {\n"
+      << "  switch (T->expr_base) {\n";
+    for (int32_t b : bases)
+        o << "    case " << b << ": jit_lo" << b << "<true>(T, sd, j, sh, lpp, gsh); break;\n";
     o << "    default: break;\n  }\n}\n}  // namespace mc\n";
     return o.str();
 }
 
-bool is_lane_kernel(const std::string& kernel) { return kernel.rfind("mc::k_hmc_lr<", 0) == 0; }
+bool is_lane_kernel(const std::string& kernel) {
+    return kernel.rfind("mc::k_hmc_lr<", 0) == 0 || kernel.rfind("mc::k_nuts_sl<", 0) == 0;
+}
 
 // hiprtc options: the device's own architecture (gcnArchName's processor,
 // e.g. "gfx950"), so a library built for another ARCH still compiles for the

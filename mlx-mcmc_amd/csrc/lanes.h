@@ -612,6 +612,11 @@ MC_DEV void lr_affine(const MC_CONST LrTerm* T, const float* sd, int j, LrPriv<R
 MC_DEV void mc_jit_lane_expr(const MC_CONST LrTerm* T, const float* sd, int j,
                              const LrShared& sh, float (&lpp)[2],
                              float (&gshp)[kLrMaxShared][2], bool need_lp);
+// The same for one chain per wave (k_nuts_sl: lane K of sh holds shared
+// ordinal K; two elements packed per instruction): log p into lpp, the
+// shared cotangent partials into gsh[K].
+MC_DEV void mc_jit_lane_expr1(const MC_CONST LrTerm* T, const float* sd, int j,
+                              const LrShared& sh, float& lpp, float (&gsh)[kLrMaxShared]);
 #endif
 
 // Log p partial of this slice at the current point; private gradients

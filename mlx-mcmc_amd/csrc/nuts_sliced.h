@@ -188,8 +188,10 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
     const int64_t* blk = P.blocks + 4 * (int64_t)slice;
     const int64_t doff = blk[0];
     const int dlen = (int)blk[1];
+    const int nact = (int)blk[2];
     const int nsweep = (int)(blk[3] & 255);
     const int ndirect = (int)((blk[3] >> 8) & 255);
+    (void)nact;
     for (int i = tid; 4 * i < dlen; i += 64 * NW)
         *(float4*)(sd + 4 * i) = *(const float4*)(P.data + doff + 4 * i);
     LrSterm* sst = (LrSterm*)(smem + P.sdata_floats);
@@ -517,6 +519,17 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                         lpp += d_w * (1.0f * (d_c0 - lg) - (0.5f * s2) * iv);
                     }
                 }
+                // the expression terms (LS_EXPR, after the swept / direct
+                // terms: a program planned with LanePlan::nuts_expr), their
+                // element code generated per program (jit.hip gen_lane_term,
+                // one chain, element pairs packed): log p and the shared
+                // cotangent partials by ordinal (the run-time form's slots)
+#ifdef MC_JIT_LANES
+                float gxe[kLrMaxShared] = {0.0f, 0.0f, 0.0f, 0.0f};
+                if constexpr (!CF)
+                    for (int t = nsweep + ndirect; t < nact; ++t)
+                        if (tt[t].sig == LS_EXPR) mc_jit_lane_expr1(tt + t, sd, j, sh, lpp, gxe);
+#endif
                 if (rep > 1) {
 #pragma unroll
                     for (int r = 0; r < RS; ++r) {
@@ -606,8 +619,13 @@ k_nuts_sl(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_sca
                     } else {
 #pragma unroll
                         for (int kk = 0; kk < NSH; ++kk)
+                        {
                             vv[2 + kk] = ((F.sw_ks == kk ? cs : 0.0f) + (F.d_km == kk ? cm : 0.0f)) +
                                          (F.d_ks == kk ? cd : 0.0f);
+#ifdef MC_JIT_LANES
+                            vv[2 + kk] += gxe[kk];
+#endif
+                        }
                     }
                     dots(0, vv[IT_TOPA], vv[IT_TOPB]);
                     if (IT_K0 < 8 && first_leaf) vv[IT_K0 & 7] = k0p;

@@ -19,9 +19,12 @@ static bool nuts_use_lds(const mc_program* p, int32_t max_depth) {
 
 extern "C" int64_t mc_nuts_workspace_bytes(const mc_program* p, int64_t C, int32_t max_depth) {
     if (!p || C < 0 || max_depth < 0 || max_depth > kMaxTreeDepth) return -1;
-    if (use_nuts_sliced(p, max_depth)) return nuts_sl_workspace_bytes(p, C, max_depth);
-    if (nuts_use_lds(p, max_depth)) return 0;
-    return C * nuts_arena_vectors(max_depth) * (int64_t)dpad_of(p->D) * 4;
+    const int64_t tape =
+        nuts_use_lds(p, max_depth) ? 0 : C * nuts_arena_vectors(max_depth) * (int64_t)dpad_of(p->D) * 4;
+    // (an expression program's sliced launch may fall back to the tape: jit.hip)
+    if (use_nuts_sliced(p, max_depth))
+        return std::max(nuts_sl_workspace_bytes(p, C, max_depth), p->lr.fast ? 0 : tape);
+    return tape;
 }
 
 template <int WPC, bool LDS, bool EX>
@@ -171,9 +174,11 @@ extern "C" int mc_nuts_run(const mc_program* p, const mc_run_config* cfg, void* 
         // (tags continue on this workspace: no ws_forget, nuts_sliced.h)
         if (device_cus() <= 0) return fail(MC_ERR_HIP, "no HIP device");
         constexpr int HIER = LF_SW | LF_SWS | LF_DIR | LF_DM | LF_DS;
-        return (p->lr.form == HIER && lanes_forms_enabled())
-                   ? nuts_sl_hier(p, cfg, state, samples, tr, ws, st)
-                   : nuts_sl_rt(p, cfg, state, samples, tr, ws, st);
+        const int rc_sl = (p->lr.fast && p->lr.form == HIER && lanes_forms_enabled())
+                              ? nuts_sl_hier(p, cfg, state, samples, tr, ws, st)
+                              : nuts_sl_rt(p, cfg, state, samples, tr, ws, st);
+        if (rc_sl != kLanesNoJit) return rc_sl;
+        // (expression terms without their compiled kernel: the tape below)
     }
     if (ws) ws_forget(ws);  // another kernel's data: a later sliced launch clears it
     if (use_nuts_lanes(p, cfg->max_tree_depth)) {

@@ -4,6 +4,7 @@
 // instantiations compile in parallel.
 #pragma once
 #include "host.h"
+#include "jit.h"
 
 // chains (waves) per workgroup of k_nuts_sl
 constexpr int kNslWaves = 8;
@@ -91,6 +92,74 @@ inline int launch_nuts_sl(const mc_program* p, const mc_run_config* cfg, void* s
     return MC_OK;
 }
 
+// The run-time form compiled with the program's expression terms (jit.hip):
+// kLanesNoJit when the JIT is off or the compilation failed (the caller runs
+// the program on the tape).
+template <int RS, int NSH, int OCC>
+inline int launch_nuts_sl_jit(const mc_program* p, const mc_run_config* cfg, void* state,
+                              float* samples, const mc_trace* tr, void* ws, hipStream_t st) {
+    const std::string name = "mc::k_nuts_sl<" + std::to_string(RS) + ", " + std::to_string(NSH) +
+                             ", " + std::to_string(kNslWaves) + ", " + std::to_string(OCC) + ", -1";
+    hipFunction_t f = nullptr, fxl = nullptr;
+    int rc = jit_function(p, name + ", false>", &f);
+    if (rc != MC_OK) return rc;
+    if (f == nullptr) return kLanesNoJit;
+    int64_t qo, go;
+    mc_state_offsets(p, cfg->num_chains, &qo, &go);
+    char* b = (char*)state;
+    RunArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.cfg = *cfg;
+    LrCtx ctx = lrctx_of(p);
+    const int maxj = cfg->max_tree_depth;
+    const size_t lds = nuts_sl_lds_bytes(p, maxj);
+    const int64_t C = cfg->num_chains;
+    const int64_t groups = (C + kNslWaves - 1) / kNslWaves;
+    const int S = p->lr.S;
+    int n = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 64 * kNslWaves, lds) !=
+        hipSuccess)
+        n = 0;
+    const int64_t cap = (int64_t)n * device_cus();
+    if (cap < S)
+        return fail(MC_ERR_UNSUPPORTED,
+                    "sliced NUTS (expression JIT): a chain block's %d workgroups must be "
+                    "co-resident, the device holds %lld of this kernel", S, (long long)cap);
+    const int64_t gpl = std::min(groups, cap / S);
+    const int64_t lines = nuts_sl_line_bytes(p, C);
+    int* status = (int*)ws;
+    unsigned long long* xch = (unsigned long long*)((char*)ws + kSlStatusBytes);
+    float* pool = (float*)((char*)ws + kSlStatusBytes + lines);
+    A.fault = g_exchange_fault;
+    const uint64_t per_launch = (uint64_t)cfg->iter_count * (1ull << maxj) + 1;
+    const int64_t nlaunch = (groups + gpl - 1) / gpl;
+    uint32_t base = 0;
+    if (ws_reserve(ws, per_launch * (uint64_t)nlaunch, (uint64_t)(kSlStatusBytes + lines), &base))
+        MC_HIP_TRY(hipMemsetAsync(ws, 0, kSlStatusBytes + lines, st));
+    ws_mark_status(ws);
+    mc_chain_scalars* scal = (mc_chain_scalars*)b;
+    float *sq = (float*)(b + qo), *sg = (float*)(b + go);
+    TraceDev td = trace_of(tr);
+    for (int64_t g0 = 0; g0 < groups; g0 += gpl) {
+        int64_t ng = std::min(gpl, groups - g0);
+        int64_t cb = g0 * kNslWaves;
+        hipFunction_t k = f;
+        if (xcd_round_robin(ng * S, S)) {
+            if (fxl == nullptr) {
+                rc = jit_function(p, name + ", true>", &fxl);
+                if (rc != MC_OK) return rc;
+            }
+            if (fxl != nullptr) k = fxl;
+        }
+        void* args[] = {&ctx, &A, &cb, &ng, &scal, &sq, &sg, &samples, &td, &xch, &pool, &status,
+                        &base};
+        MC_HIP_TRY(hipModuleLaunchKernel(k, (unsigned)(ng * S), 1, 1, 64 * kNslWaves, 1, 1,
+                                         (unsigned)lds, st, args, nullptr));
+        base += (uint32_t)per_launch;
+    }
+    return MC_OK;
+}
+
 // the compile-time hierarchical form (run_nuts_sl.hip) and the run-time form
 // (run_nuts_sl_rt.hip)
 int nuts_sl_hier(const mc_program* p, const mc_run_config* cfg, void* state, float* samples,
@@ -111,8 +180,12 @@ inline bool nuts_sliced_enabled() {
     }
     return g_nuts_sliced == 1;
 }
+// A program with expression terms (LanePlan::nuts_expr) runs the JIT-compiled
+// run-time form (their element code exists only compiled per program): not
+// while the JIT is off or after its compilation failed (the tape runs it).
 inline bool use_nuts_sliced(const mc_program* p, int max_depth) {
-    return nuts_sliced_enabled() && p->sl.S >= 2 && p->lr.ok && p->lr.fast &&
+    const bool expr = p->lr.nuts_expr && jit_enabled() && jit_error(p).empty();
+    return nuts_sliced_enabled() && p->sl.S >= 2 && p->lr.ok && (p->lr.fast || expr) &&
            lanes_fast_enabled() && p->lr.S >= 2 && p->lr.S <= kLrSlices &&
            p->slice_kernel != 1 && max_depth >= 1 && max_depth <= kNslMaxDepth &&
            nuts_sl_lds_bytes(p, max_depth) <= (size_t)kSlLdsBudget;

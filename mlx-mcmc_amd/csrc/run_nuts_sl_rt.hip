@@ -5,6 +5,16 @@
 int nuts_sl_rt(const mc_program* p, const mc_run_config* cfg, void* state, float* samples,
                const mc_trace* tr, void* ws, hipStream_t st) {
     const bool n4 = p->lr.Dsh > 3;
+    if (!p->lr.fast) {  // expression terms (LanePlan::nuts_expr): the JIT-compiled form
+        switch (p->lr.rs) {
+            case 1: return n4 ? launch_nuts_sl_jit<1, 4, 2>(p, cfg, state, samples, tr, ws, st)
+                              : launch_nuts_sl_jit<1, 3, 2>(p, cfg, state, samples, tr, ws, st);
+            case 2: return n4 ? launch_nuts_sl_jit<2, 4, 2>(p, cfg, state, samples, tr, ws, st)
+                              : launch_nuts_sl_jit<2, 3, 2>(p, cfg, state, samples, tr, ws, st);
+            default: return n4 ? launch_nuts_sl_jit<4, 4, 2>(p, cfg, state, samples, tr, ws, st)
+                               : launch_nuts_sl_jit<4, 3, 2>(p, cfg, state, samples, tr, ws, st);
+        }
+    }
     switch (p->lr.rs) {
         case 1: return n4 ? launch_nuts_sl<1, 4, 2, -1>(p, cfg, state, samples, tr, ws, st)
                           : launch_nuts_sl<1, 3, 2, -1>(p, cfg, state, samples, tr, ws, st);

@@ -106,3 +106,51 @@ def test_expr_lanes_without_jit_run_on_the_tape(gpu):
     assert ic.extra["kernel"] == "lanes"
     for k in start:  # (the lane kernel: another summation order, same chain)
         np.testing.assert_allclose(c[k], a[k], rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("model,eps,seed", [("logistic", 2e-3, 21), ("two_predictor", 1e-3, 22)])
+def test_expr_lanes_nuts_matches_oracle(gpu, model, eps, seed):
+    """NUTS on the sliced kernel (k_nuts_sl's run-time form compiled with the
+    program's expression terms: one chain per wave, element pairs packed):
+    trees (depth, leaves) identical to the oracle's NUTS (oracle/samplers.py
+    nuts, restating nuts.py:137-330) for the first iterations at a fixed step
+    size — the oracle sums the 100 K-element log density in another order, so
+    the comparison ends at the first tree that differs, which must not come
+    before iteration 6 on either chain — and the draws before it within rtol
+    1e-3.  With dual averaging acting the run completes on the same kernel."""
+    import mlx_mcmc_amd as m
+    from mlx_mcmc_amd import _lib, _trace
+
+    f, start = _start(model)
+    lp, _ = f(W.ns_product(), N)
+    olp, _ = f(W.ns_oracle(), N)
+    prog = _trace.compile_model(lp, start)
+    assert prog.nuts_kernel(10) == "sliced", prog.kernel_note
+    kw = dict(num_samples=8, num_warmup=4, step_size=eps, max_tree_depth=10,
+              adapt_step_size=False)
+    s, rate, info = m.nuts(lp, start, key=m.random.key(seed), num_chains=8, progress=False,
+                           return_info=True, return_trace=True, keep_on_device=True, **kw)
+    assert info.extra["kernel"] == "sliced"
+    assert _lib.load().mc_program_expr_jit(prog.handle) == 1
+    draws = info.device_samples.cpu().numpy()
+    n = kw["num_samples"] + kw["num_warmup"]
+    tr = info.trace
+    for c in (0, 5):
+        ref = S.nuts(olp, start, seed=seed, chain=c, **kw)
+        same = 0
+        for i in range(n):
+            if (tr["tree_depth"][c][i] != ref.trace["depth"][i]
+                    or tr["n_leapfrog"][c][i] != ref.trace["leaves"][i]):
+                break
+            same += 1
+        print(f"{model} NUTS chain {c}: trees identical for {same} of {n}, depths "
+              f"{list(ref.trace['depth'][:same])}")
+        assert same >= 6, f"{model} chain {c}: trees differ at iteration {same}"
+        ns = max(0, same - kw["num_warmup"])
+        np.testing.assert_allclose(draws[c, :ns], np.asarray(ref.samples)[:ns], rtol=1e-3,
+                                   atol=1e-4, err_msg=f"{model} NUTS chain {c}")
+    # dual averaging acting: the same kernel, moving chains
+    s2, rate2, info2 = m.nuts(lp, start, key=m.random.key(seed), num_chains=16, progress=False,
+                              return_info=True, num_samples=20, num_warmup=20, step_size=eps)
+    assert info2.extra["kernel"] == "sliced"
+    assert np.all(info2.mean_tree_depth >= 1)
