@@ -6,14 +6,20 @@ int nuts_sl_rt(const mc_program* p, const mc_run_config* cfg, void* state, float
                const mc_trace* tr, void* ws, hipStream_t st) {
     const bool n4 = p->lr.Dsh > 3;
     if (!p->lr.fast) {  // expression terms (LanePlan::nuts_expr): the JIT-compiled form
+        // (4 waves per SIMD with more than 8 slices, as the hierarchical form:
+        // every chain block of 256 chains resident in one launch)
+        const bool o4 = nuts_sl_occ(p) == 4;
+#define MC_NSLJ(R)                                                                              \
+        return o4 ? (n4 ? launch_nuts_sl_jit<R, 4, 4>(p, cfg, state, samples, tr, ws, st)       \
+                        : launch_nuts_sl_jit<R, 3, 4>(p, cfg, state, samples, tr, ws, st))      \
+                  : (n4 ? launch_nuts_sl_jit<R, 4, 2>(p, cfg, state, samples, tr, ws, st)       \
+                        : launch_nuts_sl_jit<R, 3, 2>(p, cfg, state, samples, tr, ws, st))
         switch (p->lr.rs) {
-            case 1: return n4 ? launch_nuts_sl_jit<1, 4, 2>(p, cfg, state, samples, tr, ws, st)
-                              : launch_nuts_sl_jit<1, 3, 2>(p, cfg, state, samples, tr, ws, st);
-            case 2: return n4 ? launch_nuts_sl_jit<2, 4, 2>(p, cfg, state, samples, tr, ws, st)
-                              : launch_nuts_sl_jit<2, 3, 2>(p, cfg, state, samples, tr, ws, st);
-            default: return n4 ? launch_nuts_sl_jit<4, 4, 2>(p, cfg, state, samples, tr, ws, st)
-                               : launch_nuts_sl_jit<4, 3, 2>(p, cfg, state, samples, tr, ws, st);
+            case 1: MC_NSLJ(1);
+            case 2: MC_NSLJ(2);
+            default: MC_NSLJ(4);
         }
+#undef MC_NSLJ
     }
     switch (p->lr.rs) {
         case 1: return n4 ? launch_nuts_sl<1, 4, 2, -1>(p, cfg, state, samples, tr, ws, st)

@@ -114,3 +114,36 @@ for jit, sl, nm in VARIANTS:
     r, tb, k = rate(lp, {"a": np.float32(-0.3), "b": np.float32(1.1)}, jit=jit, slices=sl)
     print(f"logistic N={N} expression ({nm}): {r / 1e6:.3f} M chain-steps/s "
           f"(kernel {k}; build {tb:.2f} s)")
+
+
+def nuts_rate(lp, init, slices, chains=256, eps=2e-3, iters=10):
+    """NUTS leaf-steps/s (all chains) at a fixed step size: slices 0 = the
+    sliced kernel (k_nuts_sl's run-time form JIT-compiled with the expression
+    terms), 1 = the tape (k_nuts)."""
+    prog = _trace.compile_model(lp, init, slices=slices)
+    kern = prog.nuts_kernel(10)
+    cs = _engine.ChainSet(prog, chains, prog.layout.flatten(init), eps,
+                          device=torch.device("cuda"))
+    cfg = dict(chain_offset=0, num_warmup=10 ** 6, num_samples=0, sample_begin=0,
+               sample_capacity=0, seed=0, step_size=eps, target_accept=0.8, max_tree_depth=10,
+               adapt_step_size=False, slice_mode=0)
+    cs.run_nuts(iter_begin=0, iter_count=2, **cfg)
+    torch.cuda.synchronize()
+    g0 = cs.scalars()["n_grad"].astype(np.int64).sum()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    cs.run_nuts(iter_begin=2, iter_count=iters, **cfg)
+    e1.record()
+    torch.cuda.synchronize()
+    cs.check_status()
+    leaves = cs.scalars()["n_grad"].astype(np.int64).sum() - g0
+    return leaves / (e0.elapsed_time(e1) * 1e-3), kern
+
+
+for name, f, start, eps in (
+        ("logistic", W.logistic_regression, {"a": np.float32(-0.3), "b": np.float32(1.1)}, 2e-3),
+        ("two-predictor", W.two_predictor_regression, i2, 1e-3)):
+    lpn, _ = f(W.ns_product(), N)
+    for sl in (0, 1):
+        r, k = nuts_rate(lpn, start, sl, eps=eps)
+        print(f"{name} N={N} NUTS (fixed eps {eps}): {r / 1e6:.3f} M leaf-steps/s (kernel {k})")
