@@ -6,9 +6,12 @@ int nuts_sl_rt(const mc_program* p, const mc_run_config* cfg, void* state, float
                const mc_trace* tr, void* ws, hipStream_t st) {
     const bool n4 = p->lr.Dsh > 3;
     if (!p->lr.fast) {  // expression terms (LanePlan::nuts_expr): the JIT-compiled form
-        // (4 waves per SIMD with more than 8 slices, as the hierarchical form:
-        // every chain block of 256 chains resident in one launch)
-        const bool o4 = nuts_sl_occ(p) == 4;
+        // (2 waves per SIMD: at 16 slices 4 — every chain block of 256 chains
+        // resident in one launch — measured no faster on the N = 100 K GLMs,
+        // logistic 4.30 vs 4.25 M leaf-steps/s, two-predictor 8.97 vs 8.18;
+        // MC_NUTS_SL_OCC=4 selects it)
+        const char* oe = std::getenv("MC_NUTS_SL_OCC");
+        const bool o4 = oe && std::atoi(oe) == 4;
 #define MC_NSLJ(R)                                                                              \
         return o4 ? (n4 ? launch_nuts_sl_jit<R, 4, 4>(p, cfg, state, samples, tr, ws, st)       \
                         : launch_nuts_sl_jit<R, 3, 4>(p, cfg, state, samples, tr, ws, st))      \
