@@ -447,14 +447,15 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
         else x << "exf2{rl(sh." << f << ", " << 2 * K << "), rl(sh." << f << ", " << 2 * K + 1 << ")}";
         return x.str();
     };
-    o << "template <bool LP>\n"
+    o << (one ? "template <bool LP, bool G>\n" : "template <bool LP>\n")
       << "MC_DEV void jit_l" << (one ? "o" : "t") << T.expr_base
       << "(const MC_CONST LrTerm* T, const float* sd, int j, const LrShared& sh,\n"
       << (one ? "    float& lpp, float (&gsh)[kLrMaxShared]) {\n"
               : "    float (&lpp)[2], float (&gshp)[kLrMaxShared][2]) {\n")
       << "  const int len = ((const int32_t*)sd)[T->len_off + j];\n"
       << "  const exf2 wv = {T->weight, T->weight};\n"
-      << "  exf2 lpa = {0.0f, 0.0f}, lpt = {0.0f, 0.0f};\n  (void)lpa; (void)lpt;\n";
+      << "  exf2 lpa = {0.0f, 0.0f}, lpt = {0.0f, 0.0f};\n  (void)lpa; (void)lpt;\n"
+      << (one ? "  (void)gsh;\n" : "");
     auto xf_node = [&](int k) {
         const DevExprNode& d = N[k];
         if ((d.op != MC_EX_EXP && d.op != MC_EX_LOG) || d.a < 0) return -1;
@@ -536,6 +537,8 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
         for (int e = 0; e < E; ++e)
             o << ind << "if constexpr (LP) " << (tail ? "lpt" : "lpa") << " += wv * "
               << nm('v', nn - 1, e) << ";\n";
+        // (one chain, G = false: the value only — k_mh_sl's forward pass)
+        if (one) o << ind << "if constexpr (G) {\n";
         // (adjoints start at -0, as the tape's: -0 + x == x)
         for (int k = 0; k < nn; ++k)
             for (int e = 0; e < E; ++e)
@@ -558,6 +561,7 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
                 o << " (void)dx; (void)dy; (void)dz; }\n";
             }
         }
+        if (one) o << ind << "}\n";
     };
     // four elements per trip (a 16-byte LDS load per data array): two chains,
     // four elements interleaved; one chain, two element pairs interleaved
@@ -589,12 +593,13 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
     }
     o << "  }\n";
     if (one) {
-        o << "  if constexpr (LP) lpp += (lpa.x + lpa.y) + lpt.x;\n";
+        o << "  if constexpr (LP) lpp += (lpa.x + lpa.y) + lpt.x;\n  if constexpr (G) {\n";
         for (int k = 0; k < nn; ++k) {
             if (!part(k)) continue;
             const int K = xf_node(k) >= 0 ? xf_node(k) : ordinal(N[k].leaf.poff);
-            o << "  gsh[" << K << "] += (p" << k << ".x + p" << k << ".y) + t" << k << ".x;\n";
+            o << "    gsh[" << K << "] += (p" << k << ".x + p" << k << ".y) + t" << k << ".x;\n";
         }
+        o << "  }\n";
     } else {
         o << "  if constexpr (LP) {\n    lpp[0] += lpa.x;\n    lpp[1] += lpa.y;\n  }\n";
         for (int k = 0; k < nn; ++k) {
@@ -613,7 +618,7 @@ void gen_lane_term(std::ostringstream& o, const DevTerm& T, const DevExprNode* N
 std::string gen_lane_source(const mc_program* p) {
     std::ostringstream o;
     o << "// generated by jit.hip (lane-resident expression terms) for one program: do not edit\n"
-      << "#define MC_JIT_LANES 1\n#include \"nuts_sliced.h\"\nnamespace mc {\n";
+      << "#define MC_JIT_LANES 1\n#include \"mh_sliced.h\"\nnamespace mc {\n";
     std::vector<int32_t> bases;
     for (const DevTerm& T : p->raw) {
         if (T.dist != MC_DIST_EXPR) continue;
@@ -634,13 +639,20 @@ std::string gen_lane_source(const mc_program* p) {
       << "    const LrShared& sh, float& lpp, float (&gsh)[kLrMaxShared]) {\n"
       << "  switch (T->expr_base) {\n";
     for (int32_t b : bases)
-        o << "    case " << b << ": jit_lo" << b << "<true>(T, sd, j, sh, lpp, gsh); break;\n";
+        o << "    case " << b << ": jit_lo" << b << "<true, true>(T, sd, j, sh, lpp, gsh); break;\n";
+    o << "    default: break;\n  }\n}\n"
+      << "MC_DEV void mc_jit_lane_expr1v(const MC_CONST LrTerm* T, const float* sd, int j,\n"
+      << "    const LrShared& sh, float& lpp) {\n  float gsh[kLrMaxShared];\n"
+      << "  switch (T->expr_base) {\n";
+    for (int32_t b : bases)
+        o << "    case " << b << ": jit_lo" << b << "<true, false>(T, sd, j, sh, lpp, gsh); break;\n";
     o << "    default: break;\n  }\n}\n}  // namespace mc\n";
     return o.str();
 }
 
 bool is_lane_kernel(const std::string& kernel) {
-    return kernel.rfind("mc::k_hmc_lr<", 0) == 0 || kernel.rfind("mc::k_nuts_sl<", 0) == 0;
+    return kernel.rfind("mc::k_hmc_lr<", 0) == 0 || kernel.rfind("mc::k_nuts_sl<", 0) == 0 ||
+           kernel.rfind("mc::k_mh_sl<", 0) == 0;
 }
 
 // hiprtc options: the device's own architecture (gcnArchName's processor,

@@ -617,6 +617,9 @@ MC_DEV void mc_jit_lane_expr(const MC_CONST LrTerm* T, const float* sd, int j,
 // shared cotangent partials into gsh[K].
 MC_DEV void mc_jit_lane_expr1(const MC_CONST LrTerm* T, const float* sd, int j,
                               const LrShared& sh, float& lpp, float (&gsh)[kLrMaxShared]);
+// Its log p alone (k_mh_sl's forward pass).
+MC_DEV void mc_jit_lane_expr1v(const MC_CONST LrTerm* T, const float* sd, int j,
+                               const LrShared& sh, float& lpp);
 #endif
 
 // Log p partial of this slice at the current point; private gradients

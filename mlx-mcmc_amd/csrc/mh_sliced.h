@@ -96,8 +96,10 @@ k_mh_sl(LrCtx P, RunArgs A, float scale, int64_t chain_base, int64_t n_groups,
     const int64_t* blk = P.blocks + 4 * (int64_t)slice;
     const int64_t doff = blk[0];
     const int dlen = (int)blk[1];
+    const int nact = (int)blk[2];
     const int nsweep = (int)(blk[3] & 255);
     const int ndirect = (int)((blk[3] >> 8) & 255);
+    (void)nact;
     for (int i = tid; 4 * i < dlen; i += 64 * NW)
         *(float4*)(sd + 4 * i) = *(const float4*)(P.data + doff + 4 * i);
     LrSterm* sst = (LrSterm*)(smem + P.sdata_floats);
@@ -252,6 +254,21 @@ k_mh_sl(LrCtx P, RunArgs A, float scale, int64_t chain_base, int64_t n_groups,
                 lpp += F.d_w * (1.0f * (F.d_c0 - lg) - (0.5f * (d * d)) * iv);
             }
         }
+#ifdef MC_JIT_LANES
+        // the expression terms (LS_EXPR beside a fast form: LanePlan::nuts_expr),
+        // their element code generated per program, value only (jit.hip)
+        if constexpr (!CF) {
+            LrShared shp;
+            shp.q = qsn;
+            shp.v = v;
+            shp.p = shp.g = 0.0f;
+            shp.is = is;
+            shp.iv = is * is;
+            shp.lg = lgv;
+            for (int t = nsweep + ndirect; t < nact; ++t)
+                if (tt[t].sig == LS_EXPR) mc_jit_lane_expr1v(tt + t, sd, j, shp, lpp);
+        }
+#endif
         {  // the own prior of the lane's shared parameter, identity terms (slice 0)
             const float d = own.hn ? v : v - own.m;
             const bool out = own.hn && !(v >= 0.0f);

@@ -23,9 +23,10 @@ extern "C" int32_t mc_program_mh_sliced(const mc_program* p) {
 
 extern "C" int64_t mc_mh_workspace_bytes(const mc_program* p, int64_t C) {
     if (!p || C < 0) return -1;
-    if (use_mh_sliced(p)) return mh_sl_workspace_bytes(p, C);
-    if (mh_use_lds(p)) return 0;
-    return C * 2 * (int64_t)dpad_of(p->D) * 4;
+    const int64_t tape = mh_use_lds(p) ? 0 : C * 2 * (int64_t)dpad_of(p->D) * 4;
+    // (an expression program's sliced launch may fall back to the tape: jit.hip)
+    if (use_mh_sliced(p)) return std::max(mh_sl_workspace_bytes(p, C), p->lr.fast ? 0 : tape);
+    return tape;
 }
 
 template <int WPC, bool LDS, bool EX>
@@ -74,8 +75,10 @@ extern "C" int mc_mh_run(const mc_program* p, const mc_run_config* cfg, double p
         if (ws == nullptr || ws_bytes < need)
             return fail(MC_ERR_INVALID, "workspace too small: need %lld bytes", (long long)need);
         if (device_cus() <= 0) return fail(MC_ERR_HIP, "no HIP device");
-        return mh_sliced_run(p, cfg, (float)proposal_scale, state, samples, tr, ws,
-                             (hipStream_t)stream);
+        const int rc_sl = mh_sliced_run(p, cfg, (float)proposal_scale, state, samples, tr, ws,
+                                        (hipStream_t)stream);
+        if (rc_sl != kLanesNoJit) return rc_sl;
+        // (expression terms without their compiled kernel: the tape below)
     }
     const bool lds = mh_use_lds(p);
     const int64_t need = mc_mh_workspace_bytes(p, cfg->num_chains);

@@ -20,8 +20,12 @@ inline bool mh_sliced_enabled() {
     }
     return g_mh_sliced == 1;
 }
+// (a program with expression terms, LanePlan::nuts_expr: the JIT-compiled
+// run-time form, not while the JIT is off or after its compilation failed)
 inline bool use_mh_sliced(const mc_program* p) {
-    return mh_sliced_enabled() && p->sl.S >= 2 && p->lr.ok && p->lr.fast && lanes_fast_enabled() &&
+    const bool expr = p->lr.nuts_expr && jit_enabled() && jit_error(p).empty();
+    return mh_sliced_enabled() && p->sl.S >= 2 && p->lr.ok && (p->lr.fast || expr) &&
+           lanes_fast_enabled() &&
            p->lr.S >= 2 && p->lr.S <= kLrSlices && p->slice_kernel != 1 &&
            (size_t)p->lr.sdata_floats * 4 + p->lr.sterms.size() * sizeof(LrSterm) <=
                (size_t)kSlLdsBudget;

@@ -70,7 +70,8 @@ def test_lane_expression_source_compiles(model, nsh):
     """GLM expression programs sliced onto the lane-resident layout (lanes.h
     LS_EXPR): the host planner takes them, and the generated lane code
     (jit.hip gen_lane_term) compiles into k_hmc_lr with the sliced exchange
-    (8 slices, 4 waves) and its L2-resident variant."""
+    (8 slices, 4 waves) and its L2-resident variant, and into the sliced NUTS
+    and MH kernels' run-time forms."""
     from mlx_mcmc_amd import _lib
 
     lib = _lib.load()
@@ -80,10 +81,13 @@ def test_lane_expression_source_compiles(model, nsh):
         assert lib.mc_debug_lane_plan_host(h, 8) == 0, (lib.mc_last_error() or b"").decode()
         src = _lane_source(h)
         assert "mc_jit_lane_expr" in src and "ex2_fwd(" in src and "#include \"lanes.h\"" in src
-        for xl in ("false", "true"):
-            k = f"mc::k_hmc_lr<1, {nsh}, 4, false, {xl}>"
+        kernels = [f"mc::k_hmc_lr<1, {nsh}, 4, false, {xl}>" for xl in ("false", "true")]
+        # NUTS and MH: the sliced kernels' run-time forms (one chain per wave)
+        kernels += [f"mc::k_nuts_sl<1, {nsh}, 8, 2, -1, false>",
+                    f"mc::k_mh_sl<1, {nsh}, 8, 2, -1, true>"]
+        for k in kernels:
             rc = lib.mc_debug_expr_jit_compile(h, k.encode())
-            assert rc == 0, (lib.mc_last_error() or b"").decode()[:3000]
+            assert rc == 0, (k, (lib.mc_last_error() or b"").decode()[:3000])
     finally:
         lib.mc_program_destroy(h)
 

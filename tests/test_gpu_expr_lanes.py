@@ -154,3 +154,43 @@ def test_expr_lanes_nuts_matches_oracle(gpu, model, eps, seed):
                               return_info=True, num_samples=20, num_warmup=20, step_size=eps)
     assert info2.extra["kernel"] == "sliced"
     assert np.all(info2.mean_tree_depth >= 1)
+
+
+@pytest.mark.parametrize("model,scale,seed", [("logistic", 4e-3, 31), ("huber", 3e-3, 32)])
+def test_expr_lanes_mh_matches_oracle(gpu, model, scale, seed):
+    """Random-walk MH (metropolis.py:6-101, the MCMC.run default) on the
+    sliced kernel k_mh_sl's run-time form compiled with the expression terms
+    (value only): the same proposals as the oracle, decisions equal until a
+    proven near-tie (8 ulp of |log p|), log p and draws before it."""
+    import mlx_mcmc_amd as m
+    from mlx_mcmc_amd import _lib, _trace
+    from _near_tie import tie_bound
+
+    f, start = _start(model)
+    lp, _ = f(W.ns_product(), N)
+    olp, _ = f(W.ns_oracle(), N)
+    prog = _trace.compile_model(lp, start)
+    assert _lib.load().mc_program_mh_sliced(prog.handle) == 1, prog.kernel_note
+    n = 60
+    s, rate, info = m.metropolis_hastings(lp, start, num_samples=n, proposal_scale=scale,
+                                          random_seed=seed, return_info=True,
+                                          return_trace=True, keep_on_device=True)
+    ref = S.metropolis_hastings(olp, start, num_samples=n, proposal_scale=scale,
+                                random_seed=seed)
+    acc = info.trace["accepted"][0].astype(bool)
+    racc = np.array(ref.trace["accepted"])
+    assert 0 < racc.sum() < n, "mixed decisions"
+    flips = np.nonzero(acc != racc)[0]
+    same = int(flips[0]) if flips.size else n
+    print(f"{model} MH: decisions identical for {same} of {n}")
+    if same < n:
+        lu = log_u(m.random.key(seed).seed, 0, n)
+        tie = tie_bound(ref.trace["logp"][same])
+        gap = abs(float(lu[same]) - ref.trace["ratio"][same])
+        assert gap <= tie, f"flip at {same} is not a near-tie: gap {gap} > {tie}"
+    assert same >= 20
+    np.testing.assert_allclose(info.trace["energy"][0][:same], ref.trace["logp"][:same],
+                               rtol=2e-6)
+    draws = info.device_samples[0].cpu().numpy()
+    np.testing.assert_allclose(draws[:same], np.asarray(ref.samples)[:same], rtol=1e-5,
+                               atol=1e-6)
