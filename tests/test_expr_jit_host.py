@@ -80,7 +80,7 @@ def test_lane_expression_source_compiles(model, nsh):
     try:
         assert lib.mc_debug_lane_plan_host(h, 8) == 0, (lib.mc_last_error() or b"").decode()
         src = _lane_source(h)
-        assert "mc_jit_lane_expr" in src and "ex2_fwd(" in src and "#include \"lanes.h\"" in src
+        assert "mc_jit_lane_expr" in src and "ex2_fwd(" in src and "#include \"mh_sliced.h\"" in src
         kernels = [f"mc::k_hmc_lr<1, {nsh}, 4, false, {xl}>" for xl in ("false", "true")]
         # NUTS and MH: the sliced kernels' run-time forms (one chain per wave)
         kernels += [f"mc::k_nuts_sl<1, {nsh}, 8, 2, -1, false>",
