@@ -136,17 +136,27 @@ MC_DEV f2 lf_hi_minus(f2 xy, f2 th) {
 // s2 = fma(d, d, s2), with the even and odd elements in separate packed
 // accumulators (two independent dependency chains each).
 MC_DEV void lf_moments(const float* xv, int len, int lmin4, int lmax, f2 th, f2& s1, f2& s2) {
-    f2 a1[2] = {{0.f, 0.f}, {0.f, 0.f}}, a2[2] = {{0.f, 0.f}, {0.f, 0.f}};
+    f2 a1[2], a2[2];
     // a register pair's elements broadcast by swizzle (op_sel on the pair,
-    // no copy of the odd register)
-    auto pair = [&](f2 xy) {
+    // no copy of the odd register); the first pair assigns the accumulators
+    // (d and d * d: what 0 + d and fma(d, d, 0) round to), so no zeros are
+    // materialised per sweep
+    auto pair = [&](f2 xy, auto first) {
         const f2 d0 = xy.xx - th;
-        a1[0] += d0;
-        a2[0] = pk_fma(d0, d0, a2[0]);
         const f2 d1 = lf_hi_minus(xy, th);
-        a1[1] += d1;
-        a2[1] = pk_fma(d1, d1, a2[1]);
+        if constexpr (decltype(first)::value) {
+            a1[0] = d0;
+            a2[0] = d0 * d0;
+            a1[1] = d1;
+            a2[1] = d1 * d1;
+        } else {
+            a1[0] += d0;
+            a2[0] = pk_fma(d0, d0, a2[0]);
+            a1[1] += d1;
+            a2[1] = pk_fma(d1, d1, a2[1]);
+        }
     };
+    const std::false_type acc;
     int u4 = 0;
     // 16 elements per round; the next round's LDS loads are issued before
     // this round's arithmetic (software pipelined over two register sets that
@@ -158,29 +168,39 @@ MC_DEV void lf_moments(const float* xv, int len, int lmin4, int lmax, f2 th, f2&
 #pragma unroll
             for (int q = 0; q < 4; ++q) X[q] = *(const float4*)(xv + (g + q) * 256);
         };
-        auto round = [&](const float4 (&X)[4]) {
+        auto round = [&](const float4 (&X)[4], auto first) {
+            pair((f2){X[0].x, X[0].y}, first);
+            pair((f2){X[0].z, X[0].w}, acc);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                pair((f2){X[q].x, X[q].y});
-                pair((f2){X[q].z, X[q].w});
+            for (int q = 1; q < 4; ++q) {
+                pair((f2){X[q].x, X[q].y}, acc);
+                pair((f2){X[q].z, X[q].w}, acc);
             }
         };
         // (the prefetch index is clamped to the last full round: the loads
         // are unconditional, so the register sets never need copies)
         const int last = lmin4 - 4;
         load(A, 0);
-        for (;;) {
-            const bool more_b = u4 + 8 <= lmin4;
-            load(B, min(u4 + 4, last));
-            round(A);
-            u4 += 4;
-            if (!more_b) break;
-            const bool more_a = u4 + 8 <= lmin4;
-            load(A, min(u4 + 4, last));
-            round(B);
-            u4 += 4;
-            if (!more_a) break;
+        const bool more = 8 <= lmin4;
+        load(B, min(4, last));
+        round(A, std::true_type());
+        u4 = 4;
+        if (more) {
+            for (;;) {
+                const bool more_a = u4 + 8 <= lmin4;
+                load(A, min(u4 + 4, last));
+                round(B, acc);
+                u4 += 4;
+                if (!more_a) break;
+                const bool more_b = u4 + 8 <= lmin4;
+                load(B, min(u4 + 4, last));
+                round(A, acc);
+                u4 += 4;
+                if (!more_b) break;
+            }
         }
+    } else {
+        a1[0] = a1[1] = a2[0] = a2[1] = (f2){0.f, 0.f};
     }
     // the groups every lane holds in full (uniform), then the ragged end:
     // element e of the lanes with more elements (e < lmax, uniform bounds),
@@ -188,8 +208,8 @@ MC_DEV void lf_moments(const float* xv, int len, int lmin4, int lmax, f2 th, f2&
     // in bounds); no exec-masked loop, no per-lane branch
     for (; u4 < lmin4; ++u4) {
         const float4 a = *(const float4*)(xv + u4 * 256);
-        pair((f2){a.x, a.y});
-        pair((f2){a.z, a.w});
+        pair((f2){a.x, a.y}, acc);
+        pair((f2){a.z, a.w}, acc);
     }
     const f2 z = {0.f, 0.f};
     for (int e = 4 * lmin4; e < lmax; e += 4) {
@@ -453,6 +473,9 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
     const f2 sw_cinv = vpin(bc2(F.sw_cinv)), sw_cinv2 = vpin(bc2(F.sw_cinv2)),
              sw_clogs = vpin(bc2(F.sw_clogs));
     const f2 d_w = vpin(bc2(F.d_w)), d_c0 = vpin(bc2(F.d_c0)), d_m = vpin(bc2(F.d_m));
+    // (one slot: the direct term's weight per lane, zero where the lane's
+    // parameter has no direct term)
+    const f2 d_w1 = vpin(bc2(pdir[0] ? F.d_w : 0.0f));
     const f2 d_cinv = vpin(bc2(F.d_cinv)), d_cinv2 = vpin(bc2(F.d_cinv2)),
              d_clogs = vpin(bc2(F.d_clogs));
     const f2 half = bc2(0.5f), one = bc2(1.0f);
@@ -665,8 +688,12 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
         // K1 items, log p) nor its uniform branches and their live masks:
         // 0 first (l = 0 < L - 1), 1 intermediate, 2 last (l = L - 1 > 0),
         // 3 the only step (L = 1).  Returns false on an exchange timeout.
-        auto step = [&](int l, auto kind) -> bool {
+        // PAR: the record lines' parity when the caller knows it (an
+        // intermediate step, compiled once per parity: the publish and poll
+        // addresses are then fixed registers, no per-step selects), else -1
+        auto step = [&](int l, auto kind, auto parc) -> bool {
             constexpr int KIND = decltype(kind)::value;
+            constexpr int PAR = decltype(parc)::value;
             constexpr bool FIRST = KIND == 0 || KIND == 3, LAST = KIND == 2 || KIND == 3;
             (void)l;
             // no vector-memory operation is in flight here (the last poll was
@@ -735,17 +762,21 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 const f2 iv = DS ? is * is : d_cinv2;
 #pragma unroll
                 for (int r = 0; r < RS; ++r) {
-                    if (!pdir[r]) continue;
+                    // one slot: a lane without the term weighs it by zero (its
+                    // cotangent items 0 * finite, its gradient g - 0) instead
+                    // of branching around it under an exec mask
+                    if (RS > 1 && !pdir[r]) continue;
+                    const f2 dw = RS == 1 ? d_w1 : d_w;
                     const f2 d = q[r] - um;
                     const f2 s2 = d * d;
-                    const f2 u = d_w * (d * iv);
+                    const f2 u = dw * (d * iv);
                     acc(g[r], g0r[r], -u);
                     acc(cm, cm0, u);
-                    acc(cd, cd0, d_w * ((s2 * iv - one) * is));
+                    acc(cd, cd0, dw * ((s2 * iv - one) * is));
                     if (lst) {
                         const f2 lg = DS ? lf_sh2(sh.lg, kds) : d_clogs;
                         const f2 lpt = one * (d_c0 - lg) - (half * s2) * iv;
-                        acc(lpp, lpp0, d_w * lpt);
+                        acc(lpp, lpp0, dw * lpt);
                     }
                 }
             }
@@ -835,7 +866,7 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
                 k1w[1] = wave_sum(k1p[1]);
             }
             ++epoch;
-            const int par = epoch & 1;
+            const int par = PAR >= 0 ? PAR : (int)(epoch & 1);
             if constexpr (!X1 && !FIRST && !LAST) {
                 // an intermediate step: the record pairs only (addresses and
                 // the lane's pair fixed per launch)
@@ -996,12 +1027,17 @@ k_hmc_lf(LrCtx P, RunArgs A, int64_t chain_base, int64_t n_groups, mc_chain_scal
             MC_STAMP(4);
             return true;
         };
+        const std::integral_constant<int, -1> rtpar;
         if (L == 1) {
-            ok = step(0, std::integral_constant<int, 3>());
+            ok = step(0, std::integral_constant<int, 3>(), rtpar);
         } else {
-            ok = step(0, std::integral_constant<int, 0>());
-            for (int l = 1; ok && l < L - 1; ++l) ok = step(l, std::integral_constant<int, 1>());
-            if (ok) ok = step(L - 1, std::integral_constant<int, 2>());
+            ok = step(0, std::integral_constant<int, 0>(), rtpar);
+            for (int l = 1; ok && l < L - 1; ++l) {
+                if (X1) ok = step(l, std::integral_constant<int, 1>(), rtpar);
+                else if (epoch & 1) ok = step(l, std::integral_constant<int, 1>(), std::integral_constant<int, 0>());
+                else ok = step(l, std::integral_constant<int, 1>(), std::integral_constant<int, 1>());
+            }
+            if (ok) ok = step(L - 1, std::integral_constant<int, 2>(), rtpar);
         }
         if (!ok) break;
         // ---- accept / adapt (identical in every slice of the block) ------------
