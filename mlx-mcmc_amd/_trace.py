@@ -53,12 +53,22 @@ and beta.py:59-91).  What raises ``TraceError``, and why:
   the model is traced once, so a branch would freeze one side of it;
 * ``mx.where`` over a traced condition other than one comparison of traced
   values (x > y, mx.less(x, y) ...: a comparison node, no cotangent);
-* indexing a parameter expression or a log density (``(a + b * x)[i]``,
-  ``lp[i]``): index the parameter or the data before combining them;
-* a log density multiplied by a traced value (``lp * theta``): a term's
-  weight is a constant;
-* reductions other than a full ``mx.sum`` of a log density, multi-dimensional
-  or strided parameter indexing, and expression terms over 32 nodes.
+* indexing a log density (``lp[i]``): per-element log densities are summed
+  whole or over an axis;
+* a log density times a log density (``lp * lp``), divided into a constant
+  (``1 / lp``), or under a per-element weight after an axis reduction;
+* reductions other than ``mx.sum`` / ``mx.mean`` of a log density,
+  multi-dimensional or strided parameter indexing, and expression terms over
+  32 nodes.
+
+Indexing a parameter expression (``(a + b * x)[group]``, ``mx.exp(...)[i]``)
+pushes the index to its leaves — parameters become gathers (a gather of a
+gather composes), data is indexed on the host, scalars broadcast — so an
+indexed affine form stays affine.  A log density under a traced or
+per-element weight (``mx.sigmoid(t) * lp``, ``mx.sum(w * lp)``, ``lp /
+theta``) becomes expression terms whose roots are the terms' per-element log
+densities times (over) the weight, both factors differentiated as mx.grad
+differentiates the reference's product.
 """
 from __future__ import annotations
 
@@ -152,8 +162,17 @@ class Param:
         return self.shape[0]
 
     def __getitem__(self, idx):
-        if self.view is not None and self.view[0] != "slice":
-            raise TraceError("indexing a view of a parameter is not supported; " + _UNSUPPORTED)
+        if self.view is not None and self.view[0] == "elem":
+            raise TraceError(f"indexing a scalar view of parameter '{self.name}'")
+        if self.view is not None and self.view[0] == "gather":
+            # a gather of a gather: the composed index (NumPy indexing of the
+            # view's index array), as MLX indexes the gathered array
+            sub = np.asarray(self.view[1], np.int64).reshape(self.view[2])[idx]
+            if np.ndim(sub) == 0:
+                return Param(self.name, self.offset, self.base_shape, ("elem", int(sub)), self.xf)
+            sub = np.asarray(sub)
+            return Param(self.name, self.offset, self.base_shape,
+                         ("gather", sub.astype(np.int32).ravel(), sub.shape), self.xf)
         base = 0
         length = self.size
         if self.view is not None:
@@ -189,11 +208,15 @@ class Param:
     # affine arithmetic (a + b * x, the fast fused paths): see Affine; any
     # other elementwise arithmetic builds an expression (Expr)
     def __mul__(self, other):
+        if isinstance(other, LogProbExpr):  # theta * lp: a traced weight
+            return other * self
         if isinstance(other, Expr):
             return Expr.binary(_lib.MC_EX_MUL, self, other)
         return _affine_or_expr(lambda: Affine.product(self, other), _lib.MC_EX_MUL, self, other)
 
     def __rmul__(self, other):
+        if isinstance(other, LogProbExpr):
+            return other * self
         if isinstance(other, Expr):
             return Expr.binary(_lib.MC_EX_MUL, other, self)
         return _affine_or_expr(lambda: Affine.product(other, self), _lib.MC_EX_MUL, other, self)
@@ -363,9 +386,13 @@ class Affine:
         return Expr.binary(_lib.MC_EX_SUB, other, self)
 
     def __mul__(self, other):
+        if isinstance(other, LogProbExpr):
+            return other * self
         return Expr.binary(_lib.MC_EX_MUL, self, other)
 
     def __rmul__(self, other):
+        if isinstance(other, LogProbExpr):
+            return other * self
         return Expr.binary(_lib.MC_EX_MUL, other, self)
 
     def __truediv__(self, other):
@@ -387,8 +414,18 @@ class Affine:
         return Expr.unary(_lib.MC_EX_ABS, self)
 
     def __getitem__(self, item):
-        raise TraceError("indexing a traced parameter expression ((a + b * x)[i]: index the "
-                         "parameter or the data before the arithmetic): " + _UNSUPPORTED)
+        """(loc + slope * x)[i] = loc[i] + slope * x[i]: the index pushed to
+        the vector operands (an elementwise expression commutes with a
+        gather), so the result is the same affine form, rounded per element as
+        the reference's indexed MLX array.  A gather that repeats parameters
+        anywhere but in the loc over a data x (the fused affine terms' rule,
+        api.hip) makes it an expression instead."""
+        loc, x = _index_operand(self.loc, item), _index_operand(self.x, item)
+        x_data = x is None or not isinstance(x, Param)
+        if _repeats(x) or (_repeats(loc) and not x_data):
+            e = Expr.of(self)
+            return _index_expr(e, item, np.empty(e.shape, np.int8)[item].shape)
+        return Affine(loc, self.slope, x)
 
     def __float__(self):
         raise TraceError("float() of a traced parameter expression: " + _UNSUPPORTED)
@@ -517,9 +554,13 @@ class Expr:
         return Expr.binary(_lib.MC_EX_SUB, other, self)
 
     def __mul__(self, other):
+        if isinstance(other, LogProbExpr):
+            return other * self
         return Expr.binary(_lib.MC_EX_MUL, self, other)
 
     def __rmul__(self, other):
+        if isinstance(other, LogProbExpr):
+            return other * self
         return Expr.binary(_lib.MC_EX_MUL, other, self)
 
     def __truediv__(self, other):
@@ -541,8 +582,15 @@ class Expr:
         return Expr.unary(_lib.MC_EX_ABS, self)
 
     def __getitem__(self, item):
-        raise TraceError("indexing a traced expression (expr[i]: index the parameter or the "
-                         "data before the arithmetic): " + _UNSUPPORTED)
+        """expr[i]: the index pushed down to the leaves (every node is
+        elementwise, so indexing commutes with it): parameter leaves become
+        gathers / element views, data leaves are indexed on the host, scalar
+        operands broadcast unchanged.  The same per-element arithmetic as the
+        reference's indexed MLX array."""
+        if self.shape == ():
+            raise TraceError("indexing a scalar traced expression")
+        shape = np.empty(self.shape, np.int8)[item].shape  # (IndexError as NumPy's)
+        return _index_expr(self, item, shape)
 
     def __float__(self):
         raise TraceError("float() of a traced expression (a Python branch on a parameter value "
@@ -558,6 +606,41 @@ class Expr:
         if self.op == _lib.MC_EX_LEAF:
             return f"Expr(leaf {self.leaf!r})"
         return f"Expr(op {self.op}, {len(self.args)} args, shape={self.shape})"
+
+
+def _index_operand(v, item):
+    """An affine operand indexed: vectors (a parameter or data) take the index,
+    scalars broadcast unchanged."""
+    if v is None:
+        return None
+    if isinstance(v, Param):
+        return v if v.shape == () else v[item]
+    arr = np.asarray(_to_numpy(v))
+    if arr.ndim == 0:
+        return v
+    return np.ascontiguousarray(np.asarray(arr, np.float32)[item])
+
+
+def _repeats(v) -> bool:
+    """A parameter gather whose index repeats an element (non-injective)."""
+    if not (isinstance(v, Param) and v.view is not None and v.view[0] == "gather"):
+        return False
+    idx = np.asarray(v.view[1])
+    return np.unique(idx).size != idx.size
+
+
+def _index_expr(e: "Expr", item, shape) -> "Expr":
+    """e[item] with the index pushed to e's leaves (Expr.__getitem__)."""
+    if e.shape == ():
+        return e
+    if e.op == _lib.MC_EX_LEAF:
+        if isinstance(e.leaf, Param):
+            return Expr.of(e.leaf[item])
+        if isinstance(e.leaf, np.ndarray):
+            return Expr.of(e.leaf[item])
+        return e
+    args = [None if a is None else _index_expr(a, item, shape) for a in e.args]
+    return Expr(e.op, args, shape=shape)
 
 
 def expr_term(root: Expr) -> "LogProbExpr":
@@ -666,6 +749,10 @@ class Term:
     weight: float = 1.0
     aff: Optional[Tuple[Operand, Operand]] = None  # affine loc: (slope, x)
     expr: Optional["Expr"] = None                   # MC_DIST_EXPR: the root node
+    # the traced arguments the term was made from — (dist name, value, loc,
+    # scale) or ("identity", value) — so a traced or per-element weight can
+    # rebuild it as an expression (LogProbExpr._weighted)
+    src: Optional[tuple] = None
 
 
 def broadcast_n(dist_name: str, ops: List[Operand]) -> Tuple[int, Tuple[int, ...]]:
@@ -729,10 +816,45 @@ class LogProbExpr:
         return self * -1.0
 
     def __mul__(self, other):
+        if isinstance(other, (Param, Affine, Expr)) or _is_vector_const(other):
+            return self._weighted(other, _lib.MC_EX_MUL)
         c = _scalar_const(other)
         return LogProbExpr([_scaled(t, c) for t in self.terms], self.const * c, self.shape)
 
     __rmul__ = __mul__
+
+    def __truediv__(self, other):
+        if isinstance(other, (Param, Affine, Expr)) or _is_vector_const(other):
+            return self._weighted(other, _lib.MC_EX_DIV)
+        c = _scalar_const(other)
+        return self * float(np.float32(1.0) / np.float32(c))
+
+    def __rtruediv__(self, other):
+        raise TraceError("dividing by a log density: " + _UNSUPPORTED)
+
+    def _weighted(self, w, op: int) -> "LogProbExpr":
+        """lp * w or lp / w with w a traced value (a parameter, an affine or
+        elementwise expression) or a per-element data array: every term
+        becomes an expression term whose root is the term's per-element log
+        density times (or over) w — sum_i lp_i * w_i, as the reference's MLX
+        graph computes it and mx.grad differentiates it (both factors get a
+        cotangent).  w is a scalar or has the log density's shape."""
+        W = Expr.of(w)
+        if W.shape not in ((), self.shape):
+            raise TraceError(f"a log density of shape {self.shape} weighted by shape {W.shape} "
+                             "(a weight is a scalar or has the log density's shape)")
+        terms = []
+        for t in self.terms:
+            root = _term_root(t)
+            if W.shape != () and root.shape != self.shape:
+                raise TraceError("a per-element weight on a log density summed over some axes "
+                                 "(weight the unreduced log density): " + _UNSUPPORTED)
+            node = Expr(op, [root, W], shape=_bshape("weighted log density", [root.shape, W.shape]))
+            terms.append(Term(_lib.MC_DIST_EXPR, NONE_OPERAND, NONE_OPERAND, NONE_OPERAND,
+                              node.size, t.weight, None, node))
+        if self.const != 0.0:
+            terms += expr_term(Expr.binary(op, float(self.const), W)).terms
+        return LogProbExpr(terms, 0.0, self.shape)
 
     def _reduced(self, axis, keepdims):
         """The shape after summing `axis` (None, an int or a tuple; negative
@@ -816,12 +938,39 @@ def identity_expr(x) -> LogProbExpr:
     if const and shape != ():
         raise TraceError("adding a parameter vector plus a constant to a log density: "
                          + _UNSUPPORTED)
-    term = Term(_lib.MC_DIST_IDENTITY, op, NONE_OPERAND, NONE_OPERAND, n, weight)
+    term = Term(_lib.MC_DIST_IDENTITY, op, NONE_OPERAND, NONE_OPERAND, n, weight,
+                src=("identity", x))
     return LogProbExpr([term], const, shape)
 
 
 def _scaled(t: Term, c: float) -> Term:
-    return Term(t.dist, t.value, t.loc, t.scale, t.n, t.weight * c, t.aff, t.expr)
+    return Term(t.dist, t.value, t.loc, t.scale, t.n, t.weight * c, t.aff, t.expr, t.src)
+
+
+def _term_root(t: Term) -> "Expr":
+    """A term's per-element log density as an expression (its weight apart)."""
+    if t.dist == _lib.MC_DIST_EXPR:
+        return t.expr
+    if t.src is None:
+        raise TraceError("this log density cannot take a traced or per-element weight: "
+                         + _UNSUPPORTED)
+    if t.src[0] == "identity":
+        return Expr.of(t.src[1])
+    name, value, loc, scale = t.src
+    if name not in _EXPR_DIST:
+        raise TraceError(f"{name} under a traced or per-element weight: " + _UNSUPPORTED)
+    return dist_expr(name, value, loc, scale).terms[0].expr
+
+
+def _is_vector_const(x) -> bool:
+    """A non-scalar numeric constant (data), i.e. a per-element weight."""
+    if is_symbolic(x):
+        return False
+    try:
+        arr = np.asarray(_to_numpy(x))
+    except Exception:
+        return False
+    return arr.dtype != object and arr.size != 1
 
 
 def _scalar_const(x) -> float:
@@ -870,7 +1019,8 @@ def _make_fused_term(dist: int, dist_name: str, value, loc, scale) -> LogProbExp
     for o in ops + (list(aff) if aff else []):
         if o.kind in (_lib.MC_OP_DATA, _lib.MC_OP_GATHER) and o.shape == ():
             o.shape = (1,)
-    return LogProbExpr([Term(dist, ops[0], ops[1], ops[2], n, 1.0, aff)], 0.0, shape)
+    return LogProbExpr([Term(dist, ops[0], ops[1], ops[2], n, 1.0, aff,
+                             src=(dist_name, value, loc, scale))], 0.0, shape)
 
 
 def stack(items) -> LogProbExpr:

@@ -87,6 +87,9 @@ case $STEP in
   bench) bench "$@" ;;
   bench-lines) bench_lines ;;
   kt) n=$1; shift; prof kt_$n "$*" --kernel-trace --stats ;;
+  sq1)  # NAME [bench args]: the instruction-mix SQ pass alone
+    n=$1; shift
+    prof sq1_$n "$*" --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_SMEM ;;
   pmc)
     n=$1; k=$2; ipl=$3; lf=$4; fl=$5; key=$6; shift 6
     prof fetch_$n "$*" --pmc FETCH_SIZE && prof write_$n "$*" --pmc WRITE_SIZE &&

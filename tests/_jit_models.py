@@ -26,6 +26,8 @@ MODELS = {"two_predictor": W.two_predictor_regression,
           "gamma_beta": W.gamma_beta_regression,
           "axis_reductions": W.axis_reductions,
           "huber": W.huber_regression,
+          "weighted_indexed": W.weighted_indexed,
+          "tempered": W.tempered,
           "tiny_scalar": tiny_scalar}
 
 

@@ -42,6 +42,8 @@ MODELS = {"two_predictor": W.two_predictor_regression,
           "gamma_beta": W.gamma_beta_regression,
           "axis_reductions": W.axis_reductions,
           "huber": W.huber_regression,
+          "weighted_indexed": W.weighted_indexed,
+          "tempered": W.tempered,
           "tiny_scalar": tiny_scalar}
 POSITIVE = ("sigma", "v")
 
@@ -106,13 +108,19 @@ def test_expr_nan_and_support(gpu):
     ("axis_reductions", {"a": 0.4, "b": 1.4, "log_sigma": -0.4}, 0.01, 5),
     # mx.where over a traced condition (|residual| < c: comparison nodes)
     ("huber", {"a": 0.4, "b": 1.3}, 0.01, 6),
+    # per-observation weights, indexed affine / elementwise expressions
+    ("weighted_indexed", {"alpha": np.zeros(8), "beta": 0.5, "log_sigma": -0.3, "c": 0.0},
+     0.02, 7),
+    # a likelihood under a traced weight (mx.sigmoid(t) * lp), a log density
+    # divided by a parameter expression
+    ("tempered", {"mu": 1.0, "t": 0.5, "log_s": 0.0}, 0.15, 8),
 ])
 def test_expr_hmc_trace_matches_oracle(gpu, model, start, eps, seed):
     import mlx_mcmc_amd as m
 
     lp, _ = MODELS[model](W.ns_product())
     olp, _ = MODELS[model](W.ns_oracle())
-    start = {k: np.float32(v) for k, v in start.items()}
+    start = {k: np.asarray(v, np.float32) if np.ndim(v) else np.float32(v) for k, v in start.items()}
     kw = dict(num_samples=40, num_warmup=40, step_size=eps, num_leapfrog_steps=10)
     s, rate, info = m.hmc(lp, start, key=m.random.key(seed), progress=False, return_info=True,
                           return_trace=True, **kw)
@@ -135,7 +143,8 @@ def test_expr_hmc_trace_matches_oracle(gpu, model, start, eps, seed):
     name = list(start)[0]
     # positions: the same draws and decisions, 1-ulp transcendental
     # differences carried through the leapfrog steps
-    np.testing.assert_allclose(s[name][:ns], ref.samples[:ns, 0], rtol=1e-3, atol=2e-3)
+    first = np.asarray(s[name]).reshape(np.asarray(s[name]).shape[0], -1)[:, 0]
+    np.testing.assert_allclose(first[:ns], ref.samples[:ns, 0], rtol=1e-3, atol=2e-3)
 
 
 def test_expr_varying_slopes_hmc_trace(gpu):

@@ -141,14 +141,18 @@ X3 = np.arange(3, dtype=np.float32)
     (lambda p: m.Normal(0, 1).log_prob(p["v"]), "must return a scalar"),  # unsummed vector
     (lambda p: m.Normal(0, 1).log_prob(p["x"]) + p["v"],                   # unsummed identity
      "adding a scalar log density to an unsummed vector one"),
-    (lambda p: mx.sum(m.Normal(0, 1).log_prob((p["v"] * 2.0)[0])),         # indexing an expr
-     "indexing a traced"),
+    (lambda p: m.Normal(0, 1).log_prob(mx.tanh(p["x"])[0]),                 # indexing a scalar
+     "indexing a scalar"),
     (lambda p: mx.sum(mx.where((p["v"] > 0) * 1.0, p["v"], 0.0)),           # arithmetic mask
      "mx.where over a traced condition other than one comparison"),
-    (lambda p: m.Normal(0, 1).log_prob(p["x"]) * p["x"],                   # density x parameter
+    (lambda p: m.Normal(0, 1).log_prob(p["x"]) * m.Normal(0, 1).log_prob(p["x"]),  # lp * lp
      "a log density times a traced value"),
-    (lambda p: mx.sum(m.Normal(0, 1).log_prob(p["v"]) * X3),               # per-element weights
-     "a log density times a non-scalar constant"),
+    (lambda p: mx.sum(m.Normal(0, 1).log_prob(p["v"]) * np.ones(4, np.float32)),  # bad weight
+     "weighted by shape (4,)"),
+    (lambda p: mx.sum(mx.sum(m.Normal(p["x"], 1.0).log_prob(np.ones((2, 3), np.float32)),
+                             axis=1) * np.ones(2, np.float32)),          # weight after an axis sum
+     "a per-element weight on a log density summed over some axes"),
+    (lambda p: 1.0 / m.Normal(0, 1).log_prob(p["x"]), "dividing by a log density"),
     (lambda p: mx.sum(m.Normal(p["v"] * X3, 1.0).log_prob(np.zeros(4, np.float32))),
      "cannot broadcast shapes"),
     (lambda p: mx.sum(_deep(p["v"], 40)), "nodes (at most 32)"),           # too deep
@@ -200,6 +204,17 @@ def _deep(x, k):
     lambda p: mx.sum(mx.where(p["v"] > 0, p["v"], 0.0)),          # a traced condition
     lambda p: mx.sum(mx.where(mx.abs(p["v"] - X3) < p["x"], mx.square(p["v"]), p["v"])),
     lambda p: mx.sum(mx.where(mx.less_equal(X3, p["v"]), 1.0, -mx.square(p["v"]))),
+    # indexing pushed to the leaves: an expression, an affine form, a gather
+    # of a gather
+    lambda p: mx.sum(m.Normal(0, 1).log_prob((p["v"] * 2.0)[np.array([0, 2, 2])])),
+    lambda p: mx.sum(m.Normal(mx.exp(p["x"] * X3)[1:], 1.0).log_prob(X3[:2])),
+    lambda p: mx.sum(m.Normal(0, 1).log_prob(mx.tanh(p["v"][np.array([2, 1, 0])])[np.array([0, 0])])),
+    # log densities under traced or per-element weights
+    lambda p: m.Normal(0, 1).log_prob(p["x"]) * p["x"],
+    lambda p: mx.sigmoid(p["y"]) * mx.sum(m.Normal(p["x"], 1.0).log_prob(X3)),
+    lambda p: mx.sum(m.Normal(0, 1).log_prob(p["v"]) * X3),
+    lambda p: mx.sum(X3 * m.HalfNormal(mx.exp(p["x"])).log_prob(X3 + 1.0)),
+    lambda p: (m.Normal(0, 1).log_prob(p["x"]) + 2.0) / (1.0 + p["y"] * p["y"]),
 ])
 def test_general_expressions_trace(good):
     tm = _trace.trace(good, {"x": 1.0, "y": 0.5, "v": np.zeros(3, np.float32)})
@@ -233,6 +248,51 @@ def test_expression_models_trace_to_expected_terms():
     for f in (W.logistic_regression, W.cauchy_location):
         tm = _trace.trace(*f(W.ns_product()))
         assert any(t.dist == _lib.MC_DIST_EXPR for t in tm.terms)
+
+
+def test_indexing_pushes_to_the_leaves():
+    """(alpha + beta * z)[group] stays the fused affine form (loc a gather of
+    alpha, x the host-indexed z); an elementwise expression indexed by the
+    group gathers its parameter leaves; the gather of a gather composes."""
+    z = np.arange(4, dtype=np.float32)
+    grp = np.array([0, 3, 3, 1, 2, 0])
+    y = np.linspace(-1, 1, 6).astype(np.float32)
+
+    def lp(p):
+        mu = (p["a"] + p["b"] * z)[grp]
+        sc = mx.exp(p["b"] * z + 0.5)[grp]
+        return mx.sum(m.Normal(mu, 1.0).log_prob(y)) + mx.sum(m.Normal(0, sc).log_prob(y))
+
+    tm = _trace.trace(lp, {"a": np.zeros(4, np.float32), "b": 0.5})
+    aff = [t for t in tm.terms if t.aff is not None]
+    assert len(aff) == 1 and aff[0].loc.kind == _lib.MC_OP_GATHER
+    assert list(aff[0].loc.index) == list(grp)
+    assert aff[0].aff[1].kind == _lib.MC_OP_DATA and np.array_equal(aff[0].aff[1].data, z[grp])
+    ex = [t for t in tm.terms if t.dist == _lib.MC_DIST_EXPR]
+    assert len(ex) == 1 and ex[0].n == 6
+    v = _trace.Param("v", 0, (5,))
+    g = v[np.array([4, 3, 2])][np.array([2, 2, 0])]
+    assert g.view[0] == "gather" and list(g.view[1]) == [2, 2, 4]
+    assert v[np.array([4, 3])][1].view == ("elem", 3)
+
+
+def test_traced_weights_make_expression_terms():
+    """lp * w with w traced or per-element data: every term of lp becomes an
+    expression term whose root is its log density times w (the fused
+    Normal's arguments rebuilt as an MC_EX_NORMAL_LP node); a constant part
+    of lp becomes a term of its own."""
+    X = np.arange(3, dtype=np.float32)
+
+    def lp(p):
+        base = m.Normal(p["x"], 1.0).log_prob(X)                 # fused, vector
+        return mx.sum(base * X) + (m.HalfNormal(2).log_prob(p["y"]) + 1.5) * p["x"]
+
+    tm = _trace.trace(lp, {"x": 1.0, "y": 0.5})
+    assert [t.dist for t in tm.terms] == [_lib.MC_DIST_EXPR] * 3
+    assert [t.n for t in tm.terms] == [3, 1, 1]
+    ops = [tm.c_nodes[i].op for i in range(tm.n_nodes)]
+    assert _lib.MC_EX_NORMAL_LP in ops and _lib.MC_EX_HALFNORMAL_LP in ops
+    assert ops.count(_lib.MC_EX_MUL) == 3
 
 
 def test_layout_roundtrip():

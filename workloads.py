@@ -359,6 +359,55 @@ def huber_regression(ns, n=1000, c=1.0):
     return log_prob, {"a": np.float32(0.4), "b": np.float32(1.3)}
 
 
+def weighted_indexed_data(G=8, n=400, seed=9):
+    rng = np.random.default_rng(seed)
+    group = rng.integers(0, G, n).astype(np.int64)           # unsorted, repeats
+    z = rng.normal(0.0, 1.0, G).astype(np.float32)            # a group-level covariate
+    w = rng.uniform(0.5, 1.5, n).astype(np.float32)           # per-observation weights
+    alpha = rng.normal(0.5, 1.0, G)
+    y = (alpha[group] + 0.8 * z[group] + rng.normal(0.0, 0.6, n)).astype(np.float32)
+    return group, z, w, y
+
+
+def weighted_indexed(ns, G=8, n=400):
+    """Per-observation weights on a log density (mx.sum(w * lp)), an indexed
+    affine expression ((alpha + beta * z)[group]) and an indexed elementwise
+    expression (mx.exp(...)[group] as a per-group scale)."""
+    group, z, w, y = weighted_indexed_data(G, n)
+
+    def log_prob(params):
+        al, b, ls, c = params["alpha"], params["beta"], params["log_sigma"], params["c"]
+        lp = ns.sum(ns.Normal(0, 2).log_prob(al)) + ns.Normal(0, 2).log_prob(b)
+        lp = lp + ns.Normal(0, 1).log_prob(ls) + ns.Normal(0, 1).log_prob(c)
+        mu = (al + b * ns.array(z))[group]
+        scale = ns.exp(ls + c * ns.array(z))[group]
+        return lp + ns.sum(ns.array(w) * ns.Normal(mu, scale).log_prob(ns.array(y)))
+
+    return log_prob, {"alpha": np.zeros(G, np.float32), "beta": np.float32(0.5),
+                      "log_sigma": np.float32(-0.3), "c": np.float32(0.0)}
+
+
+def tempered_data(n=300, seed=10):
+    rng = np.random.default_rng(seed)
+    return rng.normal(1.5, 0.8, n).astype(np.float32)
+
+
+def tempered(ns, n=300):
+    """A likelihood weighted by a parameter (mx.sigmoid(t) * lp, a power
+    posterior whose temperature is sampled) and a log density divided by a
+    parameter expression: log densities under traced weights."""
+    y = tempered_data(n)
+
+    def log_prob(params):
+        mu, t, ls = params["mu"], params["t"], params["log_s"]
+        lp = ns.Normal(0, 5).log_prob(mu) + ns.Normal(0, 1).log_prob(t)
+        lp = lp + ns.Normal(0, 1).log_prob(ls) / (1.0 + ns.square(t))
+        lik = ns.sum(ns.Normal(mu, ns.exp(ls)).log_prob(ns.array(y)))
+        return lp + ns.sigmoid(t) * lik
+
+    return log_prob, {"mu": np.float32(1.0), "t": np.float32(0.5), "log_s": np.float32(0.0)}
+
+
 def logistic_data(n=500, seed=6):
     rng = np.random.default_rng(seed)
     x = rng.normal(0.0, 1.0, n).astype(np.float32)
