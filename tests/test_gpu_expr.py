@@ -113,7 +113,7 @@ def test_expr_nan_and_support(gpu):
      0.02, 7),
     # a likelihood under a traced weight (mx.sigmoid(t) * lp), a log density
     # divided by a parameter expression
-    ("tempered", {"mu": 1.0, "t": 0.5, "log_s": 0.0}, 0.15, 8),
+    ("tempered", {"mu": 1.0, "t": 0.5, "log_s": 0.0}, 0.05, 8),
 ])
 def test_expr_hmc_trace_matches_oracle(gpu, model, start, eps, seed):
     import mlx_mcmc_amd as m
