@@ -600,6 +600,10 @@ def main_nuts(args):
     launch_ms_total = float(sum(a.elapsed_time(b) for a, b in ev))
     elapsed = max_over_ranks(elapsed, device=dev)
     leaves_all = int(sum_over_ranks(float(leaves), device=dev))   # every rank's chains
+    # ESS/s of the timed draws (the metric's second half; every chain's
+    # draws — a NUTS step always returns a state of its trajectory — with the
+    # same R-hat gate as the HMC line; collective under torch.distributed)
+    ess = ess_block(samples, np.ones(C, np.int64), K, elapsed)
     if rank == 0:
         value = leaves_all / elapsed
         # per launch: the timed leaves spread over the launches by their time
@@ -645,6 +649,8 @@ def main_nuts(args):
             "accept_stat_mean": float(np.mean(sc["alpha_sum"]) / max(Wm + K, 1)),
             "step_size": float(np.mean(sc["step_size"])),
             "clock_warm_ms": args.clock_warm_ms,
+            "ess_per_sec": ess.pop("ess_per_sec"),
+            "ess_timed": ess,
         }
         if world == 1 and not args.no_cpu_baseline:
             cb = nuts_cpu_baseline(min(args.cpu_seconds, 15.0), args)
