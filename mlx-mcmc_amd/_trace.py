@@ -1365,6 +1365,45 @@ class Program:
             self.handle = None
 
 
+def affine_as_expressions(model: TracedModel) -> Optional[TracedModel]:
+    """The same model with every fused affine-loc term (``Normal(a + b * x,
+    s)``, mc_affine) rebuilt as an expression term of the same per-element
+    arithmetic (its MC_EX_NORMAL_LP node over ADD(a, MUL(b, x))), the other
+    terms unchanged; None when the model has no such term.  The sliced NUTS
+    kernel takes expression terms (LS_EXPR, csrc/nuts_sliced.h) but not affine
+    ones, so this form moves NUTS on a large regression off the tape."""
+    if not any(t.aff is not None for t in model.terms):
+        return None
+    terms = []
+    for t in model.terms:
+        if t.aff is None:
+            terms.append(t)
+            continue
+        root = _term_root(t)
+        terms.append(Term(_lib.MC_DIST_EXPR, NONE_OPERAND, NONE_OPERAND, NONE_OPERAND,
+                          root.size, t.weight, None, root))
+    out = TracedModel(model.layout, terms, model.lp_const)
+    _build_pools(out)
+    return out
+
+
+def nuts_program(prog: "Program", max_tree_depth: int = 10) -> "Program":
+    """The program NUTS runs: `prog`, or — when its affine-loc terms keep
+    NUTS on the chain-per-workgroup tape and the same model with those terms
+    as expression terms plans onto the sliced kernel — that program.  (HMC
+    keeps `prog`: the lane kernel k_hmc_lr runs affine terms natively.)"""
+    if prog.nuts_kernel(max_tree_depth) != "tape":
+        return prog
+    try:
+        alt = affine_as_expressions(prog.model)
+    except TraceError:
+        return prog
+    if alt is None:
+        return prog
+    p2 = Program(alt)
+    return p2 if p2.nuts_kernel(max_tree_depth) == "sliced" else prog
+
+
 def compile_model(log_prob_fn, initial_params: dict, slices: int = 0,
                   slice_kernel: str = "auto") -> Program:
     _lib.require_device()

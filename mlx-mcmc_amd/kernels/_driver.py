@@ -71,6 +71,10 @@ def run_sampler(algorithm: str, log_prob_fn, initial_params, *, num_samples: int
     k = _as_key(key)
     program = _trace.compile_model(log_prob_fn, initial_params, slices=num_slices,
                                    slice_kernel=slice_kernel)
+    if algorithm == "nuts" and num_slices == 0 and slice_kernel == "auto":
+        # a large regression's affine terms as expression terms: the sliced
+        # NUTS kernel instead of the tape (_trace.nuts_program)
+        program = _trace.nuts_program(program, max_tree_depth)
     layout = program.layout
     note = program.kernel_note
     # no warning where the user cannot act on it: no lane-resident kernel

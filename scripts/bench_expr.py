@@ -116,11 +116,14 @@ for jit, sl, nm in VARIANTS:
           f"(kernel {k}; build {tb:.2f} s)")
 
 
-def nuts_rate(lp, init, slices, chains=256, eps=2e-3, iters=10):
+def nuts_rate(lp, init, slices, chains=256, eps=2e-3, iters=10, nuts_program=False):
     """NUTS leaf-steps/s (all chains) at a fixed step size: slices 0 = the
     sliced kernel (k_nuts_sl's run-time form JIT-compiled with the expression
-    terms), 1 = the tape (k_nuts)."""
+    terms), 1 = the tape (k_nuts); nuts_program: the program nuts() runs
+    (_trace.nuts_program: affine terms as expression terms)."""
     prog = _trace.compile_model(lp, init, slices=slices)
+    if nuts_program:
+        prog = _trace.nuts_program(prog, 10)
     kern = prog.nuts_kernel(10)
     cs = _engine.ChainSet(prog, chains, prog.layout.flatten(init), eps,
                           device=torch.device("cuda"))
@@ -147,3 +150,11 @@ for name, f, start, eps in (
     for sl in (0, 1):
         r, k = nuts_rate(lpn, start, sl, eps=eps)
         print(f"{name} N={N} NUTS (fixed eps {eps}): {r / 1e6:.3f} M leaf-steps/s (kernel {k})")
+
+# a fused affine-loc regression: the tape, and the program nuts() runs (the
+# affine term as an expression term on the sliced kernel)
+start = {"a": np.float32(1.5), "b": np.float32(2.0), "sigma": np.float32(0.5)}
+for label, conv in (("fused affine term, tape", False), ("nuts() program", True)):
+    r, k = nuts_rate(fused, start, 0, eps=1e-3, nuts_program=conv)
+    print(f"regression N={N} NUTS {label} (fixed eps 0.001): {r / 1e6:.3f} M leaf-steps/s "
+          f"(kernel {k})")

@@ -156,6 +156,50 @@ def test_expr_lanes_nuts_matches_oracle(gpu, model, eps, seed):
     assert np.all(info2.mean_tree_depth >= 1)
 
 
+def test_affine_regression_nuts_runs_sliced(gpu):
+    """NUTS on a linear regression at N = 100 K: its fused affine-loc term
+    keeps k_nuts_lr / k_nuts_sl off and would run the tape (k_nuts); nuts()
+    runs the same model with that term as an expression term
+    (_trace.nuts_program) on the sliced kernel instead.  Trees identical to
+    the oracle's for >= 6 iterations on two chains at a fixed step size, the
+    draws before the first difference within rtol 1e-3 (as above)."""
+    import mlx_mcmc_amd as m
+    from mlx_mcmc_amd import _trace
+
+    x, y = W.regression_data(N)
+    b, a = np.polyfit(x.astype(np.float64), y.astype(np.float64), 1)
+    sd = float(np.std(y - (a + b * x)))
+    start = {"a": np.float32(a), "b": np.float32(b), "sigma": np.float32(sd)}
+    lp, _ = W.linear_regression(W.ns_product(), N)
+    olp, _ = W.linear_regression(W.ns_oracle(), N)
+    prog = _trace.compile_model(lp, start)
+    assert prog.model.n_affines == 1 and prog.nuts_kernel(10) == "tape"
+    alt = _trace.nuts_program(prog, 10)
+    assert alt is not prog and alt.nuts_kernel(10) == "sliced"
+    kw = dict(num_samples=8, num_warmup=4, step_size=2e-3, max_tree_depth=10,
+              adapt_step_size=False)
+    s, rate, info = m.nuts(lp, start, key=m.random.key(41), num_chains=8, progress=False,
+                           return_info=True, return_trace=True, keep_on_device=True, **kw)
+    assert info.extra["kernel"] == "sliced"
+    draws = info.device_samples.cpu().numpy()
+    n = kw["num_samples"] + kw["num_warmup"]
+    tr = info.trace
+    for c in (0, 3):
+        ref = S.nuts(olp, start, seed=41, chain=c, **kw)
+        same = 0
+        for i in range(n):
+            if (tr["tree_depth"][c][i] != ref.trace["depth"][i]
+                    or tr["n_leapfrog"][c][i] != ref.trace["leaves"][i]):
+                break
+            same += 1
+        print(f"affine regression NUTS chain {c}: trees identical for {same} of {n}, depths "
+              f"{list(ref.trace['depth'][:same])}")
+        assert same >= 6, f"chain {c}: trees differ at iteration {same}"
+        ns = max(0, same - kw["num_warmup"])
+        np.testing.assert_allclose(draws[c, :ns], np.asarray(ref.samples)[:ns], rtol=1e-3,
+                                   atol=1e-4, err_msg=f"affine regression NUTS chain {c}")
+
+
 @pytest.mark.parametrize("model,scale,seed", [("logistic", 4e-3, 31), ("huber", 3e-3, 32)])
 def test_expr_lanes_mh_matches_oracle(gpu, model, scale, seed):
     """Random-walk MH (metropolis.py:6-101, the MCMC.run default) on the

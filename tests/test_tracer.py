@@ -295,6 +295,24 @@ def test_traced_weights_make_expression_terms():
     assert ops.count(_lib.MC_EX_MUL) == 3
 
 
+def test_affine_terms_as_expressions():
+    """_trace.affine_as_expressions (the NUTS program of a regression): the
+    fused affine-loc term becomes one expression term, NORMAL_LP over
+    ADD(a, MUL(b, x)), the priors stay fused; a model without affine terms
+    gives None."""
+    lp, init = W.linear_regression(W.ns_product(), 50)
+    tm = _trace.trace(lp, init)
+    assert tm.n_affines == 1
+    alt = _trace.affine_as_expressions(tm)
+    assert alt.n_affines == 0 and alt.n_exprs == 1
+    assert [t.dist for t in alt.terms].count(_lib.MC_DIST_EXPR) == 1
+    assert len(alt.terms) == len(tm.terms) and alt.lp_const == tm.lp_const
+    ops = [alt.c_nodes[i].op for i in range(alt.n_nodes)]
+    assert ops[-1] == _lib.MC_EX_NORMAL_LP and _lib.MC_EX_ADD in ops and _lib.MC_EX_MUL in ops
+    lp2, init2 = W.two_predictor_regression(W.ns_product())
+    assert _trace.affine_as_expressions(_trace.trace(lp2, init2)) is None
+
+
 def test_layout_roundtrip():
     init = {"a": 1.0, "b": np.arange(6, dtype=np.float32).reshape(2, 3), "c": 2.0}
     lay = _trace.layout_of(init)
