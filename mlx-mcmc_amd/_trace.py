@@ -1404,6 +1404,23 @@ def nuts_program(prog: "Program", max_tree_depth: int = 10) -> "Program":
     return p2 if p2.nuts_kernel(max_tree_depth) == "sliced" else prog
 
 
+def mh_program(prog: "Program") -> "Program":
+    """The program random-walk MH runs: `prog`, or its affine-loc terms as
+    expression terms (affine_as_expressions) when that moves MH from the
+    tape (k_mh) onto the sliced kernel k_mh_sl (value-only LS_EXPR pass)."""
+    lib = _lib.load()
+    if lib.mc_program_mh_sliced(prog.handle) == 1:
+        return prog
+    try:
+        alt = affine_as_expressions(prog.model)
+    except TraceError:
+        return prog
+    if alt is None:
+        return prog
+    p2 = Program(alt)
+    return p2 if lib.mc_program_mh_sliced(p2.handle) == 1 else prog
+
+
 def compile_model(log_prob_fn, initial_params: dict, slices: int = 0,
                   slice_kernel: str = "auto") -> Program:
     _lib.require_device()

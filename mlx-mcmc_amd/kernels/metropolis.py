@@ -44,7 +44,9 @@ def metropolis_hastings(log_prob_fn, initial_params, num_samples=1000, proposal_
     if num_samples < 0:
         raise ValueError("num_samples must be non-negative")
     k = _as_key(random_seed)
-    program = _trace.compile_model(log_prob_fn, initial_params)
+    # (a large regression's affine terms as expression terms: the sliced MH
+    # kernel instead of the tape, _trace.mh_program)
+    program = _trace.mh_program(_trace.compile_model(log_prob_fn, initial_params))
     layout = program.layout
     C = int(num_chains)
     if C < 1:

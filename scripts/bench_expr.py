@@ -158,3 +158,31 @@ for label, conv in (("fused affine term, tape", False), ("nuts() program", True)
     r, k = nuts_rate(fused, start, 0, eps=1e-3, nuts_program=conv)
     print(f"regression N={N} NUTS {label} (fixed eps 0.001): {r / 1e6:.3f} M leaf-steps/s "
           f"(kernel {k})")
+
+
+
+def mh_rate(lp, init, chains=256, scale=2e-3, iters=200, mh_program=False):
+    """Random-walk MH chain-iterations/s (all chains): the compiled program,
+    or the one metropolis_hastings() runs (_trace.mh_program)."""
+    prog = _trace.compile_model(lp, init)
+    if mh_program:
+        prog = _trace.mh_program(prog)
+    kern = "sliced" if LIB.mc_program_mh_sliced(prog.handle) == 1 else "tape"
+    cs = _engine.ChainSet(prog, chains, prog.layout.flatten(init), scale,
+                          device=torch.device("cuda"))
+    cfg = dict(chain_offset=0, num_warmup=0, num_samples=0, sample_begin=0,
+               sample_capacity=0, seed=0)
+    cs.run_mh(proposal_scale=scale, iter_begin=0, iter_count=20, **cfg)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    cs.run_mh(proposal_scale=scale, iter_begin=20, iter_count=iters, **cfg)
+    e1.record()
+    torch.cuda.synchronize()
+    cs.check_status()
+    return chains * iters / (e0.elapsed_time(e1) * 1e-3), kern
+
+
+for label, conv in (("fused affine term", False), ("metropolis_hastings() program", True)):
+    r, k = mh_rate(fused, start, mh_program=conv)
+    print(f"regression N={N} MH {label}: {r / 1e6:.3f} M chain-iterations/s (kernel {k})")

@@ -238,3 +238,48 @@ def test_expr_lanes_mh_matches_oracle(gpu, model, scale, seed):
     draws = info.device_samples[0].cpu().numpy()
     np.testing.assert_allclose(draws[:same], np.asarray(ref.samples)[:same], rtol=1e-5,
                                atol=1e-6)
+
+
+def test_affine_regression_mh_runs_sliced(gpu):
+    """Random-walk MH on the N = 100 K linear regression: the fused affine
+    term keeps k_mh_sl off; metropolis_hastings() runs the model with it as an
+    expression term (_trace.mh_program) on the sliced kernel.  Decisions equal
+    the oracle's until a proven near-tie, log p and draws before it (the bars
+    of test_expr_lanes_mh_matches_oracle)."""
+    import mlx_mcmc_amd as m
+    from mlx_mcmc_amd import _lib, _trace
+    from _near_tie import tie_bound
+
+    x, y = W.regression_data(N)
+    b, a = np.polyfit(x.astype(np.float64), y.astype(np.float64), 1)
+    sd = float(np.std(y - (a + b * x)))
+    start = {"a": np.float32(a), "b": np.float32(b), "sigma": np.float32(sd)}
+    lp, _ = W.linear_regression(W.ns_product(), N)
+    olp, _ = W.linear_regression(W.ns_oracle(), N)
+    lib = _lib.load()
+    prog = _trace.compile_model(lp, start)
+    assert lib.mc_program_mh_sliced(prog.handle) == 0
+    assert lib.mc_program_mh_sliced(_trace.mh_program(prog).handle) == 1
+    n, scale, seed = 60, 2e-3, 42
+    s, rate, info = m.metropolis_hastings(lp, start, num_samples=n, proposal_scale=scale,
+                                          random_seed=seed, return_info=True,
+                                          return_trace=True, keep_on_device=True)
+    ref = S.metropolis_hastings(olp, start, num_samples=n, proposal_scale=scale,
+                                random_seed=seed)
+    acc = info.trace["accepted"][0].astype(bool)
+    racc = np.array(ref.trace["accepted"])
+    assert 0 < racc.sum() < n, "mixed decisions"
+    flips = np.nonzero(acc != racc)[0]
+    same = int(flips[0]) if flips.size else n
+    print(f"affine regression MH: decisions identical for {same} of {n}")
+    if same < n:
+        lu = log_u(m.random.key(seed).seed, 0, n)
+        tie = tie_bound(ref.trace["logp"][same])
+        gap = abs(float(lu[same]) - ref.trace["ratio"][same])
+        assert gap <= tie, f"flip at {same} is not a near-tie: gap {gap} > {tie}"
+    assert same >= 20
+    np.testing.assert_allclose(info.trace["energy"][0][:same], ref.trace["logp"][:same],
+                               rtol=2e-6)
+    draws = info.device_samples[0].cpu().numpy()
+    np.testing.assert_allclose(draws[:same], np.asarray(ref.samples)[:same], rtol=1e-5,
+                               atol=1e-6)
