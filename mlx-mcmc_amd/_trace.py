@@ -1365,21 +1365,58 @@ class Program:
             self.handle = None
 
 
-def affine_as_expressions(model: TracedModel) -> Optional[TracedModel]:
+def _has_data_leaf(e: "Expr") -> bool:
+    if e.op == _lib.MC_EX_LEAF:
+        return isinstance(e.leaf, np.ndarray)
+    return any(a is not None and _has_data_leaf(a) for a in e.args)
+
+
+def _own_prior_like(t: Term) -> bool:
+    """A scalar term the sliced kernels evaluate as a shared parameter's own
+    prior (api.hip plan_lanes LrSterm::own): Normal / HalfNormal of an
+    untransformed scalar parameter with constant loc and scale."""
+    return (t.dist in (_lib.MC_DIST_NORMAL, _lib.MC_DIST_HALFNORMAL) and t.aff is None
+            and t.value.kind == _lib.MC_OP_PSCALAR and t.value.transform == 0
+            and t.loc.kind in (_lib.MC_OP_CONST, _lib.MC_OP_NONE)
+            and t.scale.kind == _lib.MC_OP_CONST)
+
+
+def affine_as_expressions(model: TracedModel, scalars: bool = False) -> Optional[TracedModel]:
     """The same model with every fused affine-loc term (``Normal(a + b * x,
     s)``, mc_affine) rebuilt as an expression term of the same per-element
     arithmetic (its MC_EX_NORMAL_LP node over ADD(a, MUL(b, x))), the other
-    terms unchanged; None when the model has no such term.  The sliced NUTS
-    kernel takes expression terms (LS_EXPR, csrc/nuts_sliced.h) but not affine
-    ones, so this form moves NUTS on a large regression off the tape."""
-    if not any(t.aff is not None for t in model.terms):
+    terms unchanged; None when nothing changes.  The sliced NUTS / MH kernels
+    take expression terms (LS_EXPR, csrc/nuts_sliced.h, mh_sliced.h) but not
+    affine ones, so this form moves NUTS and MH on a large regression off the
+    tape.  scalars: also every scalar term those kernels cannot take as a
+    shared parameter's own prior (``Exponential(1).log_prob(sigma)``, a
+    second prior on one parameter, a prior with a parameter argument) — the
+    kernels evaluate scalar terms only as own priors."""
+    owned = set()
+    convert = []
+    for t in model.terms:
+        c = t.aff is not None
+        if scalars and not c and t.n == 1 and t.dist not in (_lib.MC_DIST_EXPR,
+                                                             _lib.MC_DIST_IDENTITY):
+            own = _own_prior_like(t) and t.value.param_offset not in owned
+            if own:
+                owned.add(t.value.param_offset)
+            c = not own and t.src is not None and t.src[0] in _EXPR_DIST
+        convert.append(c)
+    if not any(convert):
         return None
     terms = []
-    for t in model.terms:
-        if t.aff is None:
+    for t, c in zip(model.terms, convert):
+        if not c:
             terms.append(t)
             continue
         root = _term_root(t)
+        if not _has_data_leaf(root):
+            # the lane planner tiles an expression term by its data arrays
+            # (host.h expr_lanes_ok): a scalar prior gets a one-element mask,
+            # where(1, lp, lp) — the same value and the same cotangent
+            mask = Expr.of(np.ones(max(root.size, 1), np.float32).reshape(root.shape or (1,)))
+            root = Expr(_lib.MC_EX_WHERE, [mask, root, root], shape=mask.shape)
         terms.append(Term(_lib.MC_DIST_EXPR, NONE_OPERAND, NONE_OPERAND, NONE_OPERAND,
                           root.size, t.weight, None, root))
     out = TracedModel(model.layout, terms, model.lp_const)
@@ -1388,37 +1425,45 @@ def affine_as_expressions(model: TracedModel) -> Optional[TracedModel]:
 
 
 def nuts_program(prog: "Program", max_tree_depth: int = 10) -> "Program":
-    """The program NUTS runs: `prog`, or — when its affine-loc terms keep
-    NUTS on the chain-per-workgroup tape and the same model with those terms
-    as expression terms plans onto the sliced kernel — that program.  (HMC
-    keeps `prog`: the lane kernel k_hmc_lr runs affine terms natively.)"""
+    """The program NUTS runs: `prog`, or — when its affine-loc terms (and,
+    failing that, its scalar terms other than own priors) keep NUTS on the
+    chain-per-workgroup tape and the same model with those terms as
+    expression terms plans onto the sliced kernel — that program.  (HMC keeps
+    `prog`: the lane kernel k_hmc_lr runs affine and generic scalar terms.)"""
     if prog.nuts_kernel(max_tree_depth) != "tape":
         return prog
-    try:
-        alt = affine_as_expressions(prog.model)
-    except TraceError:
-        return prog
-    if alt is None:
-        return prog
-    p2 = Program(alt)
-    return p2 if p2.nuts_kernel(max_tree_depth) == "sliced" else prog
+    for scalars in (False, True):
+        try:
+            alt = affine_as_expressions(prog.model, scalars)
+        except TraceError:
+            continue
+        if alt is None:
+            continue
+        p2 = Program(alt)
+        if p2.nuts_kernel(max_tree_depth) == "sliced":
+            return p2
+    return prog
 
 
 def mh_program(prog: "Program") -> "Program":
-    """The program random-walk MH runs: `prog`, or its affine-loc terms as
-    expression terms (affine_as_expressions) when that moves MH from the
-    tape (k_mh) onto the sliced kernel k_mh_sl (value-only LS_EXPR pass)."""
+    """The program random-walk MH runs: `prog`, or its affine-loc (and then
+    non-own scalar) terms as expression terms (affine_as_expressions) when
+    that moves MH from the tape (k_mh) onto the sliced kernel k_mh_sl
+    (value-only LS_EXPR pass)."""
     lib = _lib.load()
     if lib.mc_program_mh_sliced(prog.handle) == 1:
         return prog
-    try:
-        alt = affine_as_expressions(prog.model)
-    except TraceError:
-        return prog
-    if alt is None:
-        return prog
-    p2 = Program(alt)
-    return p2 if lib.mc_program_mh_sliced(p2.handle) == 1 else prog
+    for scalars in (False, True):
+        try:
+            alt = affine_as_expressions(prog.model, scalars)
+        except TraceError:
+            continue
+        if alt is None:
+            continue
+        p2 = Program(alt)
+        if lib.mc_program_mh_sliced(p2.handle) == 1:
+            return p2
+    return prog
 
 
 def compile_model(log_prob_fn, initial_params: dict, slices: int = 0,

@@ -156,13 +156,16 @@ def test_expr_lanes_nuts_matches_oracle(gpu, model, eps, seed):
     assert np.all(info2.mean_tree_depth >= 1)
 
 
-def test_affine_regression_nuts_runs_sliced(gpu):
+@pytest.mark.parametrize("model", ["linear_regression", "linear_regression_exp"])
+def test_affine_regression_nuts_runs_sliced(gpu, model):
     """NUTS on a linear regression at N = 100 K: its fused affine-loc term
     keeps k_nuts_lr / k_nuts_sl off and would run the tape (k_nuts); nuts()
     runs the same model with that term as an expression term
     (_trace.nuts_program) on the sliced kernel instead.  Trees identical to
     the oracle's for >= 6 iterations on two chains at a fixed step size, the
-    draws before the first difference within rtol 1e-3 (as above)."""
+    draws before the first difference within rtol 1e-3 (as above).
+    linear_regression_exp: sigma ~ Exponential(1), a scalar term the sliced
+    kernels cannot take as an own prior, rebuilt as an expression term too."""
     import mlx_mcmc_amd as m
     from mlx_mcmc_amd import _trace
 
@@ -170,8 +173,8 @@ def test_affine_regression_nuts_runs_sliced(gpu):
     b, a = np.polyfit(x.astype(np.float64), y.astype(np.float64), 1)
     sd = float(np.std(y - (a + b * x)))
     start = {"a": np.float32(a), "b": np.float32(b), "sigma": np.float32(sd)}
-    lp, _ = W.linear_regression(W.ns_product(), N)
-    olp, _ = W.linear_regression(W.ns_oracle(), N)
+    lp, _ = getattr(W, model)(W.ns_product(), N)
+    olp, _ = getattr(W, model)(W.ns_oracle(), N)
     prog = _trace.compile_model(lp, start)
     assert prog.model.n_affines == 1 and prog.nuts_kernel(10) == "tape"
     alt = _trace.nuts_program(prog, 10)
@@ -192,7 +195,7 @@ def test_affine_regression_nuts_runs_sliced(gpu):
                     or tr["n_leapfrog"][c][i] != ref.trace["leaves"][i]):
                 break
             same += 1
-        print(f"affine regression NUTS chain {c}: trees identical for {same} of {n}, depths "
+        print(f"{model} NUTS chain {c}: trees identical for {same} of {n}, depths "
               f"{list(ref.trace['depth'][:same])}")
         assert same >= 6, f"chain {c}: trees differ at iteration {same}"
         ns = max(0, same - kw["num_warmup"])
@@ -240,7 +243,8 @@ def test_expr_lanes_mh_matches_oracle(gpu, model, scale, seed):
                                atol=1e-6)
 
 
-def test_affine_regression_mh_runs_sliced(gpu):
+@pytest.mark.parametrize("model", ["linear_regression", "linear_regression_exp"])
+def test_affine_regression_mh_runs_sliced(gpu, model):
     """Random-walk MH on the N = 100 K linear regression: the fused affine
     term keeps k_mh_sl off; metropolis_hastings() runs the model with it as an
     expression term (_trace.mh_program) on the sliced kernel.  Decisions equal
@@ -254,12 +258,13 @@ def test_affine_regression_mh_runs_sliced(gpu):
     b, a = np.polyfit(x.astype(np.float64), y.astype(np.float64), 1)
     sd = float(np.std(y - (a + b * x)))
     start = {"a": np.float32(a), "b": np.float32(b), "sigma": np.float32(sd)}
-    lp, _ = W.linear_regression(W.ns_product(), N)
-    olp, _ = W.linear_regression(W.ns_oracle(), N)
+    lp, _ = getattr(W, model)(W.ns_product(), N)
+    olp, _ = getattr(W, model)(W.ns_oracle(), N)
     lib = _lib.load()
     prog = _trace.compile_model(lp, start)
     assert lib.mc_program_mh_sliced(prog.handle) == 0
-    assert lib.mc_program_mh_sliced(_trace.mh_program(prog).handle) == 1
+    mp = _trace.mh_program(prog)  # (kept alive while its handle is queried)
+    assert lib.mc_program_mh_sliced(mp.handle) == 1
     n, scale, seed = 60, 2e-3, 42
     s, rate, info = m.metropolis_hastings(lp, start, num_samples=n, proposal_scale=scale,
                                           random_seed=seed, return_info=True,
@@ -271,7 +276,7 @@ def test_affine_regression_mh_runs_sliced(gpu):
     assert 0 < racc.sum() < n, "mixed decisions"
     flips = np.nonzero(acc != racc)[0]
     same = int(flips[0]) if flips.size else n
-    print(f"affine regression MH: decisions identical for {same} of {n}")
+    print(f"{model} MH: decisions identical for {same} of {n}")
     if same < n:
         lu = log_u(m.random.key(seed).seed, 0, n)
         tie = tie_bound(ref.trace["logp"][same])

@@ -281,6 +281,20 @@ def linear_regression(ns, n=1000):
     return log_prob, {"a": np.float32(0.0), "b": np.float32(0.0), "sigma": np.float32(1.0)}
 
 
+def linear_regression_exp(ns, n=1000):
+    """The linear regression with an Exponential(1) prior on the noise scale
+    (a scalar term the sliced kernels cannot take as an own prior)."""
+    x, y = regression_data(n)
+
+    def log_prob(params):
+        a, b, sigma = params["a"], params["b"], params["sigma"]
+        lp = ns.Normal(0, 10).log_prob(a) + ns.Normal(0, 10).log_prob(b)
+        lp = lp + ns.Exponential(1.0).log_prob(sigma)
+        return lp + ns.sum(ns.Normal(a + b * ns.array(x), sigma).log_prob(ns.array(y)))
+
+    return log_prob, {"a": np.float32(0.0), "b": np.float32(0.0), "sigma": np.float32(1.0)}
+
+
 def varying_intercept_data(G=20, N=2000, seed=4):
     rng = np.random.default_rng(seed)
     group = np.sort(rng.integers(0, G, N)).astype(np.int32)
