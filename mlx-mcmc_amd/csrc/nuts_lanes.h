@@ -34,6 +34,11 @@ namespace mc {
 __host__ __device__ constexpr int64_t nuts_lr_arena_floats(int rs, int max_depth) {
     return (2 * (int64_t)(max_depth + 1) + 2 * (int64_t)(max_depth + 2)) * (rs + 1) * 64;
 }
+// k_nuts_lr's draw wave (PW): two buffers of 2^max_depth merge draws and 33
+// flag words after the arena
+__host__ __device__ constexpr int64_t nuts_lr_draw_words(int max_depth) {
+    return 2 * ((int64_t)1 << max_depth) + 36;
+}
 
 // SPEC 1: every slice term has a specialised form (no LS_GENERIC term) and
 // every scalar term is an own prior (the planner checks it): the generic
@@ -44,14 +49,21 @@ __host__ __device__ constexpr int64_t nuts_lr_arena_floats(int rs, int max_depth
 // (lane, slot) — a data-scale term (config 5's theta_i ~ N(0, s_i)) or a
 // direct term with constant loc and scale (theta_i ~ N(m, s)): the gradient
 // is that term's arithmetic on per-slot registers, nothing else is compiled.
-template <int RS, int NSH, int SPEC>
-__global__ void __launch_bounds__(64)
+// PW (draw wave): the workgroup's second wave computes the tree merges'
+// Philox draws ahead into LDS (nuts_lr_draw_words: two iteration buffers of
+// 2^MAXJ words and the flags), the chain's wave reads each with one LDS
+// load instead of a scalar Philox (~100 SALU) in its leaf's issue stream.
+// The same draws, so the same trees.
+template <int RS, int NSH, int SPEC, bool PW = false>
+__global__ void __launch_bounds__(PW ? 128 : 64)
 k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, float* samples,
           TraceDev tr) {
     static_assert(NSH <= kLrMaxShared, "shared parameters");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const mc_run_config& cfg = A.cfg;
-    const int j = threadIdx.x;  // lane
+    const int j = threadIdx.x & 63;  // lane
+    // (PW: wave 1 is the draw wave)
+    const int wv = PW ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
     const int64_t c = blockIdx.x;
     if (c >= cfg.num_chains) return;
     constexpr bool REG = SPEC == 2;
@@ -67,13 +79,57 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
     const int nsweep = (int)(blk[3] & 255);
     const int ndirect = (int)((blk[3] >> 8) & 255);
     const int nfast = nsweep + ndirect;
-    for (int i = j; 4 * i < dlen; i += 64)
-        *(float4*)(sd + 4 * i) = *(const float4*)(P.data + doff + 4 * i);
+    if (wv == 0)
+        for (int i = j; 4 * i < dlen; i += 64)
+            *(float4*)(sd + 4 * i) = *(const float4*)(P.data + doff + 4 * i);
     LrSterm* sst = (LrSterm*)(smem + P.sdata_floats);
     const int sterm_floats = P.n_sterms * (int)(sizeof(LrSterm) / 4);
-    for (int i = j; i < sterm_floats / 4; i += 64) ((float4*)sst)[i] = ((const float4*)P.sterms)[i];
+    if (wv == 0)
+        for (int i = j; i < sterm_floats / 4; i += 64)
+            ((float4*)sst)[i] = ((const float4*)P.sterms)[i];
     float* ar = smem + P.sdata_floats + sterm_floats;  // the arena (16-byte aligned)
+    // PW: the draw buffers and flags after the arena (flags: ready[2][16]
+    // (iteration + 1 whose depth-jd draws are in buffer b), then the number
+    // of iterations the chain's wave has completed)
+    uint32_t* dbufs = (uint32_t*)(ar + nuts_lr_arena_floats(RS, MAXJ));
+    int* dflags = (int*)(dbufs + 2 * (1 << MAXJ));
+    if (PW && wv == 1 && j < 33) dflags[j] = 0;
     __syncthreads();
+    if constexpr (PW) {
+        if (wv == 1) {  // ---- the draw wave --------------------------------------
+            const uint32_t cid = (uint32_t)(cfg.chain_offset + c);
+            const int64_t it0 = cfg.iter_begin, it1 = cfg.iter_begin + cfg.iter_count;
+            for (int64_t it = it0; it < it1; ++it) {
+                const int rel = (int)(it - it0), b = rel & 1;
+                // buffer b was iteration rel - 2's: wait until the chain's wave
+                // has completed it
+                while (__hip_atomic_load(dflags + 32, __ATOMIC_ACQUIRE,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP) < rel - 1)
+                    __builtin_amdgcn_s_sleep(2);
+                uint32_t* buf = dbufs + b * (1 << MAXJ);
+                for (int jd = 1; jd < MAXJ; ++jd) {
+                    // the level-l merge at leaf k, (k + 1) a multiple of
+                    // 2^(l+1), is word (2^jd - 1) + (2^jd - 2^(jd-l)) + m,
+                    // m = (k + 1) / 2^(l+1) - 1 (the chain's wave reads it so)
+                    const int cnt = (1 << jd) - 1;
+                    for (int i0 = 0; i0 < cnt; i0 += 64) {
+                        const int idx = i0 + j;
+                        if (idx < cnt) {
+                            int l = 0;
+                            while (idx >= (1 << jd) - (1 << (jd - l - 1))) ++l;
+                            const int m = idx - ((1 << jd) - (1 << (jd - l)));
+                            const uint32_t k = (uint32_t)(((m + 1) << (l + 1)) - 1);
+                            buf[cnt + idx] = mc_draw(cfg.seed, cid, (uint32_t)it, MC_RNG_TAG_MERGE,
+                                                     (uint32_t)jd, ((uint32_t)l << 20) | k).x;
+                        }
+                    }
+                    __hip_atomic_store(dflags + b * 16 + jd, rel + 1, __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            return;
+        }
+    }
 
     // arena addressing: slot s of kind 0 (first: q, r) or 1 (pool: q, g),
     // component comp, register slot r (RS: the shared value)
@@ -500,6 +556,19 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
         while (s && jd < MAXJ) {
             const mc_u32x4 rd = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_DEPTH,
                                         (uint32_t)jd, 0);
+            // PW: this depth's merge draws (the draw wave's buffer for this
+            // iteration; it runs ahead, so this rarely waits)
+            const uint32_t* dbuf = dbufs + ((int)(it - cfg.iter_begin) & 1) * (1 << MAXJ) +
+                                   ((1 << jd) - 1);
+            if constexpr (PW) {
+                if (jd >= 1) {
+                    const int want = (int)(it - cfg.iter_begin) + 1;
+                    const int* fl = dflags + ((int)(it - cfg.iter_begin) & 1) * 16 + jd;
+                    while (__hip_atomic_load(fl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) !=
+                           want)
+                        __builtin_amdgcn_s_sleep(1);
+                }
+            }
             const int v = (mc_u01_f32(rd.x) < 0.5f) ? 1 : -1;
             const double ve = (double)v * eps;
             const float h = (float)(0.5 * ve);
@@ -542,8 +611,10 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                 // the leaf's dependency stalls; in the merge it was on the
                 // critical path)
                 uint32_t u0 = 0;
-                if (k & 1) u0 = mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_MERGE,
-                                        (uint32_t)jd, (uint32_t)k).x;
+                if (k & 1)
+                    u0 = PW ? __builtin_amdgcn_readfirstlane(dbuf[((k + 1) >> 1) - 1])
+                            : mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_MERGE,
+                                      (uint32_t)jd, (uint32_t)k).x;
                 // leaf: leapfrog_step(theta, r, v*eps) + hamiltonian (nuts.py:160-164)
                 // (both packed halves in one instruction each: the same IEEE
                 // operations as the per-half form)
@@ -653,6 +724,8 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
                     const int pn = __builtin_amdgcn_readlane(pend_n, l);
                     const uint32_t ux =
                         l == 0 ? u0
+                        : PW   ? __builtin_amdgcn_readfirstlane(
+                                   dbuf[((1 << jd) - (1 << (jd - l))) + ((k + 1) >> (l + 1)) - 1])
                                : mc_draw(cfg.seed, chain_id, (uint32_t)it, MC_RNG_TAG_MERGE,
                                          (uint32_t)jd, ((uint32_t)l << 20) | (uint32_t)k).x;
                     const double den = (double)(pn + cn) > 1.0 ? (double)(pn + cn) : 1.0;
@@ -793,6 +866,9 @@ k_nuts_lr(LrCtx P, RunArgs A, mc_chain_scalars* scal, float* st_q, float* st_g, 
             }
         }
         MC_STAMP(15);
+        if constexpr (PW)  // (the draw wave may now refill this iteration's buffer)
+            __hip_atomic_store(dflags + 32, (int)(it - cfg.iter_begin) + 1, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     MC_STAMP_FLUSH
 

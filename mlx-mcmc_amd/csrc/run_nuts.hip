@@ -130,6 +130,16 @@ extern "C" int mc_debug_nuts_sliced(int on) {
     return MC_OK;
 }
 
+// k_nuts_lr's draw wave for the register-only variant: MC_NUTS_DRAW_WAVE=0 in
+// the environment keeps one wave per chain (A/B)
+static bool nuts_draw_wave_enabled() {
+    static const int on = [] {
+        const char* e = std::getenv("MC_NUTS_DRAW_WAVE");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    return on == 1;
+}
+
 static int g_nuts_variant = -1;  // mc_debug_nuts_variant
 extern "C" int mc_debug_nuts_variant(int variant) {
     g_nuts_variant = (variant < -1 || variant > 1) ? -1 : variant;
@@ -145,13 +155,24 @@ static int launch_nuts_lr(const mc_program* p, const mc_run_config* cfg, void* s
     RunArgs A;
     std::memset(&A, 0, sizeof(A));
     A.cfg = *cfg;
-    const size_t lds = nuts_lr_lds_bytes(p, cfg->max_tree_depth);
+    size_t lds = nuts_lr_lds_bytes(p, cfg->max_tree_depth);
     auto kern = lanes_specialised(p) ? k_nuts_lr<RS, NSH, 1> : k_nuts_lr<RS, NSH, 0>;
+    int threads = 64;
     if constexpr (NSH == 3)
-        if (lanes_register_only(p) && g_nuts_variant < 0) kern = k_nuts_lr<RS, NSH, 2>;
+        if (lanes_register_only(p) && g_nuts_variant < 0) {
+            kern = k_nuts_lr<RS, NSH, 2>;
+            // the draw wave (nuts_lanes.h PW) when its buffers fit
+            const size_t lds_pw = lds + (size_t)nuts_lr_draw_words(cfg->max_tree_depth) * 4;
+            if (nuts_draw_wave_enabled() && cfg->max_tree_depth <= 12 &&
+                lds_pw <= (size_t)kSlLdsBudget) {
+                kern = k_nuts_lr<RS, NSH, 2, true>;
+                lds = lds_pw;
+                threads = 128;
+            }
+        }
     if (g_nuts_variant == 0) kern = k_nuts_lr<RS, NSH, 0>;
     MC_HIP_TRY(allow_lds(kern, lds));
-    hipLaunchKernelGGL(kern, dim3((unsigned)cfg->num_chains), dim3(64), lds, st, lrctx_of(p), A,
+    hipLaunchKernelGGL(kern, dim3((unsigned)cfg->num_chains), dim3(threads), lds, st, lrctx_of(p), A,
                        (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples,
                        trace_of(tr));
     MC_HIP_TRY(hipGetLastError());
