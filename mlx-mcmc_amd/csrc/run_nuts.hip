@@ -156,21 +156,18 @@ static int launch_nuts_lr(const mc_program* p, const mc_run_config* cfg, void* s
     std::memset(&A, 0, sizeof(A));
     A.cfg = *cfg;
     size_t lds = nuts_lr_lds_bytes(p, cfg->max_tree_depth);
-    auto kern = lanes_specialised(p) ? k_nuts_lr<RS, NSH, 1> : k_nuts_lr<RS, NSH, 0>;
-    int threads = 64;
+    // the draw wave (nuts_lanes.h PW) when its buffers fit
+    const size_t lds_pw = lds + (size_t)nuts_lr_draw_words(cfg->max_tree_depth) * 4;
+    const bool pw = nuts_draw_wave_enabled() && cfg->max_tree_depth <= 12 &&
+                    lds_pw <= (size_t)kSlLdsBudget;
+    auto kern = lanes_specialised(p) ? (pw ? k_nuts_lr<RS, NSH, 1, true> : k_nuts_lr<RS, NSH, 1>)
+                                     : (pw ? k_nuts_lr<RS, NSH, 0, true> : k_nuts_lr<RS, NSH, 0>);
     if constexpr (NSH == 3)
-        if (lanes_register_only(p) && g_nuts_variant < 0) {
-            kern = k_nuts_lr<RS, NSH, 2>;
-            // the draw wave (nuts_lanes.h PW) when its buffers fit
-            const size_t lds_pw = lds + (size_t)nuts_lr_draw_words(cfg->max_tree_depth) * 4;
-            if (nuts_draw_wave_enabled() && cfg->max_tree_depth <= 12 &&
-                lds_pw <= (size_t)kSlLdsBudget) {
-                kern = k_nuts_lr<RS, NSH, 2, true>;
-                lds = lds_pw;
-                threads = 128;
-            }
-        }
-    if (g_nuts_variant == 0) kern = k_nuts_lr<RS, NSH, 0>;
+        if (lanes_register_only(p) && g_nuts_variant < 0)
+            kern = pw ? k_nuts_lr<RS, NSH, 2, true> : k_nuts_lr<RS, NSH, 2>;
+    if (g_nuts_variant == 0) kern = pw ? k_nuts_lr<RS, NSH, 0, true> : k_nuts_lr<RS, NSH, 0>;
+    if (pw) lds = lds_pw;
+    const int threads = pw ? 128 : 64;
     MC_HIP_TRY(allow_lds(kern, lds));
     hipLaunchKernelGGL(kern, dim3((unsigned)cfg->num_chains), dim3(threads), lds, st, lrctx_of(p), A,
                        (mc_chain_scalars*)b, (float*)(b + qo), (float*)(b + go), samples,
