@@ -1440,7 +1440,10 @@ def nuts_program(prog: "Program", max_tree_depth: int = 10) -> "Program":
         if alt is None:
             continue
         p2 = Program(alt)
-        if p2.nuts_kernel(max_tree_depth) == "sliced":
+        # (the sliced kernel runs expression terms compiled: with the JIT off
+        # they would run interpreted on the tape, slower than the fused terms)
+        if p2.nuts_kernel(max_tree_depth) == "sliced" and _lib.load().mc_program_expr_jit(
+                p2.handle) == 1:
             return p2
     return prog
 
@@ -1461,7 +1464,7 @@ def mh_program(prog: "Program") -> "Program":
         if alt is None:
             continue
         p2 = Program(alt)
-        if lib.mc_program_mh_sliced(p2.handle) == 1:
+        if lib.mc_program_mh_sliced(p2.handle) == 1 and lib.mc_program_expr_jit(p2.handle) == 1:
             return p2
     return prog
 

@@ -167,7 +167,7 @@ def test_affine_regression_nuts_runs_sliced(gpu, model):
     linear_regression_exp: sigma ~ Exponential(1), a scalar term the sliced
     kernels cannot take as an own prior, rebuilt as an expression term too."""
     import mlx_mcmc_amd as m
-    from mlx_mcmc_amd import _trace
+    from mlx_mcmc_amd import _lib, _trace
 
     x, y = W.regression_data(N)
     b, a = np.polyfit(x.astype(np.float64), y.astype(np.float64), 1)
@@ -179,6 +179,13 @@ def test_affine_regression_nuts_runs_sliced(gpu, model):
     assert prog.model.n_affines == 1 and prog.nuts_kernel(10) == "tape"
     alt = _trace.nuts_program(prog, 10)
     assert alt is not prog and alt.nuts_kernel(10) == "sliced"
+    # with the JIT off the expression form would run interpreted: kept fused
+    lib = _lib.load()
+    lib.mc_debug_expr_jit(0)
+    try:
+        assert _trace.nuts_program(prog, 10) is prog
+    finally:
+        lib.mc_debug_expr_jit(-1)
     kw = dict(num_samples=8, num_warmup=4, step_size=2e-3, max_tree_depth=10,
               adapt_step_size=False)
     s, rate, info = m.nuts(lp, start, key=m.random.key(41), num_chains=8, progress=False,
